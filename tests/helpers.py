@@ -1,0 +1,79 @@
+"""Shared input generators for the parity tests (mirrors the reference tests'
+ray layouts, src/emitters/tests/test_sunsky.py)."""
+import numpy as np
+
+SPECIAL_ALBEDO = {  # test_sunsky.py:12-16
+    "type": "irregular",
+    "wavelengths": "320, 360, 400, 440, 480, 520, 560, 600, 640, 680, 720",
+    "values": "0.56, 0.21, 0.58, 0.24, 0.92, 0.42, 0.53, 0.75, 0.54, 0.20, 0.46",
+}
+EXR_WAVELENGTHS = [360 + (830 - 360) / 10 / 2 + i * (830 - 360) / 10 for i in range(10)]  # :88-90
+
+
+def exr_grid_wi(res=(32, 64)):
+    """si.wi of generate_and_compare (test_sunsky.py:93-100): NOT negated."""
+    phis, thetas = np.meshgrid(np.linspace(0, 2 * np.pi, res[1], dtype=np.float32),
+                               np.linspace(np.pi, 0, res[0], dtype=np.float32))
+    phis, thetas = phis.ravel(), thetas.ravel()
+    return np.stack([np.cos(phis) * np.sin(thetas), np.sin(phis) * np.sin(thetas), np.cos(thetas)],
+                    1).astype(np.float32)
+
+
+def angles_dict(turb, sun_phi, sun_theta, albedo, sky_scale, sun_scale, **kw):
+    """make_emitter_angles (test_sunsky.py:28-39)."""
+    d = {"type": "sunsky",
+         "sun_direction": [float(np.cos(sun_phi) * np.sin(sun_theta)),
+                           float(np.sin(sun_phi) * np.sin(sun_theta)), float(np.cos(sun_theta))],
+         "sun_scale": sun_scale, "sky_scale": sky_scale, "turbidity": turb, "albedo": albedo}
+    d.update(kw)
+    return d
+
+
+def hour_dict(turb, hour, albedo, sky_scale, sun_scale):
+    """make_emitter_hour (test_sunsky.py:18-26)."""
+    return {"type": "sunsky", "hour": hour, "sun_scale": sun_scale, "sky_scale": sky_scale,
+            "turbidity": turb, "albedo": albedo}
+
+
+def hemisphere_wo(n, seed=0):
+    """Uniform upper-hemisphere directions (cos theta = u1, phi = 2 pi u2), SURVEY.md §8d C2."""
+    rng = np.random.default_rng(seed)
+    u1 = rng.random(n, dtype=np.float32)
+    u2 = rng.random(n, dtype=np.float32)
+    ct = u1
+    st = np.sqrt(np.maximum(0, 1 - ct * ct))
+    ph = np.float32(2 * np.pi) * u2
+    return np.stack([st * np.cos(ph), st * np.sin(ph), ct], 1).astype(np.float32)
+
+
+def sphere_wo(n, seed=0):
+    rng = np.random.default_rng(seed)
+    v = rng.standard_normal((n, 3)).astype(np.float32)
+    return (v / np.linalg.norm(v, axis=1, keepdims=True)).astype(np.float32)
+
+
+def sun_cone_wo(n, sun_dir, half_aperture, seed=0, scale=1.0):
+    """Directions inside (scale<1) / around the sun cone, for sun-disc coverage."""
+    rng = np.random.default_rng(seed)
+    s = np.asarray(sun_dir, dtype=np.float64)
+    s = s / np.linalg.norm(s)
+    a = np.array([1.0, 0, 0]) if abs(s[0]) < 0.9 else np.array([0, 1.0, 0])
+    t1 = np.cross(s, a)
+    t1 /= np.linalg.norm(t1)
+    t2 = np.cross(s, t1)
+    g = half_aperture * scale * np.sqrt(rng.random(n))
+    ph = 2 * np.pi * rng.random(n)
+    d = (np.cos(g)[:, None] * s + np.sin(g)[:, None] * (np.cos(ph)[:, None] * t1 + np.sin(ph)[:, None] * t2))
+    return d.astype(np.float32)
+
+
+def mean_rel(x, ref, eps):
+    return float(np.mean(np.abs(x - ref) / (np.abs(ref) + eps)))
+
+
+def max_rel(x, ref, floor_frac=1e-6):
+    """max |x-ref| / max(|ref|, floor_frac * max|ref|)   (SURVEY.md §8d parity metric)."""
+    x = np.asarray(x, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    floor = floor_frac * max(np.abs(ref).max(), 1e-30)
+    return float(np.max(np.abs(x - ref) / np.maximum(np.abs(ref), floor)))

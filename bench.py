@@ -1,0 +1,296 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X sun/sky emitter hot path (BASELINE.json north_star).
+
+Headline (config 2 of BASELINE.json): RGB eval() of 16,777,216 uniform
+upper-hemisphere directions per GPU, turbidity in {2, 6, 10} (sun at 45 deg
+elevation, albedo 0.1).  One "step" = one eval pass over the batch for each of
+the three turbidities = 3 x 16,777,216 direction evals.  Inputs are resident
+in HBM before the timed region; outputs are written to HBM.
+
+Secondary lines (reported under "secondary", not in `value`): config 3
+(spectral eval, 16M dirs x the 11 model wavelengths, broadcast) and config 4
+(sample_direction + pdf_direction on 64M samples).
+
+Multi-GPU (torchrun, one process per GPU): every rank evaluates its own
+16M-direction shard -- weak scaling, no data-path collective.  `--gather`
+additionally times the RCCL gather of the radiance buffer to rank 0 (reported
+separately; never part of `value`).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mitsuba3-sunsky_amd"))
+import sunsky_amd as ss  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+N_DIRS = 1 << 24          # 16,777,216 (BASELINE.json configs[1])
+TURBIDITIES = (2.0, 6.0, 10.0)
+BYTES_RGB = 24            # 12 B wi + 12 B RGB per direction
+BYTES_SPEC_PER_DIR = 12 + 11 * 4
+BYTES_SAMPLE = 52
+
+
+def sun_dict(turb, eta_deg=45.0, albedo=0.1, phi=0.0):
+    th = np.deg2rad(90.0 - eta_deg)
+    return {"type": "sunsky", "turbidity": turb, "albedo": albedo,
+            "sun_direction": [float(np.cos(phi) * np.sin(th)), float(np.sin(phi) * np.sin(th)), float(np.cos(th))]}
+
+
+def hemisphere_dirs(n, seed, device):
+    """cos(theta) = u1, phi = 2 pi u2, SoA (3, n) fp32 on device."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    u = torch.rand((2, n), generator=g, device=device, dtype=torch.float32)
+    ct = u[0]
+    st = torch.sqrt(torch.clamp(1 - ct * ct, min=0))
+    ph = 2 * np.pi * u[1]
+    return torch.stack([st * torch.cos(ph), st * torch.sin(ph), ct]).contiguous()
+
+
+class KernelTimer:
+    """HIP events on the stream the C ABI launches on (torch's current stream)."""
+
+    def __init__(self):
+        self.pairs = []
+
+    def start(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def stop(self, s):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.pairs.append((s, e))
+
+    def mean_ms(self):
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else float("nan")
+
+
+def pmc_traffic(path, kernel_prefix):
+    """HBM bytes per launch from a rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE CSV pair
+    (MI355X_MICROARCH.md §HBM: FETCH_SIZE reads 1/2 of a wide streaming read on gfx950)."""
+    try:
+        import csv
+        fetch, write = [], []
+        for f in path.split(","):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if not row.get("Kernel_Name", "").startswith(kernel_prefix):
+                        continue
+                    name, val = row.get("Counter_Name"), float(row.get("Counter_Value", "nan"))
+                    if name == "FETCH_SIZE":
+                        fetch.append(val)
+                    elif name == "WRITE_SIZE":
+                        write.append(val)
+        if fetch and write:
+            return (2.0 * np.mean(fetch) + np.mean(write)) * 1024.0
+    except Exception:
+        pass
+    return None
+
+
+def cpu_baseline(wi_host, budget_s=12.0):
+    """The oracle (fp32 restatement, OpenMP) timed on this host's cores on a
+    bounded sample of the headline workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    threads = min(threads, 16)
+    O.set_threads(threads)
+    oracles = [O.Oracle(sun_dict(t), "rgb", "jit", "f32") for t in TURBIDITIES]
+    n_sample = min(wi_host.shape[0], 1 << 22)
+    sample = np.ascontiguousarray(wi_host[:n_sample])
+    oracles[0].eval(sample[:4096])   # warm
+    done, t0 = 0, time.perf_counter()
+    while True:
+        for o in oracles:
+            o.eval(sample)
+            done += n_sample
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "dir-evals/s", "cores": threads, "kind": "port",
+            "sample": f"{done} RGB evals ({n_sample} of the headline directions x T in {{2,6,10}}, "
+                      f"repeated for >= {budget_s:.0f}s), oracle/sunsky_oracle.c fp32, {threads} OpenMP threads"}
+
+
+def parity_check(ems, wi, outs, n_check=1 << 20):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    max_abs, max_rel = 0.0, 0.0
+    wi_h = wi[:, :n_check].T.cpu().numpy()
+    for t, out in zip(TURBIDITIES, outs):
+        ref = O.Oracle(sun_dict(t), "rgb", "jit", "f32").eval(wi_h)
+        got = out[:, :n_check].T.cpu().numpy()
+        # sun-disc lanes are ill-conditioned in fp32 (tests/test_gpu_parity.py); exclude them here
+        s = np.array(sun_dict(t)["sun_direction"], np.float32)
+        sky = (-wi_h @ s) < np.cos(np.deg2rad(0.5358 / 2)) - 1e-6
+        d = np.abs(got[sky] - ref[sky]).astype(np.float64)
+        max_abs = max(max_abs, float(d.max()))
+        floor = 1e-6 * np.abs(ref[sky]).max()
+        max_rel = max(max_rel, float((d / np.maximum(np.abs(ref[sky]), floor)).max()))
+    return max_abs, max_rel
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=N_DIRS, help="directions per GPU")
+    ap.add_argument("--precision", default=os.environ.get("SUNSKY_BENCH_PRECISION", "fast"))
+    ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--gather", action="store_true", help="also time an RCCL gather of the radiance to rank 0")
+    ap.add_argument("--pmc", default=os.environ.get("SUNSKY_PMC_CSV"), help="rocprofv3 --pmc CSV(s) for traffic")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    n = args.n
+    wi = -hemisphere_dirs(n, seed=1234 + rank, device=dev)     # si.wi = -wo
+    ems = [ss.SunskyEmitter(sun_dict(t), "rgb", precision=args.precision, device=dev) for t in TURBIDITIES]
+    outs = [torch.empty((3, n), dtype=torch.float32, device=dev) for _ in TURBIDITIES]
+    lib = ss.lib()
+    vin = ss._capi.Vec3In(wi[0].data_ptr(), wi[1].data_ptr(), wi[2].data_ptr())
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step(timer=None):
+        for em, out in zip(ems, outs):
+            s = timer.start() if timer else None
+            rc = lib.sunsky_eval(em._h, vin, None, 0, 0, None, n, out.data_ptr(), n, stream)
+            if rc:
+                raise RuntimeError(lib.sunsky_last_error().decode())
+            if timer:
+                timer.stop(s)
+
+    for _ in range(args.warmup):
+        step()
+    timer = KernelTimer()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timer)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = timer.mean_ms()
+    evals_per_step = len(TURBIDITIES) * n
+    value = evals_per_step * world * args.steps / elapsed
+
+    result = None
+    if rank == 0:
+        achieved = BYTES_RGB * n / (kernel_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(args.pmc, "sunsky_eval_rgb_v4") if args.pmc else None
+        max_abs, max_rel = parity_check(ems, wi, outs)
+        result = {
+            "metric": "sky-radiance evals/sec (ray-dir x lambda)", "value": value, "unit": "evals/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "RGB eval(): 16,777,216 uniform upper-hemisphere dirs per GPU x turbidity {2,6,10}",
+                       "dirs_per_gpu": n, "turbidity": list(TURBIDITIES), "sun_elevation_deg": 45,
+                       "albedo": 0.1, "precision": args.precision, "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": traffic / 1.0 if traffic else None,
+                         "kernel": "sunsky_eval_rgb_v4_" + args.precision[:4].replace("refe", "ref"),
+                         "kernel_ms": kernel_ms, "bytes_per_launch": BYTES_RGB * n},
+            "parity": {"max_abs_delta_vs_oracle_f32": max_abs, "max_rel_delta_vs_oracle_f32": max_rel,
+                       "checked_dirs": min(n, 1 << 20) * len(TURBIDITIES), "sun_disc_lanes": "excluded"},
+        }
+
+    # ---------------------------------------------------------------- secondary
+    if not args.no_secondary:
+        sec = {}
+        # C3: spectral eval, 11 model wavelengths broadcast
+        spec = ss.SunskyEmitter(dict(sun_dict(3.0), albedo=0.3), "spectral", precision=args.precision, device=dev)
+        lams = [float(x) for x in range(320, 721, 40)]
+        spec_out = torch.empty((11, n), dtype=torch.float32, device=dev)
+        for _ in range(2):
+            spec.eval_spectral_broadcast(wi, lams, out=spec_out)
+        tm = KernelTimer()
+        for _ in range(max(3, args.steps // 4)):
+            s = tm.start()
+            spec.eval_spectral_broadcast(wi, lams, out=spec_out)
+            tm.stop(s)
+        ms = tm.mean_ms()
+        sec["spectral_eval_C3"] = {"evals_per_s": 11 * n / (ms * 1e-3), "kernel_ms": ms,
+                                   "achieved_GBps": BYTES_SPEC_PER_DIR * n / (ms * 1e-3) / 1e9,
+                                   "unit": "(dir x lambda) evals/s"}
+        del spec_out
+        # C4: sample_direction + pdf_direction, 64M samples (per GPU)
+        ns = 4 * n
+        smp = ss.SunskyEmitter(dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), "rgb", precision=args.precision,
+                               device=dev)
+        g = torch.Generator(device=dev)
+        g.manual_seed(99 + rank)
+        u = torch.rand((2, ns), generator=g, device=dev)
+        it = ss.Interaction3f()
+        for _ in range(2):
+            ds, w = smp.sample_direction(it, u)
+            pdf = smp.pdf_direction(it, ds)
+        tm = KernelTimer()
+        for _ in range(max(3, args.steps // 4)):
+            s = tm.start()
+            ds, w = smp.sample_direction(it, u)
+            pdf = smp.pdf_direction(it, ds)
+            tm.stop(s)
+        ms = tm.mean_ms()
+        sec["sampling_C4"] = {"samples_per_s": ns / (ms * 1e-3), "ms": ms, "samples": ns,
+                              "achieved_GBps": BYTES_SAMPLE * ns / (ms * 1e-3) / 1e9,
+                              "note": "sample_direction (writes d, pdf, dist, p, RGB weight) + pdf_direction"}
+        del u, ds, w, pdf
+        if rank == 0:
+            result["secondary"] = sec
+
+    # ----------------------------------------------------------- optional gather
+    if args.gather and world > 1:
+        buf = outs[0]
+        gl = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        dist.gather(buf, gl, dst=0)
+        torch.cuda.synchronize()
+        gt = time.perf_counter() - t0
+        if rank == 0:
+            result["gather"] = {"seconds": gt, "bytes_to_root": buf.numel() * 4 * (world - 1),
+                                "GBps": buf.numel() * 4 * (world - 1) / gt / 1e9}
+
+    if rank == 0:
+        if not args.no_cpu:
+            result["cpu_baseline"] = cpu_baseline(wi.T.cpu().numpy())
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,202 @@
+/*
+ * sunsky_amd.h -- C ABI of the MI355X-native sun/sky emitter.
+ *
+ * Drop-in replacement for the `sunsky` emitter plugin of
+ * matttsss/mitsuba3-sunsky (src/emitters/sunsky.cpp).  Each entry point names
+ * the reference interface it replaces (file:line under the reference tree).
+ * Conventions:
+ *   - every function returns an int status (SUNSKY_OK = 0); on failure the
+ *     thread-local message from sunsky_last_error() carries the reference's
+ *     error text (the reference throws through Log(Error, ...), logger.cpp:55-60);
+ *     nothing throws across this boundary;
+ *   - batch inputs/outputs are DEVICE pointers (HBM), structure-of-arrays,
+ *     one fp32 plane per component -- the layout Dr.Jit gives the JIT variants;
+ *     multi-channel outputs are planes at `out + c * out_stride`;
+ *   - `active` is an optional per-ray uint8 mask (NULL = all active), the
+ *     `Mask active` argument of the reference methods;
+ *   - `stream` is a hipStream_t (NULL = default stream); every batch call is
+ *     asynchronous and stream-ordered, allocates nothing and may be captured
+ *     into a hipGraph;
+ *   - create/update/destroy are host-synchronous and must not race batch calls
+ *     on the same emitter (the reference's parameters_changed() contract).
+ */
+#ifndef SUNSKY_AMD_H
+#define SUNSKY_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SUNSKY_AMD_ABI_VERSION 1
+
+typedef enum sunsky_status {
+    SUNSKY_OK = 0,
+    SUNSKY_ERROR_INVALID_VALUE = 1,   /* bad parameter (reference: Log(Error, ...))      */
+    SUNSKY_ERROR_FILE = 2,            /* dataset missing / unreadable (sunsky.h:519-520) */
+    SUNSKY_ERROR_FORMAT = 3,          /* dataset header / size mismatch (sunsky.h:531)   */
+    SUNSKY_ERROR_HIP = 4,             /* HIP runtime / code object failure               */
+    SUNSKY_ERROR_NOT_IMPLEMENTED = 5, /* sample_position (sunsky.cpp:483-495)            */
+    SUNSKY_ERROR_INTERNAL = 6
+} sunsky_status;
+
+typedef enum sunsky_variant {     /* mitsuba.conf variants: *_rgb / *_spectral */
+    SUNSKY_VARIANT_RGB = 0,
+    SUNSKY_VARIANT_SPECTRAL = 1
+} sunsky_variant;
+
+typedef enum sunsky_semantics {
+    SUNSKY_SEMANTICS_JIT = 0,     /* llvm_* / cuda_*: quadrature sky/sun ratio (sunsky.cpp:784-885) */
+    SUNSKY_SEMANTICS_SCALAR = 1   /* scalar_*: ratio 0.5, uniform wavelength pdf (:778-783)         */
+} sunsky_semantics;
+
+typedef enum sunsky_precision {
+    SUNSKY_PRECISION_FAST = 0,      /* host-folded transcendental constants (default) */
+    SUNSKY_PRECISION_REFERENCE = 1  /* reference operation order, full-precision libm */
+} sunsky_precision;
+
+typedef enum sunsky_table_id {      /* staged tables, for inspection / parity tests */
+    SUNSKY_TABLE_SKY_PARAMS = 0,    /* nch x 9  (m_sky_params)            */
+    SUNSKY_TABLE_SKY_RADIANCE = 1,  /* nch      (m_sky_radiance)          */
+    SUNSKY_TABLE_SUN_RADIANCE = 2,  /* 45x3x4x6 or 45x11x4 (m_sun_radiance) */
+    SUNSKY_TABLE_SUN_LD = 3,        /* 11 x 6   (m_sun_ld)                 */
+    SUNSKY_TABLE_GAUSSIANS = 4,     /* 20 x 5   (m_gaussians)              */
+    SUNSKY_TABLE_GAUSSIAN_CDF = 5,  /* 20       (DiscreteDistribution cdf) */
+    SUNSKY_TABLE_SPECTRAL_PDF = 6,  /* m_spectral_distr pdf                */
+    SUNSKY_TABLE_SPECTRAL_CDF = 7,  /* m_spectral_distr cdf                */
+    SUNSKY_TABLE_ALBEDO = 8         /* extract_albedo() result             */
+} sunsky_table_id;
+
+#define SUNSKY_FLAG_INFINITE 0x04u          /* EmitterFlags::Infinite (emitter.h:29-30) */
+#define SUNSKY_FLAG_SPATIALLY_VARYING 0x10u /* EmitterFlags::SpatiallyVarying (emitter.h:39-40) */
+
+typedef struct sunsky_props sunsky_props;
+typedef struct sunsky_emitter sunsky_emitter;
+
+typedef struct sunsky_vec3_in { const float *x, *y, *z; } sunsky_vec3_in;
+typedef struct sunsky_vec3_out { float *x, *y, *z; } sunsky_vec3_out;
+
+typedef struct sunsky_info {
+    int variant, semantics, nb_channels, active_record;
+    float turbidity, sky_scale, sun_scale;
+    float sun_half_aperture, cos_cutoff, area_ratio;
+    float sun_dir_world[3];       /* m_sun_dir                 */
+    float sun_dir_local[3];       /* m_local_sun_frame.n       */
+    float sun_angles[2];          /* m_sun_angles (phi, theta) */
+    float sky_sampling_w;         /* m_sky_sampling_w          */
+    float bsphere_center[3], bsphere_radius;
+    unsigned flags;               /* SUNSKY_FLAG_*             */
+    int device;                   /* HIP device owning the tables */
+    int precision;                /* sunsky_precision          */
+} sunsky_info;
+
+/* ------------------------------------------------------------ library */
+int sunsky_abi_version(void);
+const char *sunsky_last_error(void);
+
+/* --------------------------------------------------- property bag
+ * mitsuba::Properties as consumed by init_from_props (sunsky.cpp:889-948):
+ * "turbidity", "sky_scale", "sun_scale", "sun_aperture" (deg), "albedo"
+ * (float / per-channel spectrum / irregular spectrum), "sun_direction" (vector)
+ * XOR {"latitude","longitude","timezone","year","month","day","hour",
+ * "minute","second"}, "to_world" (4x4 row-major).  Unqueried names are an
+ * error at create time, like the XML/dict loader (src/core/xml.cpp:1085-1102). */
+int sunsky_props_create(sunsky_props **out);
+void sunsky_props_destroy(sunsky_props *p);
+int sunsky_props_set_float(sunsky_props *p, const char *name, double value);
+int sunsky_props_set_int(sunsky_props *p, const char *name, int64_t value);
+int sunsky_props_set_vector3(sunsky_props *p, const char *name, float x, float y, float z);
+int sunsky_props_set_transform(sunsky_props *p, const char *name, const float matrix_row_major[16]);
+int sunsky_props_set_spectrum(sunsky_props *p, const char *name, const float *values, int count);
+int sunsky_props_set_irregular_spectrum(sunsky_props *p, const char *name, const float *wavelengths,
+                                        const float *values, int count);
+
+/* ------------------------------------------------------------ emitter
+ * SunskyEmitter(const Properties&) -- sunsky.cpp:162-218.  Tables are staged on
+ * the host and uploaded to the CURRENT HIP device.  dataset_path: NULL for the
+ * bundled pack, a .pack file, or a directory holding the reference's
+ * resources/sunsky/datasets/<table>.bin files (path_to_dataset, sunsky.h:124-141). */
+int sunsky_emitter_create(const sunsky_props *props, int variant, int semantics,
+                          const char *dataset_path, sunsky_emitter **out);
+/* Same staging without a device: batch calls on it fail; for inspecting the
+ * staged tables (get_info / get_table / to_string) on machines without a GPU. */
+int sunsky_emitter_create_host(const sunsky_props *props, int variant, int semantics,
+                               const char *dataset_path, sunsky_emitter **out);
+void sunsky_emitter_destroy(sunsky_emitter *e);
+/* traverse() parameters, sunsky.cpp:220-240 (name, 1/3/11/16 floats) */
+int sunsky_emitter_set_param(sunsky_emitter *e, const char *name, const float *values, int count);
+/* parameters_changed(), sunsky.cpp:242-285 */
+int sunsky_emitter_parameters_changed(sunsky_emitter *e);
+/* set_scene(), sunsky.cpp:287-301: bounding sphere of the scene bbox */
+int sunsky_emitter_set_scene(sunsky_emitter *e, int bbox_valid, const float center[3], float radius);
+int sunsky_emitter_set_precision(sunsky_emitter *e, int precision);
+int sunsky_emitter_get_info(const sunsky_emitter *e, sunsky_info *out);
+int sunsky_emitter_get_table(const sunsky_emitter *e, int table_id, float *out, size_t capacity,
+                             size_t *count);
+/* to_string(), sunsky.cpp:502-519 */
+int sunsky_emitter_to_string(const sunsky_emitter *e, char *buf, size_t capacity);
+/* bbox(), sunsky.cpp:498-500: always an invalid box (min=+inf, max=-inf) */
+int sunsky_emitter_bbox(const sunsky_emitter *e, float out_min[3], float out_max[3]);
+
+/* ------------------------------------------------------ batched hot path */
+/* eval(si, active), sunsky.cpp:303-352.  wi = si.wi.
+ * RGB: out = 3 planes.  Spectral: wavelengths = n_wavelengths planes (per-ray
+ * si.wavelengths, Mitsuba uses 4) at `wavelengths + k * wl_stride`; out likewise. */
+int sunsky_eval(const sunsky_emitter *e, sunsky_vec3_in wi, const float *wavelengths,
+                int n_wavelengths, size_t wl_stride, const uint8_t *active, size_t n,
+                float *out, size_t out_stride, void *stream);
+/* eval_direction(it, ds, active), sunsky.cpp:453-461: eval with wi = -ds.d */
+int sunsky_eval_direction(const sunsky_emitter *e, sunsky_vec3_in d, const float *wavelengths,
+                          int n_wavelengths, size_t wl_stride, const uint8_t *active, size_t n,
+                          float *out, size_t out_stride, void *stream);
+/* Spectral eval of ONE host-side wavelength list broadcast to every ray (the
+ * eval_full_spec layout of test_sunsky.py:42-59): out plane k = lambda[k]. */
+int sunsky_eval_spectral_broadcast(const sunsky_emitter *e, sunsky_vec3_in wi,
+                                   const float *wavelengths_host, int n_wavelengths,
+                                   const uint8_t *active, size_t n, float *out,
+                                   size_t out_stride, void *stream);
+/* sample_direction(it, sample, active), sunsky.cpp:399-441.
+ * it_p: interaction positions (x == NULL -> origin).  Outputs ds.d (required),
+ * ds.pdf (required), ds.dist / ds.p (optional, NULL to skip); weight planes:
+ * 3 (RGB) or n_wavelengths (spectral, wavelengths = it.wavelengths). */
+int sunsky_sample_direction(const sunsky_emitter *e, const float *sample_x, const float *sample_y,
+                            sunsky_vec3_in it_p, const float *wavelengths, int n_wavelengths,
+                            size_t wl_stride, const uint8_t *active, size_t n, sunsky_vec3_out ds_d,
+                            float *ds_pdf, float *ds_dist, sunsky_vec3_out ds_p, float *weight,
+                            size_t weight_stride, void *stream);
+/* pdf_direction(it, ds, active), sunsky.cpp:443-451 */
+int sunsky_pdf_direction(const sunsky_emitter *e, sunsky_vec3_in ds_d, const uint8_t *active,
+                         size_t n, float *pdf, void *stream);
+/* sample_ray(time, wavelength_sample, sample2, sample3, active), sunsky.cpp:354-397.
+ * Outputs ray.o, ray.d, ray.wavelengths (4 planes; zeros in RGB) and weight
+ * (3 planes RGB / 4 spectral). */
+int sunsky_sample_ray(const sunsky_emitter *e, const float *wavelength_sample, const float *sample2_x,
+                      const float *sample2_y, const float *sample3_x, const float *sample3_y,
+                      const uint8_t *active, size_t n, sunsky_vec3_out ray_o, sunsky_vec3_out ray_d,
+                      float *ray_wavelengths, size_t wl_stride, float *weight, size_t weight_stride,
+                      void *stream);
+/* sample_wavelengths(si, sample, active), sunsky.cpp:463-480 (wi = si.wi).
+ * Outputs 4 wavelength planes and 4 (spectral) / 3 (RGB) weight planes. */
+int sunsky_sample_wavelengths(const sunsky_emitter *e, sunsky_vec3_in wi, const float *sample,
+                              const uint8_t *active, size_t n, float *wavelengths, size_t wl_stride,
+                              float *weight, size_t weight_stride, void *stream);
+/* sample_position(), sunsky.cpp:483-495: NotImplementedError in the reference */
+int sunsky_sample_position(const sunsky_emitter *e);
+
+/* --------------------------------------------- dataset I/O (sunsky_v.cpp:16-18) */
+/* array_from_file_d / _f (sunsky.h:516-561): file_dtype 0 = infer, 1 = fp32, 2 = fp64.
+ * Writes min(count, capacity) fp64 values; shape gets up to 16 dims. */
+int sunsky_array_from_file(const char *path, int file_dtype, double *out, size_t capacity,
+                           size_t *count, uint64_t *shape, int *ndims);
+/* array_to_file (sunsky.h:573-597) */
+int sunsky_array_to_file(const char *path, const float *data, size_t count, const uint64_t *shape,
+                         int ndims);
+/* Path of the bundled dataset pack the library resolves by default. */
+int sunsky_default_dataset_path(char *buf, size_t capacity);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SUNSKY_AMD_H */

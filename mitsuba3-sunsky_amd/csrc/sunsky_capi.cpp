@@ -1,0 +1,575 @@
+// sunsky_capi.cpp -- the C ABI (include/sunsky_amd.h): host staging through
+// SunskyModel, device tables, and kernel launches through hipModule.
+#include "sunsky_amd.h"
+
+#include <dlfcn.h>
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <sys/stat.h>
+
+#include "sunsky_dataset.h"
+#include "sunsky_model.h"
+#include "sunsky_props.h"
+#include "sunsky_types.h"
+
+using namespace sunsky;
+
+// ---------------------------------------------------------------- errors
+namespace {
+thread_local std::string g_error;
+
+int fail(int code, const std::string& msg) {
+    g_error = msg;
+    return code;
+}
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+void hip_check(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        f();
+        return SUNSKY_OK;
+    } catch (const HipError& e) {
+        return fail(SUNSKY_ERROR_HIP, e.what());
+    } catch (const std::invalid_argument& e) {
+        return fail(SUNSKY_ERROR_INVALID_VALUE, e.what());
+    } catch (const std::runtime_error& e) {
+        std::string m = e.what();
+        int code = (m.find("does not exist") != std::string::npos || m.find("cannot open") != std::string::npos)
+                       ? SUNSKY_ERROR_FILE
+                       : SUNSKY_ERROR_FORMAT;
+        return fail(code, m);
+    } catch (const std::exception& e) {
+        return fail(SUNSKY_ERROR_INTERNAL, e.what());
+    } catch (...) {
+        return fail(SUNSKY_ERROR_INTERNAL, "unknown error");
+    }
+}
+
+// ---------------------------------------------------------------- paths
+std::string library_dir() {
+    Dl_info info;
+    if (dladdr((const void*)&library_dir, &info) && info.dli_fname) {
+        std::string p = info.dli_fname;
+        size_t s = p.rfind('/');
+        return s == std::string::npos ? std::string(".") : p.substr(0, s);
+    }
+    return ".";
+}
+
+bool file_exists(const std::string& p) {
+    struct stat st;
+    return ::stat(p.c_str(), &st) == 0;
+}
+
+std::string default_pack_path() {
+    if (const char* env = std::getenv("SUNSKY_AMD_DATASET")) return env;
+    std::string d = library_dir();
+    for (const char* rel : {"/sunsky_datasets.pack", "/../data/sunsky_datasets.pack", "/data/sunsky_datasets.pack"})
+        if (file_exists(d + rel)) return d + rel;
+    return d + "/../data/sunsky_datasets.pack";
+}
+
+std::string code_object_path() {
+    if (const char* env = std::getenv("SUNSKY_AMD_CODE_OBJECT")) return env;
+    return library_dir() + "/sunsky_kernels.hsaco";
+}
+
+// ---------------------------------------------------------------- kernels
+enum KernelId {
+    K_EVAL_RGB_V4, K_EVAL_RGB_V1, K_EVAL_SPEC_BCAST_V4, K_EVAL_SPEC_BCAST_V1, K_EVAL_SPEC_RAYS,
+    K_SAMPLE_DIRECTION, K_PDF_DIRECTION, K_SAMPLE_WAVELENGTHS, K_SAMPLE_RAY, K_COUNT
+};
+const char* kKernelNames[K_COUNT] = {
+    "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
+    "sunsky_eval_spec_rays", "sunsky_sample_direction", "sunsky_pdf_direction", "sunsky_sample_wavelengths",
+    "sunsky_sample_ray"};
+
+struct DeviceModule {
+    hipModule_t module = nullptr;
+    hipFunction_t fn[2][K_COUNT] = {};   // [precision][kernel]
+    int cu_count = 256;
+};
+
+std::mutex g_module_mutex;
+std::map<int, DeviceModule*> g_modules;
+
+DeviceModule* module_for_device(int dev) {
+    std::lock_guard<std::mutex> lock(g_module_mutex);
+    auto it = g_modules.find(dev);
+    if (it != g_modules.end()) return it->second;
+    std::unique_ptr<DeviceModule> m(new DeviceModule());
+    std::string path = code_object_path();
+    if (!file_exists(path)) throw HipError("kernel code object not found: " + path + " (run the build)");
+    hip_check(hipModuleLoad(&m->module, path.c_str()), "hipModuleLoad(sunsky_kernels.hsaco)");
+    for (int p = 0; p < 2; ++p)
+        for (int k = 0; k < K_COUNT; ++k) {
+            std::string name = std::string(kKernelNames[k]) + (p == SUNSKY_PRECISION_FAST ? "_fast" : "_ref");
+            hip_check(hipModuleGetFunction(&m->fn[p][k], m->module, name.c_str()), name.c_str());
+        }
+    hip_check(hipDeviceGetAttribute(&m->cu_count, hipDeviceAttributeMultiprocessorCount, dev),
+              "hipDeviceGetAttribute");
+    DeviceModule* raw = m.release();
+    g_modules[dev] = raw;
+    return raw;
+}
+
+constexpr int kBlock = 256;
+
+// Memory-bound streaming launch: enough workgroups to fill every CU several
+// times over, grid-striding beyond (cdna_hip_programming.md Guideline 11).
+unsigned grid_for(const DeviceModule* m, size_t work_items) {
+    static const int mult = [] {
+        const char* e = std::getenv("SUNSKY_AMD_BLOCKS_PER_CU");
+        return e ? std::max(1, std::atoi(e)) : 16;
+    }();
+    size_t need = (work_items + kBlock - 1) / kBlock;
+    size_t cap = (size_t)m->cu_count * (size_t)mult;
+    return (unsigned)std::max<size_t>(1, std::min(need, cap));
+}
+
+void launch(hipFunction_t f, unsigned grid, hipStream_t stream, void** args) {
+    hip_check(hipModuleLaunchKernel(f, grid, 1, 1, kBlock, 1, 1, 0, stream, args, nullptr),
+              "hipModuleLaunchKernel");
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+struct LambdaSet {   // mirrors the kernel-side struct
+    int m;
+    int lo[kMaxBroadcastLambda];
+    float f[kMaxBroadcastLambda];
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------- handles
+struct sunsky_props {
+    Properties props;
+};
+
+struct sunsky_emitter {
+    std::unique_ptr<SunskyModel> model;
+    SunskyKArgs kargs;
+    DeviceModule* mod = nullptr;
+    int device = 0;
+    int precision = SUNSKY_PRECISION_FAST;
+    float* d_sun_table = nullptr;
+    float* d_sun_ld = nullptr;
+
+    void upload() {
+        int cur = 0;
+        hip_check(hipGetDevice(&cur), "hipGetDevice");
+        if (cur != device) hip_check(hipSetDevice(device), "hipSetDevice");
+        const std::vector<float>& st = model->sun_table();
+        const std::vector<float>& ld = model->sun_ld();
+        if (!d_sun_table) hip_check(hipMalloc(&d_sun_table, sizeof(float) * kSunRgbTableSize), "hipMalloc");
+        if (!d_sun_ld) hip_check(hipMalloc(&d_sun_ld, sizeof(float) * kNbWavelengths * kNbSunLdParams), "hipMalloc");
+        // Tables may still be read by in-flight launches of a previous state.
+        hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        hip_check(hipMemcpy(d_sun_table, st.data(), sizeof(float) * st.size(), hipMemcpyHostToDevice), "hipMemcpy");
+        hip_check(hipMemcpy(d_sun_ld, ld.data(), sizeof(float) * std::min<size_t>(ld.size(), kNbWavelengths * kNbSunLdParams),
+                            hipMemcpyHostToDevice), "hipMemcpy");
+        kargs = model->kargs();
+        kargs.sun_table = d_sun_table;
+        kargs.sun_ld = d_sun_ld;
+        if (cur != device) (void)hipSetDevice(cur);
+    }
+
+    hipFunction_t fn(KernelId k) const {
+        if (!mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
+        return mod->fn[precision][k];
+    }
+
+    ~sunsky_emitter() {
+        if (d_sun_table) (void)hipFree(d_sun_table);
+        if (d_sun_ld) (void)hipFree(d_sun_ld);
+    }
+};
+
+extern "C" {
+
+int sunsky_abi_version(void) { return SUNSKY_AMD_ABI_VERSION; }
+const char* sunsky_last_error(void) { return g_error.c_str(); }
+
+int sunsky_props_create(sunsky_props** out) {
+    if (!out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null output pointer");
+    return guarded([&] { *out = new sunsky_props(); });
+}
+void sunsky_props_destroy(sunsky_props* p) { delete p; }
+
+#define PROPS_GUARD(p, name)                                                                   \
+    if (!(p) || !(name)) return fail(SUNSKY_ERROR_INVALID_VALUE, "null props / property name")
+
+int sunsky_props_set_float(sunsky_props* p, const char* name, double v) {
+    PROPS_GUARD(p, name);
+    return guarded([&] { p->props.set_float(name, v); });
+}
+int sunsky_props_set_int(sunsky_props* p, const char* name, int64_t v) {
+    PROPS_GUARD(p, name);
+    return guarded([&] { p->props.set_int(name, v); });
+}
+int sunsky_props_set_vector3(sunsky_props* p, const char* name, float x, float y, float z) {
+    PROPS_GUARD(p, name);
+    return guarded([&] { p->props.set_vector3(name, x, y, z); });
+}
+int sunsky_props_set_transform(sunsky_props* p, const char* name, const float m[16]) {
+    PROPS_GUARD(p, name);
+    if (!m) return fail(SUNSKY_ERROR_INVALID_VALUE, "null matrix");
+    return guarded([&] { p->props.set_transform(name, m); });
+}
+int sunsky_props_set_spectrum(sunsky_props* p, const char* name, const float* v, int n) {
+    PROPS_GUARD(p, name);
+    if (!v || n <= 0) return fail(SUNSKY_ERROR_INVALID_VALUE, "empty spectrum");
+    return guarded([&] { p->props.set_spectrum(name, v, n); });
+}
+int sunsky_props_set_irregular_spectrum(sunsky_props* p, const char* name, const float* wl, const float* v, int n) {
+    PROPS_GUARD(p, name);
+    if (!wl || !v || n <= 0) return fail(SUNSKY_ERROR_INVALID_VALUE, "empty spectrum");
+    return guarded([&] { p->props.set_irregular(name, wl, v, n); });
+}
+
+int sunsky_emitter_create(const sunsky_props* props, int variant, int semantics, const char* dataset_path,
+                          sunsky_emitter** out) {
+    if (!props || !out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null props / output pointer");
+    *out = nullptr;
+    return guarded([&] {
+        std::unique_ptr<sunsky_emitter> e(new sunsky_emitter());
+        std::string ds = dataset_path && *dataset_path ? std::string(dataset_path) : default_pack_path();
+        e->model.reset(new SunskyModel(props->props, variant, semantics, ds));
+        hip_check(hipGetDevice(&e->device), "hipGetDevice");
+        e->mod = module_for_device(e->device);
+        if (const char* env = std::getenv("SUNSKY_AMD_PRECISION"))
+            e->precision = std::strcmp(env, "reference") == 0 ? SUNSKY_PRECISION_REFERENCE : SUNSKY_PRECISION_FAST;
+        e->upload();
+        for (const std::string& w : e->model->warnings) std::fprintf(stderr, "WARN sunsky: %s\n", w.c_str());
+        *out = e.release();
+    });
+}
+
+int sunsky_emitter_create_host(const sunsky_props* props, int variant, int semantics, const char* dataset_path,
+                               sunsky_emitter** out) {
+    if (!props || !out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null props / output pointer");
+    *out = nullptr;
+    return guarded([&] {
+        std::unique_ptr<sunsky_emitter> e(new sunsky_emitter());
+        std::string ds = dataset_path && *dataset_path ? std::string(dataset_path) : default_pack_path();
+        e->model.reset(new SunskyModel(props->props, variant, semantics, ds));
+        e->device = -1;
+        e->kargs = e->model->kargs();
+        *out = e.release();
+    });
+}
+
+void sunsky_emitter_destroy(sunsky_emitter* e) { delete e; }
+
+int sunsky_emitter_set_param(sunsky_emitter* e, const char* name, const float* v, int count) {
+    if (!e || !name || !v) return fail(SUNSKY_ERROR_INVALID_VALUE, "null argument");
+    return guarded([&] { e->model->set_param(name, v, count); });
+}
+
+int sunsky_emitter_parameters_changed(sunsky_emitter* e) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    return guarded([&] {
+        e->model->parameters_changed();   // keeps the scene bounding sphere
+        if (e->device >= 0) e->upload();
+        else e->kargs = e->model->kargs();
+    });
+}
+
+int sunsky_emitter_set_scene(sunsky_emitter* e, int bbox_valid, const float center[3], float radius) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    float zero[3] = {0, 0, 0};
+    return guarded([&] {
+        e->model->set_scene(bbox_valid != 0, center ? center : zero, radius);
+        const SunskyKArgs& k = e->model->kargs();
+        std::memcpy(e->kargs.bs_center, k.bs_center, sizeof(k.bs_center));
+        e->kargs.bs_radius = k.bs_radius;
+    });
+}
+
+int sunsky_emitter_set_precision(sunsky_emitter* e, int precision) {
+    if (!e || (precision != SUNSKY_PRECISION_FAST && precision != SUNSKY_PRECISION_REFERENCE))
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "invalid precision mode");
+    e->precision = precision;
+    return SUNSKY_OK;
+}
+
+int sunsky_emitter_get_info(const sunsky_emitter* e, sunsky_info* out) {
+    if (!e || !out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null argument");
+    const SunskyKArgs& k = e->kargs;
+    std::memset(out, 0, sizeof(*out));
+    out->variant = e->model->variant();
+    out->semantics = k.semantics;
+    out->nb_channels = e->model->nch();
+    out->active_record = e->model->active_record();
+    out->turbidity = e->model->turbidity();
+    out->sky_scale = k.sky_scale;
+    out->sun_scale = k.sun_scale;
+    out->sun_half_aperture = k.half_aperture;
+    out->cos_cutoff = k.cos_cutoff;
+    out->area_ratio = k.area_ratio;
+    std::memcpy(out->sun_dir_world, e->model->sun_dir_world(), 3 * sizeof(float));
+    std::memcpy(out->sun_dir_local, k.sun_n, 3 * sizeof(float));
+    out->sun_angles[0] = k.sun_phi;
+    out->sun_angles[1] = k.sun_theta;
+    out->sky_sampling_w = k.w_sky;
+    std::memcpy(out->bsphere_center, k.bs_center, 3 * sizeof(float));
+    out->bsphere_radius = k.bs_radius;
+    out->flags = SUNSKY_FLAG_INFINITE | SUNSKY_FLAG_SPATIALLY_VARYING;
+    out->device = e->device;
+    out->precision = e->precision;
+    return SUNSKY_OK;
+}
+
+int sunsky_emitter_get_table(const sunsky_emitter* e, int id, float* out, size_t cap, size_t* count) {
+    if (!e || !count) return fail(SUNSKY_ERROR_INVALID_VALUE, "null argument");
+    std::vector<float> v;
+    const SunskyKArgs& k = e->kargs;
+    switch (id) {
+        case SUNSKY_TABLE_SKY_PARAMS: v = e->model->sky_params(); break;
+        case SUNSKY_TABLE_SKY_RADIANCE: v = e->model->sky_radiance(); break;
+        case SUNSKY_TABLE_SUN_RADIANCE: v = e->model->sun_table(); break;
+        case SUNSKY_TABLE_SUN_LD: v = e->model->sun_ld(); break;
+        case SUNSKY_TABLE_GAUSSIANS: v.assign(e->model->gaussians_raw(), e->model->gaussians_raw() + kNbMixture * kNbGaussianParams); break;
+        case SUNSKY_TABLE_GAUSSIAN_CDF: v.assign(k.gauss_cdf, k.gauss_cdf + kNbMixture); break;
+        case SUNSKY_TABLE_SPECTRAL_PDF: v.assign(k.spec_pdf, k.spec_pdf + k.spec_size); break;
+        case SUNSKY_TABLE_SPECTRAL_CDF: v.assign(k.spec_cdf, k.spec_cdf + std::max(0, k.spec_size - 1)); break;
+        case SUNSKY_TABLE_ALBEDO: v = e->model->albedo(); break;
+        default: return fail(SUNSKY_ERROR_INVALID_VALUE, "unknown table id");
+    }
+    *count = v.size();
+    if (out) std::memcpy(out, v.data(), sizeof(float) * std::min(cap, v.size()));
+    return SUNSKY_OK;
+}
+
+int sunsky_emitter_to_string(const sunsky_emitter* e, char* buf, size_t cap) {
+    if (!e || !buf || !cap) return fail(SUNSKY_ERROR_INVALID_VALUE, "null argument");
+    std::string s = e->model->to_string();
+    std::snprintf(buf, cap, "%s", s.c_str());
+    return SUNSKY_OK;
+}
+
+int sunsky_emitter_bbox(const sunsky_emitter* e, float mn[3], float mx[3]) {
+    if (!e || !mn || !mx) return fail(SUNSKY_ERROR_INVALID_VALUE, "null argument");
+    for (int i = 0; i < 3; ++i) { mn[i] = INFINITY; mx[i] = -INFINITY; }
+    return SUNSKY_OK;
+}
+
+// ---------------------------------------------------------------- hot path
+static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam, int nlam, size_t lstride,
+                     const uint8_t* active, size_t n, float* out, size_t ostride, void* stream, float sign) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (n == 0) return SUNSKY_OK;
+    if (!w.x || !w.y || !w.z || !out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null ray / output pointer");
+    const bool spec = e->kargs.variant == kSpectral;
+    if (spec && (!lam || nlam < 1 || nlam > kMaxLambdaPerRay))
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "spectral eval needs 1..16 wavelength planes");
+    const size_t nout = spec ? (size_t)nlam : 3;
+    if (nout > 1 && ostride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "out_stride < n");
+    if (spec && nlam > 1 && lstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "wl_stride < n");
+    return guarded([&] {
+        hipStream_t s = (hipStream_t)stream;
+        SunskyKArgs K = e->kargs;
+        if (!spec) {
+            bool vec = n >= 4 && aligned16(w.x) && aligned16(w.y) && aligned16(w.z) && aligned16(out) &&
+                       (ostride % 4) == 0 && (!active || ((uintptr_t)active & 3u) == 0);
+            size_t n4 = vec ? (n & ~(size_t)3) : 0;
+            if (n4) {
+                const float *x = w.x, *y = w.y, *z = w.z;
+                void* args[] = {&K, &x, &y, &z, &active, &n4, &out, &ostride, &sign};
+                launch(e->fn(K_EVAL_RGB_V4), grid_for(e->mod, n4 / 4), s, args);
+            }
+            if (n4 < n) {
+                const float *x = w.x + n4, *y = w.y + n4, *z = w.z + n4;
+                const uint8_t* a = active ? active + n4 : nullptr;
+                float* o = out + n4;
+                size_t rem = n - n4;
+                void* args[] = {&K, &x, &y, &z, &a, &rem, &o, &ostride, &sign};
+                launch(e->fn(K_EVAL_RGB_V1), grid_for(e->mod, rem), s, args);
+            }
+        } else {
+            const float *x = w.x, *y = w.y, *z = w.z;
+            int nl = nlam;
+            void* args[] = {&K, &x, &y, &z, &lam, &lstride, &nl, &active, &n, &out, &ostride, &sign};
+            launch(e->fn(K_EVAL_SPEC_RAYS), grid_for(e->mod, n), s, args);
+        }
+    });
+}
+
+int sunsky_eval(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam, int nlam, size_t lstride,
+                const uint8_t* active, size_t n, float* out, size_t ostride, void* stream) {
+    return eval_impl(e, wi, lam, nlam, lstride, active, n, out, ostride, stream, -1.f);
+}
+
+int sunsky_eval_direction(const sunsky_emitter* e, sunsky_vec3_in d, const float* lam, int nlam, size_t lstride,
+                          const uint8_t* active, size_t n, float* out, size_t ostride, void* stream) {
+    return eval_impl(e, d, lam, nlam, lstride, active, n, out, ostride, stream, 1.f);
+}
+
+int sunsky_eval_spectral_broadcast(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam_host, int m,
+                                   const uint8_t* active, size_t n, float* out, size_t ostride, void* stream) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (e->kargs.variant != kSpectral) return fail(SUNSKY_ERROR_INVALID_VALUE, "broadcast eval needs a spectral emitter");
+    if (!lam_host || m < 1 || m > kMaxBroadcastLambda)
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "1..32 broadcast wavelengths required");
+    if (n == 0) return SUNSKY_OK;
+    if (!w.x || !w.y || !w.z || !out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null ray / output pointer");
+    if (m > 1 && ostride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "out_stride < n");
+    LambdaSet L;
+    std::memset(&L, 0, sizeof(L));
+    L.m = m;
+    for (int k = 0; k < m; ++k) {
+        // normalized_wavelengths / floor2int / lerp factor, sunsky.cpp:326-332
+        float nw = (lam_host[k] - kWavelength0) / kWavelengthStep;
+        bool valid = (0.f <= nw) && (nw <= (float)(kNbWavelengths - 1));
+        int lo = valid ? (int)std::floor(nw) : 0;
+        L.lo[k] = lo;
+        L.f[k] = valid ? nw - (float)lo : -1.f;
+    }
+    return guarded([&] {
+        hipStream_t s = (hipStream_t)stream;
+        SunskyKArgs K = e->kargs;
+        float sign = -1.f;
+        bool vec = n >= 4 && aligned16(w.x) && aligned16(w.y) && aligned16(w.z) && aligned16(out) &&
+                   (ostride % 4) == 0 && (!active || ((uintptr_t)active & 3u) == 0);
+        size_t n4 = vec ? (n & ~(size_t)3) : 0;
+        if (n4) {
+            const float *x = w.x, *y = w.y, *z = w.z;
+            void* args[] = {&K, &L, &x, &y, &z, &active, &n4, &out, &ostride, &sign};
+            launch(e->fn(K_EVAL_SPEC_BCAST_V4), grid_for(e->mod, n4 / 4), s, args);
+        }
+        if (n4 < n) {
+            const float *x = w.x + n4, *y = w.y + n4, *z = w.z + n4;
+            const uint8_t* a = active ? active + n4 : nullptr;
+            float* o = out + n4;
+            size_t rem = n - n4;
+            void* args[] = {&K, &L, &x, &y, &z, &a, &rem, &o, &ostride, &sign};
+            launch(e->fn(K_EVAL_SPEC_BCAST_V1), grid_for(e->mod, rem), s, args);
+        }
+    });
+}
+
+int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const float* uy, sunsky_vec3_in it_p,
+                            const float* lam, int nlam, size_t lstride, const uint8_t* active, size_t n,
+                            sunsky_vec3_out ds_d, float* ds_pdf, float* ds_dist, sunsky_vec3_out ds_p,
+                            float* weight, size_t wstride, void* stream) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (n == 0) return SUNSKY_OK;
+    const bool spec = e->kargs.variant == kSpectral;
+    if (!ux || !uy || !ds_d.x || !ds_d.y || !ds_d.z || !ds_pdf || !weight)
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "null sample / output pointer");
+    if (spec && (!lam || nlam < 1 || nlam > kMaxLambdaPerRay))
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "spectral sample_direction needs 1..16 wavelength planes");
+    if (wstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "weight_stride < n");
+    if ((it_p.x != nullptr) != (it_p.y != nullptr) || (it_p.x != nullptr) != (it_p.z != nullptr))
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "it_p must be all-NULL or all-set");
+    if ((ds_p.x != nullptr) != (ds_p.y != nullptr) || (ds_p.x != nullptr) != (ds_p.z != nullptr))
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "ds_p must be all-NULL or all-set");
+    return guarded([&] {
+        SunskyKArgs K = e->kargs;
+        int nl = spec ? nlam : 0;
+        void* args[] = {&K, &ux, &uy, (void*)&it_p.x, (void*)&it_p.y, (void*)&it_p.z, &lam, &lstride, &nl, &active, &n,
+                        &ds_d.x, &ds_d.y, &ds_d.z, &ds_pdf, &ds_dist, &ds_p.x, &ds_p.y, &ds_p.z, &weight, &wstride};
+        launch(e->fn(K_SAMPLE_DIRECTION), grid_for(e->mod, n), (hipStream_t)stream, args);
+    });
+}
+
+int sunsky_pdf_direction(const sunsky_emitter* e, sunsky_vec3_in d, const uint8_t* active, size_t n, float* pdf,
+                         void* stream) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (n == 0) return SUNSKY_OK;
+    if (!d.x || !d.y || !d.z || !pdf) return fail(SUNSKY_ERROR_INVALID_VALUE, "null direction / output pointer");
+    return guarded([&] {
+        SunskyKArgs K = e->kargs;
+        void* args[] = {&K, (void*)&d.x, (void*)&d.y, (void*)&d.z, &active, &n, &pdf};
+        launch(e->fn(K_PDF_DIRECTION), grid_for(e->mod, n), (hipStream_t)stream, args);
+    });
+}
+
+int sunsky_sample_ray(const sunsky_emitter* e, const float* wls, const float* s2x, const float* s2y,
+                      const float* s3x, const float* s3y, const uint8_t* active, size_t n, sunsky_vec3_out o,
+                      sunsky_vec3_out d, float* lam, size_t lstride, float* weight, size_t wstride, void* stream) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (n == 0) return SUNSKY_OK;
+    if (!s2x || !s2y || !s3x || !s3y || !o.x || !o.y || !o.z || !d.x || !d.y || !d.z || !lam || !weight)
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "null sample / output pointer");
+    if (e->kargs.variant == kSpectral && !wls) return fail(SUNSKY_ERROR_INVALID_VALUE, "null wavelength sample");
+    if (lstride < n || wstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "stride < n");
+    return guarded([&] {
+        SunskyKArgs K = e->kargs;
+        void* args[] = {&K, &wls, &s2x, &s2y, &s3x, &s3y, &active, &n, &o.x, &o.y, &o.z,
+                        &d.x, &d.y, &d.z, &lam, &lstride, &weight, &wstride};
+        launch(e->fn(K_SAMPLE_RAY), grid_for(e->mod, n), (hipStream_t)stream, args);
+    });
+}
+
+int sunsky_sample_wavelengths(const sunsky_emitter* e, sunsky_vec3_in w, const float* sample, const uint8_t* active,
+                              size_t n, float* lam, size_t lstride, float* weight, size_t wstride, void* stream) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (n == 0) return SUNSKY_OK;
+    if (!w.x || !w.y || !w.z || !lam || !weight) return fail(SUNSKY_ERROR_INVALID_VALUE, "null pointer");
+    if (e->kargs.variant == kSpectral && !sample) return fail(SUNSKY_ERROR_INVALID_VALUE, "null sample");
+    if (lstride < n || wstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "stride < n");
+    return guarded([&] {
+        SunskyKArgs K = e->kargs;
+        void* args[] = {&K, (void*)&w.x, (void*)&w.y, (void*)&w.z, &sample, &active, &n, &lam, &lstride, &weight, &wstride};
+        launch(e->fn(K_SAMPLE_WAVELENGTHS), grid_for(e->mod, n), (hipStream_t)stream, args);
+    });
+}
+
+int sunsky_sample_position(const sunsky_emitter* e) {
+    (void)e;
+    return fail(SUNSKY_ERROR_NOT_IMPLEMENTED, "sample_position");
+}
+
+int sunsky_array_from_file(const char* path, int file_dtype, double* out, size_t cap, size_t* count, uint64_t* shape,
+                           int* ndims) {
+    if (!path || !count) return fail(SUNSKY_ERROR_INVALID_VALUE, "null argument");
+    Table t;
+    std::string err;
+    if (!read_array_file(path, file_dtype, &t, &err))
+        return fail(err.find("does not exist") != std::string::npos ? SUNSKY_ERROR_FILE : SUNSKY_ERROR_FORMAT, err);
+    *count = t.size();
+    if (out) std::memcpy(out, t.data.data(), sizeof(double) * std::min(cap, t.size()));
+    if (ndims) *ndims = (int)t.shape.size();
+    if (shape)
+        for (size_t i = 0; i < t.shape.size() && i < 16; ++i) shape[i] = t.shape[i];
+    return SUNSKY_OK;
+}
+
+int sunsky_array_to_file(const char* path, const float* data, size_t count, const uint64_t* shape, int ndims) {
+    if (!path || (!data && count)) return fail(SUNSKY_ERROR_INVALID_VALUE, "null argument");
+    std::vector<size_t> sh;
+    for (int i = 0; i < ndims; ++i) sh.push_back((size_t)shape[i]);
+    std::string err;
+    if (!write_array_file(path, data, count, sh.empty() ? nullptr : sh.data(), (int)sh.size(), &err))
+        return fail(SUNSKY_ERROR_FILE, err);
+    return SUNSKY_OK;
+}
+
+int sunsky_default_dataset_path(char* buf, size_t cap) {
+    if (!buf || !cap) return fail(SUNSKY_ERROR_INVALID_VALUE, "null buffer");
+    std::snprintf(buf, cap, "%s", default_pack_path().c_str());
+    return SUNSKY_OK;
+}
+
+}  // extern "C"

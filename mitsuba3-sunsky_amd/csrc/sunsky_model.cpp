@@ -1,0 +1,667 @@
+// sunsky_model.cpp -- host staging of the sun/sky emitter (see sunsky_model.h).
+// All staging arithmetic is fp32 like the reference's float variants, where
+// the tables are read as fp64 and cast to fp32 (sunsky.cpp:182-199).
+#include "sunsky_model.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+#include <stdexcept>
+#include <sys/stat.h>
+
+#include "sunsky_math.h"
+
+namespace sunsky {
+
+namespace {
+
+std::string fmt(const char* f, double v) {
+    char buf[256];
+    std::snprintf(buf, sizeof(buf), f, v);
+    return buf;
+}
+
+bool is_dir(const std::string& p) {
+    struct stat st;
+    return ::stat(p.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+
+std::vector<float> to_f32(const Table& t) {
+    std::vector<float> r(t.size());
+    for (size_t i = 0; i < t.size(); ++i) r[i] = (float)t.data[i];
+    return r;
+}
+
+// bezier_interpolate + compute_radiance_params, sunsky.h:158-231
+void compute_radiance_params(const std::vector<float>& ds, int nch, int npar, const std::vector<float>& albedo,
+                             float turbidity, float eta, std::vector<float>* out) {
+    static const float coefs[kNbSkyCtrlPts] = {1, 5, 10, 10, 5, 1};
+    const int result_size = nch * npar, a_block = kNbSkyCtrlPts * result_size, t_block = kNbAlbedo * a_block;
+    float x = cbrtf(2.f * kInvPi * eta);
+    int t_high = (int)floorf(turbidity), t_low = t_high - 1;
+    float t_rem = turbidity - (float)t_high;
+    bool in_range = (0.f <= eta) && (eta <= 0.5f * kPi);
+    out->assign(result_size, 0.f);
+    for (int e = 0; e < result_size; ++e) {
+        float bez[2][2];
+        for (int ti = 0; ti < 2; ++ti) {
+            int t = ti ? t_high : t_low;
+            for (int a = 0; a < 2; ++a) {
+                float res = 0.f;
+                if (t >= 0 && t < kNbTurbidity)   // gather mask "t < NB_TURBIDITY"
+                    for (int k = 0; k < kNbSkyCtrlPts; ++k) {
+                        float data = ds[(size_t)t * t_block + a * a_block + k * result_size + e];
+                        float term = coefs[k] * powif_(x, k);
+                        term = term * powif_(1.f - x, kNbSkyCtrlPts - 1 - k);
+                        term = term * data;
+                        res = res + term;
+                    }
+                bez[ti][a] = res;
+            }
+        }
+        float ra_low = lerpf_(bez[0][0], bez[1][0], t_rem);
+        float ra_high = lerpf_(bez[0][1], bez[1][1], t_rem);
+        float v = lerpf_(ra_low, ra_high, albedo[e / npar]);
+        (*out)[e] = in_range ? v : 0.f;
+    }
+}
+
+// compute_sun_params, sunsky.h:404-419
+void compute_sun_params(const std::vector<float>& ds, int block, float turbidity, std::vector<float>* out) {
+    int t_high = (int)floorf(turbidity), t_low = t_high - 1;
+    float t_rem = turbidity - (float)t_high;
+    out->assign(block, 0.f);
+    for (int i = 0; i < block; ++i) {
+        float lo = (t_low >= 0 && t_low < kNbTurbidity) ? ds[(size_t)t_low * block + i] : 0.f;
+        float hi = (t_high >= 0 && t_high < kNbTurbidity) ? ds[(size_t)t_high * block + i] : 0.f;
+        (*out)[i] = lerpf_(lo, hi, t_rem);
+    }
+}
+
+float clipf_(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+void invert3(const double* m, double* inv) {
+    double det = m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) +
+                 m[2] * (m[3] * m[7] - m[4] * m[6]);
+    if (det == 0.0) throw std::invalid_argument("to_world transform is singular");
+    inv[0] = (m[4] * m[8] - m[5] * m[7]) / det; inv[1] = (m[2] * m[7] - m[1] * m[8]) / det;
+    inv[2] = (m[1] * m[5] - m[2] * m[4]) / det; inv[3] = (m[5] * m[6] - m[3] * m[8]) / det;
+    inv[4] = (m[0] * m[8] - m[2] * m[6]) / det; inv[5] = (m[2] * m[3] - m[0] * m[5]) / det;
+    inv[6] = (m[3] * m[7] - m[4] * m[6]) / det; inv[7] = (m[1] * m[6] - m[0] * m[7]) / det;
+    inv[8] = (m[0] * m[4] - m[1] * m[3]) / det;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------ free helpers
+void compute_sun_coordinates(const DateTime& t, const Location& l, float out[3]) {
+    float dec_hours = t.hour - l.timezone + (t.minute + t.second / 60.f) / 60.f;
+    int li_aux_1 = (t.month - 14) / 12;
+    int li_aux_2 = (1461 * (t.year + 4800 + li_aux_1)) / 4 + (367 * (t.month - 2 - 12 * li_aux_1)) / 12 -
+                   (3 * ((t.year + 4900 + li_aux_1) / 100)) / 4 + t.day - 32075;
+    float d_julian_date = (float)li_aux_2 - 0.5f + dec_hours / 24.f;
+    float elapsed = d_julian_date - 2451545.f;
+
+    float omega = 2.1429f - 0.0010394594f * elapsed;
+    float mean_longitude = 4.8950630f + 0.017202791698f * elapsed;
+    float anomaly = 6.2400600f + 0.0172019699f * elapsed;
+    float ecl_long = mean_longitude + 0.03341607f * sinf(anomaly) + 0.00034894f * sinf(2 * anomaly) -
+                     0.0001134f - 0.0000203f * sinf(omega);
+    float ecl_obl = 0.4090928f - 6.2140e-9f * elapsed + 0.0000396f * cosf(omega);
+
+    float sin_ecl = sinf(ecl_long);
+    float dy = cosf(ecl_obl) * sin_ecl, dx = cosf(ecl_long);
+    float ra = atan2f(dy, dx);
+    ra += ra < 0.f ? kTwoPi : 0.f;
+    float decl = asinf(sinf(ecl_obl) * sin_ecl);
+
+    float gmst = 6.6974243242f + 0.0657098283f * elapsed + dec_hours;
+    const float deg2rad = (float)(3.14159265358979323846 / 180.0);
+    float lmst = (gmst * 15 + l.longitude) * deg2rad;
+    float lat = l.latitude * deg2rad;
+    float cos_lat = cosf(lat), sin_lat = sinf(lat);
+    float ha = lmst - ra, cos_ha = cosf(ha);
+    float elevation = acosf(cos_lat * cos_ha * cosf(decl) + sinf(decl) * sin_lat);
+    dy = -sinf(ha);
+    dx = tanf(decl) * cos_lat - sin_lat * cos_ha;
+    float azimuth = atan2f(dy, dx);
+    azimuth += azimuth < 0.f ? kTwoPi : 0.f;
+    elevation += (float)(6371.01 / 149597890.0) * sinf(elevation);   // parallax
+    float3_ d = sphdir(elevation, azimuth - kPi);
+    out[0] = d.x; out[1] = d.y; out[2] = d.z;
+}
+
+void gauss_legendre(int n, std::vector<double>* nodes, std::vector<double>* weights) {
+    auto legendre_pd = [](int l, double x, double* lv, double* dv) {   // math.h:93-120
+        double l_cur = 0, d_cur = 0;
+        if (l > 1) {
+            double l_p = 1, l_pred = x, d_p = 0, d_pred = 1, k0 = 3, k1 = 2, k2 = 1;
+            for (int ki = 2; ki <= l; ++ki) {
+                l_cur = (k0 * x * l_pred - k2 * l_p) / k1;
+                d_cur = d_p + k0 * l_pred;
+                l_p = l_pred; l_pred = l_cur; d_p = d_pred; d_pred = d_cur;
+                k2 = k1; k0 += 2; k1 += 1;
+            }
+        } else if (l == 0) { l_cur = 1; d_cur = 0; } else { l_cur = x; d_cur = 1; }
+        *lv = l_cur; *dv = d_cur;
+    };
+    nodes->assign(n, 0.0);
+    weights->assign(n, 0.0);
+    if (n < 1) throw std::invalid_argument("gauss_legendre(): n must be >= 1");
+    n--;
+    if (n == 0) { (*nodes)[0] = 0; (*weights)[0] = 2; return; }
+    if (n == 1) { (*nodes)[0] = -std::sqrt(1.0 / 3.0); (*nodes)[1] = -(*nodes)[0]; (*weights)[0] = (*weights)[1] = 1; }
+    int m = (n + 1) / 2;
+    for (int i = 0; i < m; ++i) {
+        double x = -std::cos((double)(2 * i + 1) / (double)(2 * n + 2) * 3.14159265358979323846);
+        for (int it = 0;; ++it) {
+            if (it >= 20) throw std::runtime_error("gauss_legendre: did not converge");
+            double lv, dv;
+            legendre_pd(n + 1, x, &lv, &dv);
+            double step = lv / dv;
+            x -= step;
+            if (std::fabs(step) <= 4 * std::fabs(x) * 1.1102230246251565e-16) break;
+        }
+        double lv, dv;
+        legendre_pd(n + 1, x, &lv, &dv);
+        (*weights)[i] = (*weights)[n - i] = 2 / ((1 - x * x) * (dv * dv));
+        (*nodes)[i] = x;
+        (*nodes)[n - i] = -x;
+    }
+    if ((n % 2) == 0) {
+        double lv, dv;
+        legendre_pd(n + 1, 0.0, &lv, &dv);
+        (*weights)[n / 2] = 2.0 / (dv * dv);
+        (*nodes)[n / 2] = 0;
+    }
+}
+
+// ------------------------------------------------------------ SunskyModel
+SunskyModel::SunskyModel(const Properties& props, int variant, int semantics, const std::string& datasets)
+    : variant_(variant), semantics_(semantics) {
+    if (variant != kRGB && variant != kSpectral)
+        throw std::invalid_argument("Unsupported spectrum type, can only render in Spectral or RGB modes!");
+    if (semantics != kJit && semantics != kScalar) throw std::invalid_argument("unknown variant semantics");
+    nch_ = variant == kSpectral ? kNbWavelengths : 3;
+    std::memset(&k_, 0, sizeof(k_));
+
+    // ---------------- init_from_props, sunsky.cpp:889-948
+    sun_scale_ = (float)props.get_float("sun_scale", 1.0);
+    if (sun_scale_ < 0.f) throw std::invalid_argument(fmt("Invalid sun scale: %f, must be positive!", sun_scale_));
+    sky_scale_ = (float)props.get_float("sky_scale", 1.0);
+    if (sky_scale_ < 0.f) throw std::invalid_argument(fmt("Invalid sky scale: %f, must be positive!", sky_scale_));
+    float turb = (float)props.get_float("turbidity", 3.0);
+    if (turb < 1.f || 10.f < turb) throw std::invalid_argument(fmt("Turbidity value %f is out of range [1, 10]", turb));
+    turbidity_ = turb;
+    const float deg2rad = (float)(3.14159265358979323846 / 180.0);
+    sun_half_aperture_ = (0.5f * (float)props.get_float("sun_aperture", 0.5358)) * deg2rad;
+    if (sun_half_aperture_ <= 0.f || 0.5f * kPi <= sun_half_aperture_)
+        throw std::invalid_argument(fmt("Invalid sun aperture angle: %f, must be in ]0, 90[ degrees!",
+                                        2.0 * sun_half_aperture_ / deg2rad));
+    extract_albedo(props);
+
+    // Endpoint base: to_world (default identity)
+    static const float ident[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    const Properties::Value* tw = props.get_typed("to_world", Properties::Type::Transform);
+    std::memcpy(to_world_, tw ? tw->m : ident, sizeof(to_world_));
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) to_world_d_[r * 3 + c] = to_world_[r * 4 + c];
+    invert3(to_world_d_, to_local_d_);
+    for (int i = 0; i < 9; ++i) { k_.to_world[i] = (float)to_world_d_[i]; k_.to_local[i] = (float)to_local_d_[i]; }
+    k_.identity_xform = 1;
+    for (int i = 0; i < 9; ++i)
+        if (k_.to_world[i] != ((i % 4) == 0 ? 1.f : 0.f) || k_.to_local[i] != ((i % 4) == 0 ? 1.f : 0.f)) k_.identity_xform = 0;
+
+    const char* tl_keys[] = {"latitude", "longitude", "timezone", "year", "month", "day", "hour", "minute", "second"};
+    if (props.has("sun_direction")) {
+        for (const char* key : tl_keys)
+            if (props.has(key))
+                throw std::invalid_argument(
+                    "Both the 'sun_direction' and parameters for time/location were provided, both "
+                    "information cannot be given at the same time!");
+        active_record_ = false;
+        const Properties::Value* v = props.get_typed("sun_direction", Properties::Type::Vector3);
+        float3_ d = mk3(v->m[0], v->m[1], v->m[2]);
+        float inv = 1.f / sqrtf(dot3(d, d));
+        sun_dir_[0] = d.x * inv; sun_dir_[1] = d.y * inv; sun_dir_[2] = d.z * inv;
+    } else {
+        location_.latitude = (float)props.get_float("latitude", 35.6894);
+        location_.longitude = (float)props.get_float("longitude", 139.6917);
+        location_.timezone = (float)props.get_float("timezone", 9.0);
+        time_.year = (int)props.get_int("year", 2010);
+        time_.month = (int)props.get_int("month", 7);
+        time_.day = (int)props.get_int("day", 10);
+        time_.hour = (float)props.get_float("hour", 15.0);
+        time_.minute = (float)props.get_float("minute", 0.0);
+        time_.second = (float)props.get_float("second", 0.0);
+        active_record_ = true;
+        float s[3];
+        compute_sun_coordinates(time_, location_, s);
+        if (s[2] < 0.f) warnings.push_back("The sun is below the horizon at the specified time and location!");
+        float3_ w = xform_vec(k_.to_world, mk3(s[0], s[1], s[2]));
+        sun_dir_[0] = w.x; sun_dir_[1] = w.y; sun_dir_[2] = w.z;
+    }
+    (void)props.find("dataset_path");  // consumed by the C-ABI layer
+
+    // ---------------- ctor body, sunsky.cpp:174-217
+    float3_ local = xform_vec(k_.to_local, mk3(sun_dir_[0], sun_dir_[1], sun_dir_[2]));
+    float lv[3] = {local.x, local.y, local.z};
+    update_angles(lv);
+    load_datasets(datasets);
+    stage();
+    k_.bs_center[0] = k_.bs_center[1] = k_.bs_center[2] = 0.f;   // unit bounding sphere until set_scene
+    k_.bs_radius = 1.f;
+
+    std::vector<std::string> unq = props.unqueried();
+    if (!unq.empty()) {
+        std::string s = "Unreferenced property \"" + unq[0] + "\" in sunsky plugin";
+        throw std::invalid_argument(s);
+    }
+}
+
+void SunskyModel::extract_albedo(const Properties& props) {
+    albedo_.assign(nch_, 0.f);
+    const Properties::Value* v = props.find("albedo");
+    if (!v) {
+        std::fill(albedo_.begin(), albedo_.end(), 0.3f);
+    } else if (v->type == Properties::Type::Float || v->type == Properties::Type::Int) {
+        float a = v->type == Properties::Type::Float ? (float)v->f : (float)v->i;
+        std::fill(albedo_.begin(), albedo_.end(), a);
+    } else if (v->type == Properties::Type::Spectrum) {
+        if ((int)v->a.size() == 1) std::fill(albedo_.begin(), albedo_.end(), v->a[0]);
+        else if ((int)v->a.size() == nch_) albedo_ = v->a;
+        else throw std::invalid_argument("albedo: expected 1 or " + std::to_string(nch_) + " values");
+    } else if (v->type == Properties::Type::Irregular) {
+        if (variant_ != kSpectral)
+            throw std::invalid_argument("irregular albedo spectra are only supported in spectral variants");
+        // IrregularSpectrum::eval at the model wavelengths (linear, 0 outside its range)
+        const std::vector<float>& wl = v->a;
+        const std::vector<float>& val = v->b;
+        if (wl.size() < 2 || wl.size() != val.size())
+            throw std::invalid_argument("irregular albedo spectrum needs >= 2 (wavelength, value) pairs");
+        for (int c = 0; c < nch_; ++c) {
+            float lam = kWavelength0 + kWavelengthStep * c, r = 0.f;
+            if (lam >= wl.front() && lam <= wl.back()) {
+                size_t i = 0;
+                while (i + 2 < wl.size() && wl[i + 1] < lam) ++i;
+                float w1 = (lam - wl[i]) / (wl[i + 1] - wl[i]), w0 = 1.f - w1;
+                r = fmaf(w0, val[i], w1 * val[i + 1]);
+            }
+            albedo_[c] = r;
+        }
+    } else {
+        throw std::invalid_argument("Expected a non-spatially varying radiance spectra!");
+    }
+    for (float a : albedo_)
+        if (a < 0.f || a > 1.f) throw std::invalid_argument(fmt("Albedo values must be in [0, 1], got: %f", a));
+}
+
+void SunskyModel::load_datasets(const std::string& where) {
+    const bool spec = variant_ == kSpectral;
+    auto check = [](const Table& t, size_t n, const char* name) {
+        if (t.size() != n) throw std::runtime_error(std::string("dataset '") + name + "' has an unexpected size");
+    };
+    Table sp, sr, sun, ld, tg;
+    std::string err;
+    if (is_dir(where)) {
+        // Reference layout: <dir>/{sky,sun}_{rgb,spec}_*.bin (path_to_dataset, sunsky.h:124-141)
+        std::string d = where + "/", ty = spec ? "_spec_" : "_rgb_";
+        if (!read_array_file(d + "sky" + ty + "params.bin", 2, &sp, &err) ||
+            !read_array_file(d + "sky" + ty + "rad.bin", 2, &sr, &err) ||
+            !read_array_file(d + "sun" + ty + "rad.bin", 2, &sun, &err) ||
+            !read_array_file(d + "sun_spec_ld.bin", 2, &ld, &err) ||
+            !read_array_file(d + "tgmm_tables.bin", 1, &tg, &err))
+            throw std::runtime_error(err);
+        // CIE Y at the model wavelengths (spectrum.cpp:158 table, 5 nm grid)
+        static const float cie_y_nodes[kNbWavelengths] = {0.f, 3.917e-06f, 0.000396f, 0.023f, 0.13902f,
+                                                          0.71f, 0.995f, 0.631f, 0.175f, 0.017f, 0.001047f};
+        std::memcpy(cie_y_, cie_y_nodes, sizeof(cie_y_));
+    } else {
+        DatasetPack pack;
+        Table cie;
+        if (!pack.open(where, &err) || !pack.get(spec ? "sky_spec_params" : "sky_rgb_params", &sp, &err) ||
+            !pack.get(spec ? "sky_spec_rad" : "sky_rgb_rad", &sr, &err) ||
+            !pack.get(spec ? "sun_spec_rad" : "sun_rgb_rad", &sun, &err) || !pack.get("sun_spec_ld", &ld, &err) ||
+            !pack.get("tgmm_tables", &tg, &err) || !pack.get("cie_y_nodes", &cie, &err))
+            throw std::runtime_error(err);
+        check(cie, kNbWavelengths, "cie_y_nodes");
+        for (int i = 0; i < kNbWavelengths; ++i) cie_y_[i] = (float)cie.data[i];
+    }
+    check(sp, (size_t)kNbTurbidity * kNbAlbedo * kNbSkyCtrlPts * nch_ * kNbSkyParams, "sky params");
+    check(sr, (size_t)kNbTurbidity * kNbAlbedo * kNbSkyCtrlPts * nch_, "sky radiance");
+    check(sun, (size_t)kNbTurbidity * (spec ? kSunSpecTableSize : kSunRgbTableSize), "sun radiance");
+    check(ld, (size_t)kNbWavelengths * kNbSunLdParams, "sun limb darkening");
+    check(tg, (size_t)(kNbTurbidity - 1) * kNbEtas * kNbGaussian * kNbGaussianParams, "tgmm tables");
+    sky_params_ds_ = to_f32(sp);
+    sky_rad_ds_ = to_f32(sr);
+    sun_rad_ds_ = to_f32(sun);
+    sun_ld_ = to_f32(ld);   // only read in spectral mode (sunsky.cpp:193-195)
+    tgmm_tables_ = to_f32(tg);
+}
+
+void SunskyModel::update_angles(const float l[3]) {
+    float3_ local = mk3(l[0], l[1], l[2]);
+    k_.sun_phi = atan2f(local.y, local.x);            // from_spherical, sunsky.h:84-89
+    k_.sun_theta = unit_angle_z(local);
+    float3_ s, t;
+    coordinate_system(local, &s, &t);                  // Frame3f(local_sun_dir)
+    k_.sun_n[0] = local.x; k_.sun_n[1] = local.y; k_.sun_n[2] = local.z;
+    k_.sun_s[0] = s.x; k_.sun_s[1] = s.y; k_.sun_s[2] = s.z;
+    k_.sun_t[0] = t.x; k_.sun_t[1] = t.y; k_.sun_t[2] = t.z;
+}
+
+void SunskyModel::stage() {
+    const bool spec = variant_ == kSpectral;
+    const float eta = 0.5f * kPi - k_.sun_theta;
+    k_.variant = variant_;
+    k_.semantics = semantics_;
+    k_.nch = nch_;
+    k_.sky_scale = sky_scale_;
+    k_.sun_scale = sun_scale_;
+    k_.half_aperture = sun_half_aperture_;
+    k_.cos_cutoff = cosf(sun_half_aperture_);
+    float sh = sinf(sun_half_aperture_);
+    k_.inv_sin2_half_ap = 1.f / (sh * sh);
+    // get_area_ratio, sunsky.h:99-101
+    k_.area_ratio = (1.f - cosf((float)(kSunHalfApertureDeg * (3.14159265358979323846 / 180.0)))) /
+                    (1.f - cosf(sun_half_aperture_));
+    k_.sun_pdf = kInvTwoPi / (1.f - k_.cos_cutoff);   // square_to_uniform_cone_pdf, warp.h:568-577
+
+    // ---------------- sky radiance (compute_radiance_params x2)
+    compute_radiance_params(sky_params_ds_, nch_, kNbSkyParams, albedo_, turbidity_, eta, &sky_params_);
+    compute_radiance_params(sky_rad_ds_, nch_, 1, albedo_, turbidity_, eta, &sky_rad_);
+    for (int c = 0; c < nch_; ++c) {
+        const float* p = &sky_params_[c * kNbSkyParams];
+        SkyChannel& ch = k_.sky[c];
+        ch.A = p[0]; ch.B = p[1]; ch.C = p[2]; ch.D = p[3]; ch.E = p[4];
+        ch.F = p[5]; ch.G = p[6]; ch.H = p[7]; ch.I = p[8];
+        ch.P = 1.f + ch.I * ch.I;
+        ch.rad = sky_rad_[c];
+        ch.Bl2 = (float)((double)ch.B * 1.4426950408889634074);
+        ch.El2 = (float)((double)ch.E * 1.4426950408889634074);
+        ch.Q = -2.f * ch.I;
+        ch.pad[0] = ch.pad[1] = 0.f;
+    }
+    // ---------------- sun radiance (compute_sun_params)
+    compute_sun_params(sun_rad_ds_, spec ? kSunSpecTableSize : kSunRgbTableSize, turbidity_, &sun_table_);
+
+    // ---------------- TGMM, sunsky.h:438-501
+    {
+        float eta_deg = eta * (float)(180.0 / 3.14159265358979323846);
+        float eta_idx_f = clipf_((eta_deg - 2.f) / 3.f, 0.f, (float)(kNbEtas - 1));
+        float t_idx_f = clipf_(turbidity_ - 2.f, 0.f, (float)(kNbTurbidity - 2));
+        int eta_lo = (int)floorf(eta_idx_f), t_lo = (int)floorf(t_idx_f);
+        int eta_hi = std::min(eta_lo + 1, kNbEtas - 1), t_hi = std::min(t_lo + 1, kNbTurbidity - 2);
+        float eta_rem = eta_idx_f - (float)eta_lo, t_rem = t_idx_f - (float)t_lo;
+        const int result_size = kNbGaussian * kNbGaussianParams, t_block = kNbEtas * result_size;
+        const int idx[4] = {t_lo * t_block + eta_lo * result_size, t_lo * t_block + eta_hi * result_size,
+                            t_hi * t_block + eta_lo * result_size, t_hi * t_block + eta_hi * result_size};
+        const float lf[4] = {(1 - t_rem) * (1 - eta_rem), (1 - t_rem) * eta_rem, t_rem * (1 - eta_rem),
+                             t_rem * eta_rem};
+        for (int m = 0; m < 4; ++m)
+            for (int i = 0; i < result_size; ++i) {
+                float v = tgmm_tables_[idx[m] + i];
+                if (i % kNbGaussianParams == kNbGaussianParams - 1) v = v * lf[m];
+                gauss_raw_[m * result_size + i] = v;
+            }
+        for (int g = 0; g < kNbMixture; ++g) {
+            const float* r = &gauss_raw_[g * kNbGaussianParams];
+            Gaussian& G = k_.gauss[g];
+            G.mu_phi = r[0]; G.mu_theta = r[1]; G.sigma_phi = r[2]; G.sigma_theta = r[3]; G.weight = r[4];
+            G.inv_sigma_phi = 1.f / r[2];
+            G.inv_sigma_theta = 1.f / r[3];
+            G.cdf_a_phi = gaussian_cdf(r[0], r[2], 0.f);
+            G.cdf_b_phi = gaussian_cdf(r[0], r[2], kTwoPi);
+            G.cdf_a_theta = gaussian_cdf(r[1], r[3], 0.f);
+            G.cdf_b_theta = gaussian_cdf(r[1], r[3], 0.5f * kPi);
+            float volume = (G.cdf_b_phi - G.cdf_a_phi) * (G.cdf_b_theta - G.cdf_a_theta) * (r[2] * r[3]);
+            G.coef = r[4] / volume;
+            k_.gauss_pmf[g] = r[4];
+        }
+        // DiscreteDistribution(mis_weights): JIT prefix_sum in fp32 (distr_1d.h:218-231),
+        // scalar accumulation in fp64 + first/last nonzero bounds (:233-265)
+        bool any_pos = false;
+        for (int g = 0; g < kNbMixture; ++g) {
+            if (k_.gauss_pmf[g] < 0.f) throw std::runtime_error("DiscreteDistribution: entries must be non-negative!");
+            any_pos |= k_.gauss_pmf[g] > 0.f;
+        }
+        if (!any_pos) throw std::runtime_error("DiscreteDistribution: no probability mass found!");
+        k_.gauss_first = -1;
+        k_.gauss_last = -1;
+        if (semantics_ == kJit) {
+            float acc = 0.f;
+            for (int g = 0; g < kNbMixture; ++g) { acc += k_.gauss_pmf[g]; k_.gauss_cdf[g] = acc; }
+            k_.gauss_first = 0;
+            k_.gauss_last = kNbMixture - 1;
+        } else {
+            double acc = 0.0;
+            for (int g = 0; g < kNbMixture; ++g) {
+                acc += (double)k_.gauss_pmf[g];
+                k_.gauss_cdf[g] = (float)acc;
+                if (k_.gauss_pmf[g] > 0.f) {
+                    if (k_.gauss_first < 0) k_.gauss_first = g;
+                    k_.gauss_last = g;
+                }
+            }
+        }
+        k_.gauss_sum = k_.gauss_cdf[k_.gauss_last];
+        k_.gauss_norm = 1.f / k_.gauss_sum;
+    }
+
+    k_.sun_table = nullptr;   // device pointers are patched in by the C-ABI layer
+    k_.sun_ld = nullptr;
+    estimate_sky_sun_ratio();
+}
+
+// estimate_sky_sun_ratio, sunsky.cpp:772-886
+void SunskyModel::estimate_sky_sun_ratio() {
+    const bool spec = variant_ == kSpectral;
+    if (semantics_ == kScalar) {
+        // Mean ratio + uniform spectral sampling (:778-783)
+        k_.w_sky = 0.5f;
+        if (spec) {
+            k_.spec_size = 2;
+            k_.spec_pdf[0] = k_.spec_pdf[1] = 1.f;
+            double interval = 720.0 - 360.0, integral = 0.5 * interval * 2.0;
+            k_.spec_cdf[0] = (float)integral;
+            k_.spec_interval = (float)interval;
+            k_.spec_integral = k_.spec_cdf[0];
+            k_.spec_norm = 1.f / k_.spec_integral;
+            k_.spec_inv_interval = 1.f / k_.spec_interval;
+        } else {
+            k_.spec_size = 0;
+        }
+        return;
+    }
+    constexpr int NQ = 200;
+    std::vector<double> xd, wd;
+    gauss_legendre(NQ, &xd, &wd);
+    float x[NQ], w[NQ];
+    for (int i = 0; i < NQ; ++i) { x[i] = (float)xd[i]; w[i] = (float)wd[i]; }
+    const float3_ sn = mk3(k_.sun_n[0], k_.sun_n[1], k_.sun_n[2]);
+    const float3_ ss = mk3(k_.sun_s[0], k_.sun_s[1], k_.sun_s[2]);
+    const float3_ st = mk3(k_.sun_t[0], k_.sun_t[1], k_.sun_t[2]);
+    float sky[kNbWavelengths] = {0}, sun[kNbWavelengths] = {0};
+    // Row partial sums in parallel, rows added in a fixed order: deterministic
+    // for any thread count.
+    std::vector<float> row_sky((size_t)NQ * nch_), row_sun((size_t)NQ * nch_);
+#pragma omp parallel for schedule(static)
+    for (int j = 0; j < NQ; ++j) {
+        // sky over the hemisphere: phi = pi (x+1), cos_theta = (x+1)/2
+        float cos_theta = 0.5f * (x[j] + 1.f);
+        float sin_theta = safe_sqrtf_(1.f - cos_theta * cos_theta);
+        // sun over its cone: cos_gamma = ((1-cc) x + (1+cc)) / 2
+        const float cc = k_.cos_cutoff;
+        float cos_gamma = 0.5f * ((1.f - cc) * x[j] + (1.f + cc));
+        float sin_gamma = safe_sqrtf_(1.f - cos_gamma * cos_gamma);
+        for (int c = 0; c < nch_; ++c) { row_sky[(size_t)j * nch_ + c] = 0.f; row_sun[(size_t)j * nch_ + c] = 0.f; }
+        for (int i = 0; i < NQ; ++i) {
+            float phi = kPi * (x[i] + 1.f);
+            float sp = sinf(phi), cp = cosf(phi);
+            float3_ wo = mk3(sin_theta * cp, sin_theta * sp, cos_theta);
+            float gamma = unit_angle(sn, wo);
+            for (int c = 0; c < nch_; ++c)
+                row_sky[(size_t)j * nch_ + c] += render_sky(k_.sky[c], cos_theta, gamma) * w[i] * w[j];
+            float3_ sw = mk3(sin_gamma * cp, sin_gamma * sp, cos_gamma);
+            float g2 = unit_angle_z(sw);
+            float3_ wl = frame_to_world(ss, st, sn, sw);
+            if (!(wl.z >= 0.f)) continue;
+            float xs;
+            int pos = sun_segment(wl.z, &xs);
+            float cpsi = cos_psi(g2, k_.inv_sin2_half_ap);
+            for (int c = 0; c < nch_; ++c) {
+                float v;
+                if (spec) {
+                    v = render_sun_spec(sun_table_.data(), pos, c, xs) * w[i] * w[j];
+                    v *= sun_limb_darkening(sun_ld_.data(), c, c, 0.f, cpsi);
+                } else {
+                    v = render_sun_rgb(sun_table_.data(), pos, c, xs, cpsi) * w[i] * w[j];
+                }
+                row_sun[(size_t)j * nch_ + c] += v;
+            }
+        }
+    }
+    for (int j = 0; j < NQ; ++j)
+        for (int c = 0; c < nch_; ++c) { sky[c] += row_sky[(size_t)j * nch_ + c]; sun[c] += row_sun[(size_t)j * nch_ + c]; }
+    const float J_sky = 0.5f * kPi, J_sun = 0.5f * kPi * (1.f - k_.cos_cutoff);
+    for (int c = 0; c < nch_; ++c) { sky[c] *= J_sky; sun[c] *= J_sun; }
+
+    float sky_lum = sky_scale_, sun_lum = sun_scale_;
+    if (!spec) {
+        auto lum = [](const float* c) { return c[0] * 0.212671f + c[1] * 0.715160f + c[2] * 0.072169f; };
+        sky_lum *= lum(sky);
+        sun_lum *= lum(sun) * k_.area_ratio * (float)kSpecToRgbSunConv;
+    } else {
+        float ls = 0.f, lu = 0.f;
+        for (int c = 0; c < kNbWavelengths; ++c) { ls += cie_y_[c] * sky[c]; lu += cie_y_[c] * sun[c]; }
+        sky_lum *= ls / (float)kNbWavelengths;
+        sun_lum *= lu / (float)kNbWavelengths * k_.area_ratio;
+    }
+    float res = sky_lum / (sky_lum + sun_lum);
+    if (std::isnan(res)) res = 0.f;
+    k_.w_sky = res;
+
+    if (spec) {
+        // ContinuousDistribution(range = [360, 720], avg_spec[1..10]), JIT compute_cdf (distr_1d.h:513-538)
+        const int size = kNbWavelengths - 1;
+        bool all_zero = true;
+        for (int i = 0; i < size; ++i) {
+            k_.spec_pdf[i] = sun[i + 1] + sky[i + 1];
+            all_zero &= k_.spec_pdf[i] == 0.f;
+        }
+        if (all_zero)
+            for (int i = 0; i < size; ++i) k_.spec_pdf[i] += 1.f;
+        for (int i = 0; i < size; ++i)
+            if (k_.spec_pdf[i] < 0.f) throw std::runtime_error("ContinuousDistribution: entries must be non-negative!");
+        k_.spec_size = size;
+        float interval = (720.f - 360.f) / (float)(size - 1), prefix = 0.f, pre[kNbWavelengths];
+        for (int i = 0; i < size; ++i) { prefix += k_.spec_pdf[i]; pre[i] = prefix; }
+        for (int i = 1; i < size; ++i)
+            k_.spec_cdf[i - 1] = interval * (pre[i] - 0.5f * k_.spec_pdf[0] - 0.5f * k_.spec_pdf[i]);
+        k_.spec_interval = interval;
+        k_.spec_integral = k_.spec_cdf[size - 2];
+        k_.spec_norm = 1.f / k_.spec_integral;
+        k_.spec_inv_interval = 1.f / interval;
+    } else {
+        k_.spec_size = 0;
+    }
+}
+
+void SunskyModel::validate() const {
+    if (sun_scale_ < 0.f) throw std::invalid_argument(fmt("Invalid sun scale: %f, must be positive!", sun_scale_));
+    if (sky_scale_ < 0.f) throw std::invalid_argument(fmt("Invalid sky scale: %f, must be positive!", sky_scale_));
+    if (turbidity_ < 1.f || 10.f < turbidity_)
+        throw std::invalid_argument(fmt("Turbidity value %f is out of range [1, 10]", turbidity_));
+    for (float a : albedo_)
+        if (a < 0.f || a > 1.f) throw std::invalid_argument(fmt("Albedo values must be in [0, 1], got: %f", a));
+}
+
+void SunskyModel::set_param(const std::string& name, const float* v, int count) {
+    auto need = [&](int n) {
+        if (count != n) throw std::invalid_argument("parameter '" + name + "' expects " + std::to_string(n) + " value(s)");
+    };
+    auto need_record = [&]() {
+        if (!active_record_) throw std::invalid_argument("parameter '" + name + "' is not exposed (sun_direction mode)");
+    };
+    if (name == "turbidity") { need(1); turbidity_ = v[0]; }
+    else if (name == "sky_scale") { need(1); sky_scale_ = v[0]; }
+    else if (name == "sun_scale") { need(1); sun_scale_ = v[0]; }
+    else if (name == "albedo") {
+        if (count == 1) std::fill(albedo_.begin(), albedo_.end(), v[0]);
+        else { need(nch_); albedo_.assign(v, v + nch_); }
+    }
+    else if (name == "latitude") { need_record(); need(1); location_.latitude = v[0]; }
+    else if (name == "longitude") { need_record(); need(1); location_.longitude = v[0]; }
+    else if (name == "timezone") { need_record(); need(1); location_.timezone = v[0]; }
+    else if (name == "year") { need_record(); need(1); time_.year = (int)v[0]; }
+    else if (name == "month") { need_record(); need(1); time_.month = (int)v[0]; }
+    else if (name == "day") { need_record(); need(1); time_.day = (int)v[0]; }
+    else if (name == "hour") { need_record(); need(1); time_.hour = v[0]; }
+    else if (name == "minute") { need_record(); need(1); time_.minute = v[0]; }
+    else if (name == "second") { need_record(); need(1); time_.second = v[0]; }
+    else if (name == "sun_direction") {
+        if (active_record_) throw std::invalid_argument("parameter 'sun_direction' is not exposed (time/location mode)");
+        need(3);
+        std::memcpy(sun_dir_, v, 3 * sizeof(float));
+    }
+    else if (name == "to_world") {
+        need(16);
+        std::memcpy(to_world_, v, sizeof(to_world_));
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) to_world_d_[r * 3 + c] = to_world_[r * 4 + c];
+        invert3(to_world_d_, to_local_d_);
+        for (int i = 0; i < 9; ++i) { k_.to_world[i] = (float)to_world_d_[i]; k_.to_local[i] = (float)to_local_d_[i]; }
+    k_.identity_xform = 1;
+    for (int i = 0; i < 9; ++i)
+        if (k_.to_world[i] != ((i % 4) == 0 ? 1.f : 0.f) || k_.to_local[i] != ((i % 4) == 0 ? 1.f : 0.f)) k_.identity_xform = 0;
+    }
+    else throw std::invalid_argument("unknown parameter '" + name + "'");
+}
+
+void SunskyModel::parameters_changed() {
+    validate();
+    float local[3];
+    if (active_record_) {
+        compute_sun_coordinates(time_, location_, local);
+        float3_ w = xform_vec(k_.to_world, mk3(local[0], local[1], local[2]));
+        sun_dir_[0] = w.x; sun_dir_[1] = w.y; sun_dir_[2] = w.z;
+    } else {
+        float3_ l = xform_vec(k_.to_local, mk3(sun_dir_[0], sun_dir_[1], sun_dir_[2]));
+        local[0] = l.x; local[1] = l.y; local[2] = l.z;
+    }
+    update_angles(local);
+    stage();
+}
+
+void SunskyModel::set_scene(bool bbox_valid, const float center[3], float radius) {
+    const float ray_eps = 5.9604644775390625e-08f * 1500.f;   // math::RayEpsilon<float>
+    if (bbox_valid) {
+        k_.bs_center[0] = center[0]; k_.bs_center[1] = center[1]; k_.bs_center[2] = center[2];
+        k_.bs_radius = std::max(ray_eps, radius * (1.f + ray_eps));
+    } else {
+        k_.bs_center[0] = k_.bs_center[1] = k_.bs_center[2] = 0.f;
+        k_.bs_radius = ray_eps;
+    }
+}
+
+std::string SunskyModel::to_string() const {
+    std::ostringstream oss;
+    oss << "SunskyEmitter[\n  bsphere = BoundingSphere3f[center = [" << k_.bs_center[0] << ", " << k_.bs_center[1]
+        << ", " << k_.bs_center[2] << "], radius = " << k_.bs_radius << "]\n  turbidity = " << turbidity_
+        << "\n  sky_scale = " << sky_scale_ << "\n  sun_scale = " << sun_scale_ << "\n  albedo = [";
+    for (size_t i = 0; i < albedo_.size(); ++i) oss << (i ? ", " : "") << albedo_[i];
+    oss << "]\n  sun aperture (\xc2\xb0) = " << 2.0 * sun_half_aperture_ * 180.0 / 3.14159265358979323846 << "\n";
+    if (active_record_)
+        oss << "  location = LocationRecord[latitude = " << location_.latitude << ", longitude = " << location_.longitude
+            << ", timezone = " << location_.timezone << "]\n  date_time = DateTimeRecord[year = " << time_.year
+            << ", month= " << time_.month << ", day = " << time_.day << ", hour = " << time_.hour
+            << ", minute = " << time_.minute << ", second = " << time_.second << "]\n";
+    else
+        oss << "  sun_dir = [" << sun_dir_[0] << ", " << sun_dir_[1] << ", " << sun_dir_[2] << "]\n";
+    oss << "]";
+    return oss.str();
+}
+
+}  // namespace sunsky

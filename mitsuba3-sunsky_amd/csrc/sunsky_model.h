@@ -1,0 +1,80 @@
+// sunsky_model.h -- host-side state and table staging of the sun/sky
+// emitter: the constructor / parameters_changed() work of the reference
+// (sunsky.cpp:162-301, 772-978; sunsky.h:158-501).  Produces a SunskyKArgs
+// block plus the two small device tables; owns no device memory itself.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "sunsky_dataset.h"
+#include "sunsky_props.h"
+#include "sunsky_types.h"
+
+namespace sunsky {
+
+struct DateTime { int year = 2010, month = 7, day = 10; float hour = 15.f, minute = 0.f, second = 0.f; };
+struct Location { float latitude = 35.6894f, longitude = 139.6917f, timezone = 9.f; };
+
+// compute_sun_coordinates, sunsky.h:284-374 (fp32, Int32 Julian-day arithmetic)
+void compute_sun_coordinates(const DateTime& t, const Location& l, float out[3]);
+// quad::gauss_legendre, quad.h:27-86 (fp64 nodes/weights)
+void gauss_legendre(int n, std::vector<double>* nodes, std::vector<double>* weights);
+
+class SunskyModel {
+public:
+    // SunskyEmitter(const Properties&), sunsky.cpp:162-218.  Throws std::invalid_argument /
+    // std::runtime_error with the reference's messages.
+    SunskyModel(const Properties& props, int variant, int semantics, const std::string& dataset_dir_or_pack);
+
+    // traverse() parameters (sunsky.cpp:220-240): turbidity, sky_scale, sun_scale,
+    // albedo (1 or nch values), latitude, longitude, timezone, year, day, month,
+    // hour, minute, second, sun_direction (3), to_world (16, row-major).
+    void set_param(const std::string& name, const float* v, int count);
+    // parameters_changed, sunsky.cpp:242-285
+    void parameters_changed();
+    // set_scene, sunsky.cpp:287-301
+    void set_scene(bool bbox_valid, const float center[3], float radius);
+
+    const SunskyKArgs& kargs() const { return k_; }
+    const std::vector<float>& sun_table() const { return sun_table_; }
+    const std::vector<float>& sun_ld() const { return sun_ld_; }
+    int variant() const { return variant_; }
+    int nch() const { return nch_; }
+    bool active_record() const { return active_record_; }
+    const float* sun_dir_world() const { return sun_dir_; }
+    float turbidity() const { return turbidity_; }
+    const std::vector<float>& albedo() const { return albedo_; }
+    const std::vector<float>& sky_params() const { return sky_params_; }
+    const std::vector<float>& sky_radiance() const { return sky_rad_; }
+    const float* gaussians_raw() const { return gauss_raw_; }
+    std::string to_string() const;
+    std::vector<std::string> warnings;
+
+private:
+    void load_datasets(const std::string& where);
+    void extract_albedo(const Properties& props);
+    void update_angles(const float local_sun[3]);
+    void stage();                 // radiance + sun + TGMM + sampling weight
+    void estimate_sky_sun_ratio();
+    void validate() const;
+
+    int variant_, semantics_, nch_;
+    // datasets (fp64 on disk -> fp32, array_from_file<Float64, Float>)
+    std::vector<float> sky_params_ds_, sky_rad_ds_, sun_rad_ds_, sun_ld_, tgmm_tables_;
+    float cie_y_[kNbWavelengths] = {0};
+    // parameters
+    float turbidity_ = 3.f, sky_scale_ = 1.f, sun_scale_ = 1.f, sun_half_aperture_ = 0.f;
+    std::vector<float> albedo_;
+    bool active_record_ = true;
+    DateTime time_;
+    Location location_;
+    float sun_dir_[3] = {0, 0, 1};   // world space (m_sun_dir)
+    float to_world_[16];
+    double to_world_d_[9], to_local_d_[9];
+    // staged
+    std::vector<float> sky_params_, sky_rad_, sun_table_;
+    float gauss_raw_[kNbMixture * kNbGaussianParams];
+    SunskyKArgs k_;
+};
+
+}  // namespace sunsky

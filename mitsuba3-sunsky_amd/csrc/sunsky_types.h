@@ -1,0 +1,104 @@
+// sunsky_types.h -- data layout shared by the host staging (C++) and the HIP
+// kernels.  Everything a kernel reads besides its ray batch travels in ONE
+// by-value kernel argument (SunskyKArgs) that the hardware places in the
+// kernarg segment: wave-uniform, fetched with s_load into SGPRs, snapshotted
+// per launch (so parameters_changed() can never race an in-flight launch).
+// Only the two sun tables (<=13 KB, read by the ~1e-5 of lanes that hit the
+// sun disc) live in device memory.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define SS_HD __host__ __device__
+#else
+#define SS_HD
+#endif
+
+namespace sunsky {
+
+// Model constants, include/mitsuba/render/sunsky/sunsky.h:19-62
+constexpr int kNbWavelengths = 11;    // NB_WAVELENGTHS
+constexpr int kNbTurbidity = 10;      // NB_TURBIDITY
+constexpr int kNbAlbedo = 2;          // NB_ALBEDO
+constexpr int kNbSkyCtrlPts = 6;      // NB_SKY_CTRL_PTS
+constexpr int kNbSkyParams = 9;       // NB_SKY_PARAMS
+constexpr int kNbSunCtrlPts = 4;      // NB_SUN_CTRL_PTS
+constexpr int kNbSunSegments = 45;    // NB_SUN_SEGMENTS
+constexpr int kNbSunLdParams = 6;     // NB_SUN_LD_PARAMS
+constexpr int kNbEtas = 30;           // NB_ETAS
+constexpr int kNbGaussian = 5;        // NB_GAUSSIAN
+constexpr int kNbGaussianParams = 5;  // NB_GAUSSIAN_PARAMS
+constexpr int kNbMixture = 4 * kNbGaussian;  // 4 corner mixtures (sunsky.h:462-474)
+constexpr float kWavelength0 = 320.f, kWavelengthStep = 40.f;  // sunsky.h:27-32
+constexpr double kSunHalfApertureDeg = 0.5358 / 2.0;           // SUN_HALF_APERTURE, sunsky.h:54
+constexpr double kSpecToRgbSunConv = 467.069280386;            // SPEC_TO_RGB_SUN_CONV, sunsky.h:62
+constexpr double kCieYNormalization = 1.0 / 106.7502593994140625;  // MI_CIE_Y_NORMALIZATION
+constexpr int kSunRgbTableSize = kNbSunSegments * 3 * kNbSunCtrlPts * kNbSunLdParams;    // 3240
+constexpr int kSunSpecTableSize = kNbSunSegments * kNbWavelengths * kNbSunCtrlPts;       // 1980
+constexpr int kMaxLambdaPerRay = 16;   // Mitsuba uses 4 (Spectrum<Float, 4>)
+constexpr int kMaxBroadcastLambda = 32;
+
+enum Variant : int { kRGB = 0, kSpectral = 1 };
+enum Semantics : int { kJit = 0, kScalar = 1 };
+
+// One sky channel (render_sky, sunsky.cpp:538-555) with the per-channel
+// constants of the formula folded on the host:
+//   c1  = 1 + A exp(B / (cos_theta + 0.01))
+//   chi = (1 + cos^2 g) / (1 + I^2 - 2 I cos g)^1.5
+//   c2  = C + D exp(E g) + F cos^2 g + G chi + H sqrt(cos_theta)
+//   L   = c1 c2 rad
+struct SkyChannel {
+    float A, B, C, D, E, F, G, H, I;
+    float P;     // 1 + I*I   (host fp32, same rounding as the per-lane reference op)
+    float rad;   // sky radiance of the channel
+    float Bl2;   // B * log2(e)   -- exp(B r) = exp2(Bl2 r)
+    float El2;   // E * log2(e)   -- exp(E g) = exp2(El2 g)
+    float Q;     // -2 I          -- 1 + I^2 - 2 I cos g = fma(Q, cos g, P)
+    float pad[2];
+};
+
+// One truncated Gaussian of the TGMM (sunsky.cpp:661-689, :732-763) with
+// its per-gaussian truncation constants hoisted out of the per-lane loop.
+struct Gaussian {
+    float mu_phi, mu_theta, sigma_phi, sigma_theta;
+    float weight;                          // mixture weight x corner lerp factor
+    float inv_sigma_phi, inv_sigma_theta;
+    float coef;                            // weight / volume, volume = (cdf_b-cdf_a).x (cdf_b-cdf_a).y sigma.x sigma.y
+    float cdf_a_phi, cdf_b_phi, cdf_a_theta, cdf_b_theta;  // gaussian_cdf at a=(0,0), b=(2pi, pi/2)
+};
+
+struct SunskyKArgs {
+    // -------- geometry
+    float to_world[9];       // 3x3 linear part of to_world (row-major)
+    float to_local[9];       // its inverse (transform_affine on vectors, transform.h:149-158)
+    float sun_n[3], sun_s[3], sun_t[3];   // local sun frame (Frame3f(local_sun_dir))
+    float sun_phi, sun_theta;             // m_sun_angles (from_spherical)
+    float cos_cutoff;        // cos(sun_half_aperture)
+    float half_aperture;     // m_sun_half_aperture
+    float inv_sin2_half_ap;  // 1 / sin^2(half_aperture)  (compute_cos_psi, sunsky.h:385-392)
+    float area_ratio;        // get_area_ratio(half_aperture)
+    float sky_scale, sun_scale;
+    float sun_pdf;           // InvTwoPi / (1 - cos_cutoff) (warp.h:568-577)
+    float w_sky;             // m_sky_sampling_w
+    float bs_center[3], bs_radius;        // bounding sphere (set_scene)
+    int   variant, semantics, nch;
+    int   identity_xform;      // to_world linear part == I: skip the 3x3 products
+    // -------- radiance
+    SkyChannel sky[kNbWavelengths];
+    const float* sun_table;  // device: 45x3x4x6 (RGB) or 45x11x4 (spectral), turbidity-lerped
+    const float* sun_ld;     // device: 11x6 limb darkening (spectral only)
+    // -------- sky sampling (TGMM + DiscreteDistribution)
+    Gaussian gauss[kNbMixture];
+    float gauss_cdf[kNbMixture];   // unnormalised inclusive prefix sum
+    float gauss_pmf[kNbMixture];
+    float gauss_sum, gauss_norm;
+    int   gauss_first, gauss_last; // scalar-variant search bounds (distr_1d.h:233-265)
+    // -------- wavelength sampling (ContinuousDistribution over [360, 720])
+    int   spec_size;               // 10 (JIT) / 2 (scalar) / 0 (RGB)
+    float spec_pdf[10], spec_cdf[9];
+    float spec_integral, spec_norm, spec_interval, spec_inv_interval;
+};
+
+static_assert(sizeof(SunskyKArgs) < 3072, "kernarg segment budget");
+
+}  // namespace sunsky

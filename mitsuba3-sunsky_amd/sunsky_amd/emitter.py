@@ -1,0 +1,410 @@
+"""Python face of the MI355X sun/sky emitter: the method names, arguments and
+errors of the reference `sunsky` plugin (src/emitters/sunsky.cpp) as exposed to
+Python by mitsuba (src/render/python/emitter_v.cpp:102-137), over the C ABI.
+
+Every batch method takes and returns torch tensors on the emitter's GPU in SoA
+layout ((3, n) vectors, (k, n) spectra) and runs on the current torch stream.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _capi
+from ._capi import Vec3In, Vec3Out, check, lib
+from .records import DirectionSample3f, Ray3f, ScalarBoundingBox3f
+
+_FLOAT_KEYS = ("turbidity", "sky_scale", "sun_scale", "sun_aperture", "latitude", "longitude",
+               "timezone", "hour", "minute", "second")
+_INT_KEYS = ("year", "month", "day")
+_VARIANTS = {"rgb": _capi.VARIANT_RGB, "spectral": _capi.VARIANT_SPECTRAL}
+_SEMANTICS = {"jit": _capi.SEMANTICS_JIT, "scalar": _capi.SEMANTICS_SCALAR}
+_PRECISION = {"fast": _capi.PRECISION_FAST, "reference": _capi.PRECISION_REFERENCE}
+
+
+def _fa(values):
+    arr = (C.c_float * len(values))(*[float(v) for v in values])
+    return arr
+
+
+def _build_props(d):
+    L = lib()
+    h = C.c_void_p()
+    check(L.sunsky_props_create(C.byref(h)))
+    try:
+        for key, val in d.items():
+            if key in ("type", "id"):
+                continue
+            k = key.encode()
+            if key == "sun_direction":
+                v = [float(x) for x in np.asarray(val, dtype=np.float64).reshape(-1)]
+                if len(v) != 3:
+                    raise ValueError("sun_direction needs 3 components")
+                check(L.sunsky_props_set_vector3(h, k, *v))
+            elif key == "to_world":
+                m = np.asarray(val, dtype=np.float32).reshape(-1)
+                if m.size != 16:
+                    raise ValueError("to_world needs a 4x4 matrix")
+                check(L.sunsky_props_set_transform(h, k, _fa(m)))
+            elif key == "albedo" and isinstance(val, dict):
+                t = val.get("type")
+                if t == "irregular":
+                    wl = [float(x) for x in str(val["wavelengths"]).split(",")]
+                    vs = [float(x) for x in str(val["values"]).split(",")]
+                    if len(wl) != len(vs):
+                        raise ValueError("irregular spectrum: wavelengths/values length mismatch")
+                    check(L.sunsky_props_set_irregular_spectrum(h, k, _fa(wl), _fa(vs), len(wl)))
+                elif t in ("rgb", "spectrum", "regular") and "value" in val:
+                    vs = np.atleast_1d(np.asarray(val["value"], dtype=np.float32)).tolist()
+                    check(L.sunsky_props_set_spectrum(h, k, _fa(vs), len(vs)))
+                elif t == "uniform":
+                    check(L.sunsky_props_set_float(h, k, float(val["value"])))
+                else:
+                    raise ValueError(f"unsupported albedo texture {val!r}")
+            elif key == "albedo" and np.ndim(val) > 0:
+                vs = np.asarray(val, dtype=np.float32).reshape(-1).tolist()
+                check(L.sunsky_props_set_spectrum(h, k, _fa(vs), len(vs)))
+            elif isinstance(val, (bool, np.bool_)):
+                raise ValueError(f"property '{key}' cannot be a boolean")
+            elif isinstance(val, (int, np.integer)) and key not in _FLOAT_KEYS:
+                check(L.sunsky_props_set_int(h, k, int(val)))
+            elif isinstance(val, (int, float, np.integer, np.floating)):
+                if key in _INT_KEYS and float(val) == int(val):
+                    check(L.sunsky_props_set_int(h, k, int(val)))
+                else:
+                    check(L.sunsky_props_set_float(h, k, float(val)))
+            else:
+                raise ValueError(f"unsupported value for property '{key}': {val!r}")
+    except Exception:
+        L.sunsky_props_destroy(h)
+        raise
+    return h
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p()
+
+
+class Parameters(dict):
+    """mi.traverse() result: assign, then update() -> parameters_changed()."""
+
+    def __init__(self, emitter, values):
+        super().__init__(values)
+        self._emitter = emitter
+        self._dirty = set()
+
+    def __setitem__(self, key, value):
+        if key not in self:
+            raise KeyError(f"unknown parameter '{key}'")
+        super().__setitem__(key, value)
+        self._dirty.add(key)
+
+    def update(self, *args, **kw):
+        if args or kw:
+            for k, v in dict(*args, **kw).items():
+                self[k] = v
+        for key in sorted(self._dirty):
+            v = np.atleast_1d(np.asarray(self[key], dtype=np.float32)).reshape(-1)
+            check(lib().sunsky_emitter_set_param(self._emitter._h, key.encode(), _fa(v.tolist()), v.size))
+        self._dirty.clear()
+        check(lib().sunsky_emitter_parameters_changed(self._emitter._h))
+        self._emitter._refresh_info()
+
+
+class SunskyEmitter:
+    """The `sunsky` emitter (sunsky.cpp:152-1037) on one MI355X.
+
+    variant   -- "rgb" | "spectral" (Mitsuba *_rgb / *_spectral variants)
+    semantics -- "jit" (llvm_/cuda_ variants: quadrature sampling weight) |
+                 "scalar" (scalar_ variants: weight 0.5, uniform wavelengths)
+    precision -- "fast" (host-folded transcendental constants) | "reference"
+    device    -- torch device for the tables, or "host" (staging only)
+    """
+
+    def __init__(self, props, variant="rgb", semantics="jit", dataset_path=None, precision="fast", device=None):
+        if props.get("type", "sunsky") != "sunsky":
+            raise ValueError(f"unsupported plugin type {props.get('type')!r}")
+        self.variant, self.semantics = variant, semantics
+        self.is_spectral = variant == "spectral"
+        self._props = dict(props)
+        self._h = None
+        host = device == "host"
+        self.device = None if host else torch.device(device if device is not None else "cuda")
+        if not host and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        ph = _build_props(props)
+        h = C.c_void_p()
+        try:
+            ds = dataset_path.encode() if dataset_path else None
+            if host:
+                check(lib().sunsky_emitter_create_host(ph, _VARIANTS[variant], _SEMANTICS[semantics], ds, C.byref(h)))
+            else:
+                with torch.cuda.device(self.device):
+                    check(lib().sunsky_emitter_create(ph, _VARIANTS[variant], _SEMANTICS[semantics], ds, C.byref(h)))
+        finally:
+            lib().sunsky_props_destroy(ph)
+        self._h = h
+        if precision != "fast":
+            self.set_precision(precision)
+        self._refresh_info()
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib().sunsky_emitter_destroy(h)
+            self._h = None
+
+    # ------------------------------------------------------------ state
+    def _refresh_info(self):
+        inf = _capi.Info()
+        check(lib().sunsky_emitter_get_info(self._h, C.byref(inf)))
+        self._info = inf
+
+    def set_precision(self, precision):
+        check(lib().sunsky_emitter_set_precision(self._h, _PRECISION[precision]))
+        self._refresh_info()
+
+    def info(self):
+        i = self._info
+        return {
+            "variant": i.variant, "semantics": i.semantics, "nb_channels": i.nb_channels,
+            "active_record": bool(i.active_record), "turbidity": i.turbidity, "sky_scale": i.sky_scale,
+            "sun_scale": i.sun_scale, "sun_half_aperture": i.sun_half_aperture, "cos_cutoff": i.cos_cutoff,
+            "area_ratio": i.area_ratio, "sun_dir_world": np.array(i.sun_dir_world),
+            "sun_dir_local": np.array(i.sun_dir_local), "sun_angles": np.array(i.sun_angles),
+            "w_sky": i.sky_sampling_w, "bsphere_center": np.array(i.bsphere_center),
+            "bsphere_radius": i.bsphere_radius, "flags": i.flags, "device": i.device,
+            "precision": "fast" if i.precision == _capi.PRECISION_FAST else "reference",
+        }
+
+    def table(self, name):
+        cnt = C.c_size_t()
+        tid = _capi.TABLES[name]
+        check(lib().sunsky_emitter_get_table(self._h, tid, None, 0, C.byref(cnt)))
+        buf = (C.c_float * max(cnt.value, 1))()
+        check(lib().sunsky_emitter_get_table(self._h, tid, buf, cnt.value, C.byref(cnt)))
+        return np.frombuffer(buf, dtype=np.float32, count=cnt.value).copy()
+
+    @property
+    def flags(self):
+        return self._info.flags
+
+    @property
+    def sky_sampling_w(self):
+        return self._info.sky_sampling_w
+
+    def bbox(self):
+        mn, mx = (C.c_float * 3)(), (C.c_float * 3)()
+        check(lib().sunsky_emitter_bbox(self._h, mn, mx))
+        return ScalarBoundingBox3f(tuple(mn), tuple(mx))
+
+    def set_scene(self, bbox_min=None, bbox_max=None):
+        """set_scene(scene) with the scene's bounding box (sunsky.cpp:287-301)."""
+        if bbox_min is None or bbox_max is None or any(a > b for a, b in zip(bbox_min, bbox_max)):
+            check(lib().sunsky_emitter_set_scene(self._h, 0, None, 0.0))
+        else:
+            mn, mx = np.asarray(bbox_min, np.float64), np.asarray(bbox_max, np.float64)
+            c = (mn + mx) / 2
+            r = float(np.linalg.norm(mx - c))   # BoundingBox::bounding_sphere
+            check(lib().sunsky_emitter_set_scene(self._h, 1, _fa(c.tolist()), r))
+        self._refresh_info()
+
+    def traverse(self):
+        """Parameters exposed by traverse() (sunsky.cpp:220-240)."""
+        inf = self.info()
+        vals = {"turbidity": inf["turbidity"], "sky_scale": inf["sky_scale"], "sun_scale": inf["sun_scale"],
+                "albedo": self.table("albedo")}
+        if inf["active_record"]:
+            for k in ("latitude", "longitude", "timezone", "year", "day", "month", "hour", "minute", "second"):
+                vals[k] = self._props.get(k, {"latitude": 35.6894, "longitude": 139.6917, "timezone": 9.0,
+                                              "year": 2010, "month": 7, "day": 10, "hour": 15.0, "minute": 0.0,
+                                              "second": 0.0}[k])
+        else:
+            vals["sun_direction"] = inf["sun_dir_world"]
+        vals["to_world"] = np.asarray(self._props.get("to_world", np.eye(4)), dtype=np.float32).reshape(4, 4)
+        return Parameters(self, vals)
+
+    def __repr__(self):
+        buf = C.create_string_buffer(4096)
+        check(lib().sunsky_emitter_to_string(self._h, buf, 4096))
+        return buf.value.decode()
+
+    # ------------------------------------------------------------ helpers
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _f32(self, t, rows=None):
+        if t is None:
+            return None
+        t = torch.as_tensor(t, dtype=torch.float32, device=self.device)
+        if rows is not None and t.dim() == 1 and rows == 1:
+            t = t.unsqueeze(0)
+        return t.contiguous()
+
+    def _mask(self, active, n):
+        if active is None or active is True:
+            return None
+        a = torch.as_tensor(active, device=self.device)
+        if a.dim() == 0:
+            a = a.expand(n)
+        return a.to(torch.uint8).contiguous()
+
+    def _vec_in(self, v):
+        v = self._f32(v)
+        if v.dim() != 2 or v.shape[0] != 3:
+            raise ValueError("vectors are SoA tensors of shape (3, n)")
+        return v, Vec3In(v[0].data_ptr(), v[1].data_ptr(), v[2].data_ptr())
+
+    def _wavelengths(self, wl, n):
+        wl = torch.as_tensor(wl, dtype=torch.float32, device=self.device)
+        if wl.dim() == 0:
+            wl = wl.expand(1, n)
+        elif wl.dim() == 1:
+            wl = wl.view(1, -1).expand(1, n) if wl.numel() == 1 else wl.view(1, n)
+        return wl.contiguous()
+
+    # ------------------------------------------------------------ hot path
+    def eval(self, si, active=None):
+        """eval(si, active) -- sunsky.cpp:303-352.  RGB -> (3, n); spectral -> (k, n)."""
+        return self._eval(si.wi, si.wavelengths, active, lib().sunsky_eval)
+
+    def eval_direction(self, it, ds, active=None):
+        """eval_direction(it, ds, active) -- sunsky.cpp:453-461 (wi = -ds.d)."""
+        wl = getattr(it, "wavelengths", None)
+        return self._eval(ds.d, wl, active, lib().sunsky_eval_direction)
+
+    def _eval(self, wi, wavelengths, active, fn):
+        wi, vin = self._vec_in(wi)
+        n = wi.shape[1]
+        m = self._mask(active, n)
+        if self.is_spectral:
+            if wavelengths is None:
+                raise ValueError("spectral eval needs si.wavelengths")
+            wl = self._wavelengths(wavelengths, n)
+            k = wl.shape[0]
+            out = torch.empty((k, n), dtype=torch.float32, device=self.device)
+            check(fn(self._h, vin, _ptr(wl), k, n, _ptr(m), n, _ptr(out), n, self._stream()))
+        else:
+            out = torch.empty((3, n), dtype=torch.float32, device=self.device)
+            check(fn(self._h, vin, None, 0, 0, _ptr(m), n, _ptr(out), n, self._stream()))
+        return out
+
+    def eval_spectral_broadcast(self, wi, wavelengths, active=None, out=None):
+        """Spectral eval of one wavelength list for every direction -> (m, n)."""
+        wi, vin = self._vec_in(wi)
+        n = wi.shape[1]
+        lam = [float(x) for x in np.atleast_1d(np.asarray(wavelengths, dtype=np.float32))]
+        if out is None:
+            out = torch.empty((len(lam), n), dtype=torch.float32, device=self.device)
+        m = self._mask(active, n)
+        check(lib().sunsky_eval_spectral_broadcast(self._h, vin, _fa(lam), len(lam), _ptr(m), n,
+                                                   _ptr(out), out.stride(0), self._stream()))
+        return out
+
+    def sample_direction(self, it, sample, active=None):
+        """sample_direction(it, sample, active) -- sunsky.cpp:399-441 -> (ds, weight)."""
+        sample = self._f32(sample)
+        if sample.dim() != 2 or sample.shape[0] != 2:
+            raise ValueError("sample is a (2, n) tensor")
+        n = sample.shape[1]
+        m = self._mask(active, n)
+        p = getattr(it, "p", None) if it is not None else None
+        if p is not None:
+            p, pin = self._vec_in(p)
+        else:
+            pin = Vec3In(None, None, None)
+        d = torch.empty((3, n), dtype=torch.float32, device=self.device)
+        pos = torch.empty((3, n), dtype=torch.float32, device=self.device)
+        pdf = torch.empty(n, dtype=torch.float32, device=self.device)
+        dist = torch.empty(n, dtype=torch.float32, device=self.device)
+        wl = None
+        k = 3
+        if self.is_spectral:
+            wl = self._wavelengths(getattr(it, "wavelengths", None), n)
+            k = wl.shape[0]
+        w = torch.empty((k, n), dtype=torch.float32, device=self.device)
+        check(lib().sunsky_sample_direction(
+            self._h, _ptr(sample[0]), _ptr(sample[1]), pin, _ptr(wl), k if self.is_spectral else 0, n,
+            _ptr(m), n, Vec3Out(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr()), _ptr(pdf), _ptr(dist),
+            Vec3Out(pos[0].data_ptr(), pos[1].data_ptr(), pos[2].data_ptr()), _ptr(w), n, self._stream()))
+        ds = DirectionSample3f(p=pos, n=-d, uv=sample, time=getattr(it, "time", None), pdf=pdf, delta=False,
+                               d=d, dist=dist, emitter=self)
+        return ds, w
+
+    def pdf_direction(self, it, ds, active=None):
+        """pdf_direction(it, ds, active) -- sunsky.cpp:443-451 -> (n,)."""
+        d, vin = self._vec_in(ds.d)
+        n = d.shape[1]
+        m = self._mask(active, n)
+        out = torch.empty(n, dtype=torch.float32, device=self.device)
+        check(lib().sunsky_pdf_direction(self._h, vin, _ptr(m), n, _ptr(out), self._stream()))
+        return out
+
+    def sample_ray(self, time, wavelength_sample, sample2, sample3, active=None):
+        """sample_ray(time, wavelength_sample, sample2, sample3, active) -- sunsky.cpp:354-397."""
+        s2, s3 = self._f32(sample2), self._f32(sample3)
+        n = s2.shape[1]
+        ws = self._f32(wavelength_sample)
+        if ws is not None and ws.dim() == 0:
+            ws = ws.expand(n).contiguous()
+        m = self._mask(active, n)
+        o = torch.empty((3, n), dtype=torch.float32, device=self.device)
+        d = torch.empty((3, n), dtype=torch.float32, device=self.device)
+        lam = torch.empty((4, n), dtype=torch.float32, device=self.device)
+        w = torch.empty((4 if self.is_spectral else 3, n), dtype=torch.float32, device=self.device)
+        check(lib().sunsky_sample_ray(
+            self._h, _ptr(ws), _ptr(s2[0]), _ptr(s2[1]), _ptr(s3[0]), _ptr(s3[1]), _ptr(m), n,
+            Vec3Out(o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr()),
+            Vec3Out(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr()), _ptr(lam), n, _ptr(w), n, self._stream()))
+        return Ray3f(o=o, d=d, time=time, wavelengths=lam), w
+
+    def sample_wavelengths(self, si, sample, active=None):
+        """sample_wavelengths(si, sample, active) -- sunsky.cpp:463-480."""
+        wi, vin = self._vec_in(si.wi)
+        n = wi.shape[1]
+        s = self._f32(sample)
+        if s is not None and s.dim() == 0:
+            s = s.expand(n).contiguous()
+        m = self._mask(active, n)
+        lam = torch.empty((4, n), dtype=torch.float32, device=self.device)
+        w = torch.empty((4 if self.is_spectral else 3, n), dtype=torch.float32, device=self.device)
+        check(lib().sunsky_sample_wavelengths(self._h, vin, _ptr(s), _ptr(m), n, _ptr(lam), n, _ptr(w), n,
+                                              self._stream()))
+        return lam, w
+
+    def sample_position(self, time=None, sample=None, active=None):
+        """sample_position -- NotImplementedError like the scalar reference (sunsky.cpp:483-495)."""
+        check(lib().sunsky_sample_position(self._h))
+
+
+def load_dict(d, variant="rgb", semantics="jit", **kw):
+    """mi.load_dict({'type': 'sunsky', ...}) counterpart."""
+    if d.get("type") != "sunsky":
+        raise ValueError(f"unsupported plugin type {d.get('type')!r} (only 'sunsky')")
+    return SunskyEmitter(d, variant=variant, semantics=semantics, **kw)
+
+
+def array_from_file(path, file_dtype=0):
+    """array_from_file_d/_f (sunsky_v.cpp:16-17) -> (float64 ndarray with the file's shape)."""
+    cnt = C.c_size_t()
+    shape = (C.c_uint64 * 16)()
+    nd = C.c_int()
+    check(lib().sunsky_array_from_file(str(path).encode(), file_dtype, None, 0, C.byref(cnt), shape, C.byref(nd)))
+    buf = (C.c_double * max(cnt.value, 1))()
+    check(lib().sunsky_array_from_file(str(path).encode(), file_dtype, buf, cnt.value, C.byref(cnt), shape, C.byref(nd)))
+    return np.frombuffer(buf, dtype=np.float64, count=cnt.value).reshape([shape[i] for i in range(nd.value)]).copy()
+
+
+def array_to_file(path, data, shape=None):
+    """array_to_file (sunsky_v.cpp:18)."""
+    arr = np.ascontiguousarray(np.asarray(data, dtype=np.float32).reshape(-1))
+    sh = list(shape) if shape else [arr.size]
+    shp = (C.c_uint64 * len(sh))(*sh)
+    check(lib().sunsky_array_to_file(str(path).encode(), arr.ctypes.data_as(C.POINTER(C.c_float)), arr.size, shp,
+                                     len(sh)))
+
+
+def default_dataset_path():
+    buf = C.create_string_buffer(4096)
+    check(lib().sunsky_default_dataset_path(buf, 4096))
+    return buf.value.decode()

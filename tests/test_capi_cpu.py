@@ -1,0 +1,132 @@
+"""CPU-side checks of the product boundary: the C-ABI library loads and
+exports every symbol include/sunsky_amd.h declares, and the host staging
+(no device) matches the oracle's restatement of the reference staging."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+import sunsky_amd as ss
+from helpers import SPECIAL_ALBEDO, angles_dict, hour_dict
+
+REF_DATASETS = "/root/reference/resources/sunsky/datasets"
+
+
+def test_library_exports_every_declared_symbol():
+    L = ctypes.CDLL(ss.LIB_PATH)
+    declared = ss.declared_functions()
+    assert len(declared) >= 30
+    missing = [f for f in declared if not hasattr(L, f)]
+    assert not missing, missing
+    assert ss.lib().sunsky_abi_version() == 1
+    assert os.path.exists(ss.CODE_OBJECT), "gfx950 code object not built"
+
+
+def test_default_dataset_path_resolves_to_bundled_pack():
+    p = ss.default_dataset_path()
+    assert os.path.exists(p) and p.endswith("sunsky_datasets.pack")
+
+
+CASES = [
+    ("rgb", "jit", hour_dict(3, 11.7753, 0.1, 1.0, 1.0)),
+    ("rgb", "jit", angles_dict(2.0, 0.3, np.deg2rad(45), 0.1, 1.0, 1.0)),
+    ("rgb", "scalar", angles_dict(6.0, -1.2, np.deg2rad(70), 0.5, 1.0, 1.0)),
+    ("rgb", "jit", angles_dict(10.0, 2.0, np.deg2rad(20), [0.1, 0.5, 0.9], 0.7, 1.3)),
+    ("spectral", "jit", angles_dict(3.0, 0.0, np.deg2rad(30), 0.3, 1.0, 1.0)),
+    ("spectral", "jit", angles_dict(4.2, 0.0, np.deg2rad(30), SPECIAL_ALBEDO, 1.0, 1.0)),
+    ("spectral", "scalar", hour_dict(5.2, 9.5, 0.2, 1.0, 1.0)),
+    ("rgb", "jit", dict(angles_dict(3.0, 0.5, np.deg2rad(40), 0.3, 1.0, 1.0), sun_aperture=30.0)),
+]
+
+
+@pytest.mark.parametrize("variant,semantics,d", CASES)
+def test_host_staging_matches_oracle(variant, semantics, d):
+    em = ss.SunskyEmitter(d, variant=variant, semantics=semantics, device="host")
+    o = O.Oracle(d, variant, semantics, "f32").info()
+    inf = em.info()
+    np.testing.assert_allclose(inf["sun_dir_world"], o["sun_dir_world"], rtol=0, atol=2e-7)
+    np.testing.assert_allclose(inf["sun_angles"], o["sun_angles"], rtol=0, atol=2e-7)
+    nch = 11 if variant == "spectral" else 3
+    np.testing.assert_allclose(em.table("sky_params").reshape(nch, 9), o["sky_params"], rtol=2e-6, atol=1e-6)
+    np.testing.assert_allclose(em.table("sky_radiance"), o["sky_radiance"], rtol=2e-6)
+    sun = em.table("sun_radiance")
+    np.testing.assert_array_equal(sun, O.Oracle(d, variant, semantics, "f32").sun_table())
+    np.testing.assert_allclose(em.table("gaussians").reshape(20, 5), o["gaussians"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(em.table("gaussian_cdf"), o["gauss_cdf"], rtol=1e-6)
+    # The sampling weight is a 200x200 fp32 quadrature: summation order differs
+    assert abs(inf["w_sky"] - o["w_sky"]) <= 2e-5 * max(1e-3, abs(o["w_sky"]))
+    if variant == "spectral":
+        np.testing.assert_allclose(em.table("spectral_pdf"), o["spec_pdf"], rtol=2e-5)
+        np.testing.assert_allclose(em.table("spectral_cdf"), o["spec_cdf"], rtol=2e-5)
+    assert inf["flags"] == (0x04 | 0x10)
+
+
+def test_parameter_errors_match_reference_messages():
+    with pytest.raises(ValueError, match="Turbidity value"):
+        ss.SunskyEmitter({"turbidity": 0.5}, device="host")
+    with pytest.raises(ValueError, match="Invalid sun scale"):
+        ss.SunskyEmitter({"sun_scale": -1.0}, device="host")
+    with pytest.raises(ValueError, match="Invalid sky scale"):
+        ss.SunskyEmitter({"sky_scale": -1.0}, device="host")
+    with pytest.raises(ValueError, match="Invalid sun aperture"):
+        ss.SunskyEmitter({"sun_aperture": 180.0}, device="host")
+    with pytest.raises(ValueError, match="Albedo values must be in"):
+        ss.SunskyEmitter({"albedo": 1.5}, device="host")
+    with pytest.raises(ValueError, match="Both the 'sun_direction'"):
+        ss.SunskyEmitter({"sun_direction": [0, 0, 1], "hour": 12.0}, device="host")
+    with pytest.raises(ValueError, match="Unreferenced property"):
+        ss.SunskyEmitter({"turbidty": 3.0}, device="host")
+    with pytest.raises(FileNotFoundError):
+        ss.SunskyEmitter({}, device="host", dataset_path="/nonexistent/sunsky.pack")
+
+
+def test_parameters_changed_restages_like_construction():
+    d = angles_dict(3.0, 0.2, np.deg2rad(50), 0.3, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, device="host")
+    params = em.traverse()
+    params["turbidity"] = 7.5
+    params["albedo"] = 0.6
+    params.update()
+    d2 = dict(d, turbidity=7.5, albedo=0.6)
+    fresh = ss.SunskyEmitter(d2, device="host")
+    np.testing.assert_array_equal(em.table("sky_params"), fresh.table("sky_params"))
+    np.testing.assert_array_equal(em.table("sun_radiance"), fresh.table("sun_radiance"))
+    assert em.sky_sampling_w == fresh.sky_sampling_w
+    with pytest.raises(ValueError, match="Turbidity"):
+        params["turbidity"] = 20.0
+        params.update()
+
+
+def test_time_location_parameters_update_sun():
+    em = ss.SunskyEmitter(hour_dict(3, 12.0, 0.2, 1.0, 1.0), device="host")
+    p = em.traverse()
+    p["hour"] = 17.0
+    p.update()
+    ref = O.sun_coordinates(hour=17.0)
+    np.testing.assert_allclose(em.info()["sun_dir_world"], ref, atol=2e-7)
+
+
+def test_array_file_roundtrip(tmp_path):
+    data = np.arange(24, dtype=np.float32) * 0.5
+    f = tmp_path / "t.bin"
+    ss.array_to_file(f, data, (2, 3, 4))
+    back = ss.array_from_file(f)
+    assert back.shape == (2, 3, 4)
+    np.testing.assert_array_equal(back.reshape(-1), data)
+    raw = open(f, "rb").read()
+    assert raw[:3] == b"SKY"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_DATASETS), reason="reference tree not mounted (GPU box)")
+def test_reference_bin_directory_equals_bundled_pack():
+    for variant in ("rgb", "spectral"):
+        d = angles_dict(4.0, 0.0, np.deg2rad(35), 0.25, 1.0, 1.0)
+        a = ss.SunskyEmitter(d, variant=variant, device="host")
+        b = ss.SunskyEmitter(d, variant=variant, device="host", dataset_path=REF_DATASETS)
+        for t in ("sky_params", "sky_radiance", "sun_radiance", "gaussians"):
+            np.testing.assert_array_equal(a.table(t), b.table(t))
+        assert a.sky_sampling_w == b.sky_sampling_w
+    arr = ss.array_from_file(os.path.join(REF_DATASETS, "sky_rgb_rad.bin"))
+    assert arr.shape == (10, 2, 6, 3)

@@ -1,0 +1,9 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, short bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; steps are chained with &&.
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -m pytest tests -m gpu -x -q -rs > gpurun_out/pytest_gpu.log 2>&1 && \
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
+timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/bench.log 2>&1

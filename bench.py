@@ -58,24 +58,25 @@ def hemisphere_dirs(n, seed, device):
 
 
 class KernelTimer:
-    """HIP events on the stream the C ABI launches on (torch's current stream)."""
+    """HIP events on the stream the C ABI launches on (torch's current stream),
+    bracketing a burst of back-to-back launches: mean duration per launch
+    (dispatch gaps included, so it is an upper bound on the rocprof average)."""
 
     def __init__(self):
-        self.pairs = []
+        self.launches = 0
+        self.t0 = torch.cuda.Event(enable_timing=True)
+        self.t1 = torch.cuda.Event(enable_timing=True)
 
-    def start(self):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        return e
+    def begin(self):
+        self.t0.record()
 
-    def stop(self, s):
-        e = torch.cuda.Event(enable_timing=True)
-        e.record()
-        self.pairs.append((s, e))
+    def end(self, launches):
+        self.t1.record()
+        self.launches = launches
 
     def mean_ms(self):
         torch.cuda.synchronize()
-        return float(np.mean([a.elapsed_time(b) for a, b in self.pairs])) if self.pairs else float("nan")
+        return self.t0.elapsed_time(self.t1) / max(self.launches, 1)
 
 
 def pmc_traffic(path, kernel_prefix):
@@ -173,14 +174,11 @@ def main():
     vin = ss._capi.Vec3In(wi[0].data_ptr(), wi[1].data_ptr(), wi[2].data_ptr())
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    def step(timer=None):
+    def step():
         for em, out in zip(ems, outs):
-            s = timer.start() if timer else None
             rc = lib.sunsky_eval(em._h, vin, None, 0, 0, None, n, out.data_ptr(), n, stream)
             if rc:
                 raise RuntimeError(lib.sunsky_last_error().decode())
-            if timer:
-                timer.stop(s)
 
     for _ in range(args.warmup):
         step()
@@ -189,8 +187,10 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    timer.begin()
     for _ in range(args.steps):
-        step(timer)
+        step()
+    timer.end(args.steps * len(TURBIDITIES))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -235,10 +235,11 @@ def main():
         for _ in range(2):
             spec.eval_spectral_broadcast(wi, lams, out=spec_out)
         tm = KernelTimer()
-        for _ in range(max(3, args.steps // 4)):
-            s = tm.start()
+        reps = max(3, args.steps // 4)
+        tm.begin()
+        for _ in range(reps):
             spec.eval_spectral_broadcast(wi, lams, out=spec_out)
-            tm.stop(s)
+        tm.end(reps)
         ms = tm.mean_ms()
         sec["spectral_eval_C3"] = {"evals_per_s": 11 * n / (ms * 1e-3), "kernel_ms": ms,
                                    "achieved_GBps": BYTES_SPEC_PER_DIR * n / (ms * 1e-3) / 1e9,
@@ -256,11 +257,12 @@ def main():
             ds, w = smp.sample_direction(it, u)
             pdf = smp.pdf_direction(it, ds)
         tm = KernelTimer()
-        for _ in range(max(3, args.steps // 4)):
-            s = tm.start()
+        reps = max(3, args.steps // 4)
+        tm.begin()
+        for _ in range(reps):
             ds, w = smp.sample_direction(it, u)
             pdf = smp.pdf_direction(it, ds)
-            tm.stop(s)
+        tm.end(reps)
         ms = tm.mean_ms()
         sec["sampling_C4"] = {"samples_per_s": ns / (ms * 1e-3), "ms": ms, "samples": ns,
                               "achieved_GBps": BYTES_SAMPLE * ns / (ms * 1e-3) / 1e9,

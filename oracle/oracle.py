@@ -257,6 +257,12 @@ class Oracle:
                                _ptr(lam), _ptr(w))
         return {"o": o.T.copy(), "d": d.T.copy(), "wavelengths": lam.T.copy(), "weight": w.T.copy()}
 
+    def override_w_sky(self, w_sky):
+        """Adopt the product's staged sampling weight so sampling parity isolates the kernels."""
+        f = self._fn("override_w_sky")
+        f.argtypes = [C.c_void_p, C.c_double]
+        f(self._h, float(w_sky))
+
     def hw_sun_radiance(self, turbidity, wavelength, elevation, gamma):
         return self._fn("hw_sun_radiance")(self._h, turbidity, wavelength, elevation, gamma)
 

@@ -97,6 +97,8 @@ void oracle_sun_coordinates(int year, int month, int day, float hour, float minu
                            const float *s2x, const float *s2y, const float *s3x,                 \
                            const float *s3y, size_t n, R *ox, R *oy, R *oz, R *dx, R *dy,        \
                            R *dz, R *lambda_out, R *weight);                                     \
+    /* test hook: adopt another implementation's staged sky/sun sampling weight */             \
+    void oracle_override_w_sky_##SFX(oracle_##SFX *o, double w_sky);                            \
     /* HW solar radiance (restates ArHosekSkyModel.c:686-784 on the packed tables) */          \
     R oracle_hw_sun_radiance_##SFX(const oracle_##SFX *o, R turbidity, R wavelength,            \
                            R elevation, R gamma);

@@ -194,31 +194,38 @@ def test_sample_direction_and_pdf_parity(variant, semantics, precision):
     it = ss.Interaction3f(wavelengths=torch.from_numpy(lam).cuda() if variant == "spectral" else None)
     ds, w = em.sample_direction(it, soa(u))
     gd, gp = host(ds.d).T, host(ds.pdf)
+    # w_sky is a 200x200 fp32 quadrature staged independently on both sides
+    # (staging parity: tests/test_capi_cpu.py); adopt the product's value so the
+    # comparison isolates the sampling kernels.
+    w_o = em.sky_sampling_w
+    o32.override_w_sky(w_o)
     ref = o32.sample_direction(u, wavelengths=lam if variant == "spectral" else None)
-    # w_sky is staged independently on both sides (200x200 fp32 quadrature): a
-    # sample within 1e-6 of the sky/sun split may legitimately switch branch.
-    w_g, w_o = em.sky_sampling_w, o32.info()["w_sky"]
-    near_split = np.abs(u[:, 0] - w_o) < 4e-6 + abs(w_g - w_o)
-    ok = ~near_split
+    ok = np.ones(n, bool)
     dir_err = np.abs(gd - ref["d"]).max(axis=1)
-    # erfinv is steep near +-1: compare directions with an absolute 2e-5 bar
-    assert np.quantile(dir_err[ok], 0.999) < 2e-6
-    assert dir_err[ok].max() < 1e-4
-    close = ok & (dir_err < 1e-6)
-    assert max_rel(gp[close], ref["pdf"][close]) < 2e-5
-    # pdf_direction on the GPU's own sampled directions vs the oracle on the same directions
-    pd = host(em.pdf_direction(ss.Interaction3f(), ds))
+    # same sample -> same direction up to transcendental rounding (erfinv is steep near +-1)
+    assert np.quantile(dir_err, 0.999) < 2e-6
+    assert dir_err.max() < 1e-4
+    # Values are compared at the GPU's own directions: near the zenith (1/sin theta) and the
+    # horizon (exp(B / (cos theta + 0.01))) a 1e-7 direction rounding moves pdf / radiance by
+    # up to 1e-4 relative, which is conditioning, not kernel error.
+    info = o32.info()
+    inside_sun = (gd @ info["sun_dir_local"]) >= info["cos_cutoff"]
+    pick_sky = u[:, 0] < w_o
     pref = o32.pdf_direction(gd)
+    same_formula = pick_sky | inside_sun      # sun picks skip the cone test (sunsky.cpp:720)
+    assert max_rel(gp[same_formula], pref[same_formula]) < 1e-5
+    # pdf_direction kernel vs oracle on identical inputs
+    pd = host(em.pdf_direction(ss.Interaction3f(), ds))
     assert max_rel(pd, pref) < 1e-5
-    # sample_direction's pdf equals pdf_direction's for sky-sampled directions
-    sky = ok & (u[:, 0] < w_o)
-    inside_sun = (gd @ o32.info()["sun_dir_local"]) >= o32.info()["cos_cutoff"]
-    np.testing.assert_allclose(gp[sky & ~inside_sun], pd[sky & ~inside_sun], rtol=1e-6)
+    # weight = eval(-d) / pdf (sunsky.cpp:438-439) on identical inputs
     gw = host(w).T
     assert np.all(np.isfinite(gw))
-    sunl = inside_sun
-    assert_parity(gw[close & ~sunl], ref["weight"][close & ~sunl], ref["weight"][close & ~sunl], np.zeros((close & ~sunl).sum(), bool),
-                  rtol=3e-5)
+    e32 = o32.eval(-gd, lam if variant == "spectral" else None)
+    e64 = o64.eval(-gd, lam if variant == "spectral" else None)
+    e32, e64 = (e32.T, e64.T) if variant == "spectral" else (e32, e64)
+    wref32 = (e32 / gp[:, None]).astype(np.float32)
+    wref64 = e64 / gp[:, None].astype(np.float64)
+    assert_parity(gw, wref32, wref64, inside_sun, rtol=2e-5)
 
 
 @pytest.mark.parametrize("variant", ["rgb", "spectral"])
@@ -234,8 +241,9 @@ def test_sample_ray_parity(variant):
     s2 = rng.random((n, 2), dtype=np.float32)
     s3 = rng.random((n, 2), dtype=np.float32)
     ray, w = em.sample_ray(None, torch.from_numpy(ws).cuda(), soa(s2), soa(s3))
+    o32.override_w_sky(em.sky_sampling_w)
     ref = o32.sample_ray(ws, s2, s3)
-    ok = np.abs(s3[:, 0] - o32.info()["w_sky"]) > 1e-5
+    ok = np.ones(n, bool)
     assert np.abs(host(ray.d).T - ref["d"])[ok].max() < 1e-4
     assert np.quantile(np.abs(host(ray.o).T - ref["o"])[ok].max(axis=1), 0.999) < 1e-4
     if variant == "spectral":

@@ -95,13 +95,13 @@ std::string code_object_path() {
 
 // ---------------------------------------------------------------- kernels
 enum KernelId {
-    K_EVAL_RGB_V4, K_EVAL_RGB_V1, K_EVAL_SPEC_BCAST_V4, K_EVAL_SPEC_BCAST_V1, K_EVAL_SPEC_RAYS,
-    K_SAMPLE_DIRECTION, K_PDF_DIRECTION, K_SAMPLE_WAVELENGTHS, K_SAMPLE_RAY, K_COUNT
+    K_EVAL_RGB_V4, K_EVAL_RGB_V1, K_EVAL_SPEC_BCAST_V2, K_EVAL_SPEC_BCAST_V1, K_EVAL_SPEC_NODES_V2,
+    K_EVAL_SPEC_RAYS, K_SAMPLE_DIRECTION, K_PDF_DIRECTION, K_SAMPLE_WAVELENGTHS, K_SAMPLE_RAY, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
-    "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
-    "sunsky_eval_spec_rays", "sunsky_sample_direction", "sunsky_pdf_direction", "sunsky_sample_wavelengths",
-    "sunsky_sample_ray"};
+    "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v2", "sunsky_eval_spec_bcast_v1",
+    "sunsky_eval_spec_nodes_v2", "sunsky_eval_spec_rays", "sunsky_sample_direction", "sunsky_pdf_direction",
+    "sunsky_sample_wavelengths", "sunsky_sample_ray"};
 
 struct DeviceModule {
     hipModule_t module = nullptr;
@@ -152,6 +152,7 @@ void launch(hipFunction_t f, unsigned grid, hipStream_t stream, void** args) {
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+bool aligned8(const void* p) { return ((uintptr_t)p & 7u) == 0; }
 
 struct LambdaSet {   // mirrors the kernel-side struct
     int m;
@@ -445,23 +446,28 @@ int sunsky_eval_spectral_broadcast(const sunsky_emitter* e, sunsky_vec3_in w, co
         L.lo[k] = lo;
         L.f[k] = valid ? nw - (float)lo : -1.f;
     }
+    // The 11 model wavelengths 320:40:720 in order: compile-time channel kernel.
+    bool nodes = m == kNbWavelengths;
+    for (int k = 0; nodes && k < m; ++k) nodes = L.lo[k] == k && L.f[k] == 0.f;
     return guarded([&] {
         hipStream_t s = (hipStream_t)stream;
         SunskyKArgs K = e->kargs;
         float sign = -1.f;
-        bool vec = n >= 4 && aligned16(w.x) && aligned16(w.y) && aligned16(w.z) && aligned16(out) &&
-                   (ostride % 4) == 0 && (!active || ((uintptr_t)active & 3u) == 0);
-        size_t n4 = vec ? (n & ~(size_t)3) : 0;
-        if (n4) {
+        // VEC = 2 (8-byte lanes): the spectral kernels are VALU-bound, so the
+        // smaller vector keeps more waves resident (DESIGN.md "Kernels").
+        bool vec = n >= 2 && aligned8(w.x) && aligned8(w.y) && aligned8(w.z) && aligned8(out) &&
+                   (ostride % 2) == 0 && (!active || ((uintptr_t)active & 1u) == 0);
+        size_t n2 = vec ? (n & ~(size_t)1) : 0;
+        if (n2) {
             const float *x = w.x, *y = w.y, *z = w.z;
-            void* args[] = {&K, &L, &x, &y, &z, &active, &n4, &out, &ostride, &sign};
-            launch(e->fn(K_EVAL_SPEC_BCAST_V4), grid_for(e->mod, n4 / 4), s, args);
+            void* args[] = {&K, &L, &x, &y, &z, &active, &n2, &out, &ostride, &sign};
+            launch(e->fn(nodes ? K_EVAL_SPEC_NODES_V2 : K_EVAL_SPEC_BCAST_V2), grid_for(e->mod, n2 / 2), s, args);
         }
-        if (n4 < n) {
-            const float *x = w.x + n4, *y = w.y + n4, *z = w.z + n4;
-            const uint8_t* a = active ? active + n4 : nullptr;
-            float* o = out + n4;
-            size_t rem = n - n4;
+        if (n2 < n) {
+            const float *x = w.x + n2, *y = w.y + n2, *z = w.z + n2;
+            const uint8_t* a = active ? active + n2 : nullptr;
+            float* o = out + n2;
+            size_t rem = n - n2;
             void* args[] = {&K, &L, &x, &y, &z, &a, &rem, &o, &ostride, &sign};
             launch(e->fn(K_EVAL_SPEC_BCAST_V1), grid_for(e->mod, rem), s, args);
         }

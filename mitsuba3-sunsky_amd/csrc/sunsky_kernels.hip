@@ -3,21 +3,25 @@
 // Compiled to a standalone code object (hipcc --genco --offload-arch=gfx950)
 // and loaded by the C-ABI layer with hipModuleLoad / hipModuleGetFunction.
 //
-// Design (DESIGN.md "Kernels"):
-//  * one direction per lane, VEC = 4 consecutive directions per lane so every
-//    global access is a 16-byte-per-lane dwordx4 (1 KiB per wave instruction);
-//  * SoA fp32 rays in HBM (x[], y[], z[] planes), SoA outputs (one plane per
-//    channel / wavelength);
+// Design (DESIGN.md "Kernels"; numbers from tools/kbench.cpp on MI355X):
+//  * SoA fp32 rays in HBM (x[], y[], z[] planes) and SoA outputs (one plane per
+//    channel / wavelength); VEC consecutive directions per lane so global
+//    accesses are 16 B (RGB, VEC = 4) or 8 B (spectral, VEC = 2) per lane.
+//    Plain loads + non-temporal stores measured fastest (RGB eval 68 us for
+//    16M directions = 5.9 TB/s);
 //  * every per-emitter constant arrives in the by-value SunskyKArgs kernarg
-//    block -> s_load -> SGPRs; tables that lanes index with DIFFERENT
-//    indices (TGMM components, per-ray spectral channels) are staged in LDS;
-//  * the sun disc (~1e-5 of random directions) runs behind an exec-masked
-//    branch that waves skip when no lane hits it; its 13 KB table is read
-//    from L2.
-//  * FAST = 1 folds the transcendental constants on the host (exp -> exp2
-//    with log2(e)-prescaled coefficients, pow(x,1.5) -> x * rsqrt(x) chains,
-//    cos(unit_angle) -> 1 - 2 h^2 identity); FAST = 0 follows the reference
-//    operation order with full-precision libm calls.  Both are parity-tested.
+//    block (s_load -> SGPRs); tables that lanes index with DIFFERENT indices
+//    (TGMM components, per-ray spectral channels, the sun polynomials in the
+//    sampling kernels where ~(1 - w_sky) of the lanes hit the sun) are staged
+//    in LDS once per workgroup;
+//  * the sun disc (~1e-5 of random directions in eval) runs behind an
+//    exec-masked branch that waves skip when no lane hits it, with rolled
+//    loops so its registers do not lower the sky path's occupancy;
+//  * FAST = true folds constants on the host (exp -> exp2 of log2(e)-scaled
+//    coefficients, radiance x sky_scale (x CIE normalisation) into the
+//    channel coefficients, pow(b, 1.5) -> rsq(b)^3, cos(unit_angle) ->
+//    1 - 2 h^2, hardware sqrt); FAST = false follows the reference operation
+//    order with full-precision libm.  Both are parity-tested against the oracle.
 #include <hip/hip_runtime.h>
 
 #include "sunsky_math.h"
@@ -28,13 +32,20 @@ using namespace sunsky;
 #define SS_BLOCK 256
 constexpr float kLog2e = 1.44269504088896340736f;
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 // ------------------------------------------------------------------ helpers
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 __device__ __forceinline__ float fast_rsq(float x) { return __builtin_amdgcn_rsqf(x); }
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+
+template <bool FAST> struct ChanSel { using T = SkyChannel; };
+template <> struct ChanSel<true> { using T = FastChannel; };
 
 struct DirTerms {
-    float cos_theta, gamma, cg, cg2;
+    float cos_theta, gamma, cg, cg2, u;   // u = 1 + cos^2 gamma
     float r;        // 1 / (cos_theta + 0.01)
     float sq;       // safe_sqrt(cos_theta)
     bool active, hit_sun;
@@ -47,46 +58,58 @@ __device__ __forceinline__ DirTerms dir_terms(const SunskyKArgs& K, float3_ wo, 
     const float3_ sn = mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]);
     t.cos_theta = wo.z;
     float d = dot3(sn, wo);
-    // unit_angle(n, wo): 2 asin(|wo -/+ n| / 2)
+    // unit_angle(n, wo) = 2 asin(|wo -/+ n| / 2)
     float3_ v = mk3(wo.x - mulsignf_(sn.x, d), wo.y - mulsignf_(sn.y, d), wo.z - mulsignf_(sn.z, d));
-    float h = 0.5f * sqrtf(dot3(v, v));
+    float h = 0.5f * (FAST ? fast_sqrt(dot3(v, v)) : sqrtf(dot3(v, v)));
     float temp = 2.f * asinf(h);
     t.gamma = d >= 0.f ? temp : kPi - temp;
     if (FAST) {
-        // cos(2 asin h) = 1 - 2 h^2 ; cos(pi - 2 asin h) = -(1 - 2 h^2)
-        float c = fmaf(-2.f * h, h, 1.f);
+        float c = fmaf(-2.f * h, h, 1.f);   // cos(2 asin h) = 1 - 2 h^2 ; cos(pi - x) = -cos x
         t.cg = d >= 0.f ? c : -c;
         t.r = fast_rcp(t.cos_theta + 0.01f);
+        t.sq = fast_sqrt(fmaxf(t.cos_theta, 0.f));
     } else {
         t.cg = cosf(t.gamma);
         t.r = 1.f / (t.cos_theta + 0.01f);
+        t.sq = safe_sqrtf_(t.cos_theta);
     }
     t.cg2 = t.cg * t.cg;
-    t.sq = safe_sqrtf_(t.cos_theta);
+    t.u = 1.f + t.cg2;
     t.active = mask && (t.cos_theta >= 0.f);
     t.hit_sun = t.active && (d >= K.cos_cutoff);
     return t;
 }
 
-// render_sky for one channel, sunsky.cpp:538-555
+// render_sky (sunsky.cpp:538-555) with the output scale folded in (FastChannel)
+__device__ __forceinline__ float sky_fast(const FastChannel& k, const DirTerms& t) {
+    float c1 = fmaf(k.A, fast_exp2(k.Bl2 * t.r), 1.f);
+    float rs = fast_rsq(fmaf(k.Q, t.cg, k.P));        // (1 + I^2 - 2 I cos g)^-1/2
+    float w = rs * rs * rs;
+    float c2 = fmaf(k.Ds, fast_exp2(k.El2 * t.gamma), k.Cs);
+    c2 = fmaf(k.Fs, t.cg2, c2);
+    c2 = fmaf(k.Gs, t.u * w, c2);
+    c2 = fmaf(k.Hs, t.sq, c2);
+    return c1 * c2;
+}
+
+// render_sky, reference operation order (sunsky.cpp:550-554), times sky_scale
+__device__ __forceinline__ float sky_ref(const SkyChannel& k, const DirTerms& t, float sky_scale) {
+    float c1 = 1.f + k.A * expf(k.B * t.r);
+    float chi = t.u / powf(1.f + k.I * k.I - 2.f * k.I * t.cg, 1.5f);
+    float c2 = k.C + k.D * expf(k.E * t.gamma) + k.F * t.cg2 + k.G * chi + k.H * t.sq;
+    return sky_scale * (c1 * c2 * k.rad);
+}
+
 template <bool FAST>
-__device__ __forceinline__ float sky_channel(const SkyChannel& k, const DirTerms& t) {
-    if (FAST) {
-        float c1 = fmaf(k.A, fast_exp2(k.Bl2 * t.r), 1.f);
-        float b = fmaf(k.Q, t.cg, k.P);                 // 1 + I^2 - 2 I cos g
-        float rs = fast_rsq(b);
-        float chi = (1.f + t.cg2) * (rs * rs * rs);      // / b^1.5
-        float c2 = fmaf(k.D, fast_exp2(k.El2 * t.gamma), k.C);
-        c2 = fmaf(k.F, t.cg2, c2);
-        c2 = fmaf(k.G, chi, c2);
-        c2 = fmaf(k.H, t.sq, c2);
-        return c1 * c2 * k.rad;
-    } else {
-        float c1 = 1.f + k.A * expf(k.B * t.r);
-        float chi = (1.f + t.cg2) / powf(1.f + k.I * k.I - 2.f * k.I * t.cg, 1.5f);
-        float c2 = k.C + k.D * expf(k.E * t.gamma) + k.F * t.cg2 + k.G * chi + k.H * t.sq;
-        return c1 * c2 * k.rad;
-    }
+__device__ __forceinline__ float sky_eval(const typename ChanSel<FAST>::T& k, const DirTerms& t, float sky_scale) {
+    if constexpr (FAST) { (void)sky_scale; return sky_fast(k, t); }
+    else return sky_ref(k, t, sky_scale);
+}
+
+template <bool FAST>
+__device__ __forceinline__ const typename ChanSel<FAST>::T* chan_table(const SunskyKArgs& K) {
+    if constexpr (FAST) return K.fsky;
+    else return K.sky;
 }
 
 __device__ __forceinline__ float3_ to_local(const SunskyKArgs& K, float3_ v) {
@@ -96,70 +119,111 @@ __device__ __forceinline__ float3_ to_world(const SunskyKArgs& K, float3_ v) {
     return K.identity_xform ? v : xform_vec(K.to_world, v);
 }
 
-// Full RGB eval for one local direction (sunsky.cpp:317-323): out[3]
-template <bool FAST>
-__device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, float3_ wo, bool mask, float out[3]) {
-    DirTerms t = dir_terms<FAST>(K, wo, mask);
-    const float cie = (float)kCieYNormalization;
+// render_sun RGB branch (sunsky.cpp:597-611) as nested Horner forms:
+// sum_k x^k (sum_j cos_psi^j S[k][j]) -- 6 table values live at a time.
+__device__ __forceinline__ float render_sun_rgb_compact(const float* table, int pos, int c, float x, float cpsi) {
+    const float* s = table + pos * (3 * kNbSunCtrlPts * kNbSunLdParams) + c * (kNbSunCtrlPts * kNbSunLdParams);
+    float res = 0.f;
+#pragma unroll 1
+    for (int k = kNbSunCtrlPts - 1; k >= 0; --k) {
+        const float* r = s + k * kNbSunLdParams;
+        float inner = r[kNbSunLdParams - 1];
 #pragma unroll
-    for (int c = 0; c < 3; ++c) out[c] = K.sky_scale * sky_channel<FAST>(K.sky[c], t);
-    if (t.hit_sun) {
-        float xs;
-        int pos = sun_segment(t.cos_theta, &xs);
-        float cpsi = cos_psi(t.gamma, K.inv_sin2_half_ap);
-        const float conv = (float)kSpecToRgbSunConv;
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-            out[c] += K.sun_scale * render_sun_rgb(K.sun_table, pos, c, xs, cpsi) * K.area_ratio * conv;
+        for (int j = kNbSunLdParams - 2; j >= 0; --j) inner = fmaf(inner, cpsi, r[j]);
+        res = fmaf(res, x, inner);
     }
-#pragma unroll
-    for (int c = 0; c < 3; ++c) out[c] = t.active ? out[c] * cie : 0.f;
+    return res;
 }
 
-// Spectral eval of one wavelength for one direction (sunsky.cpp:325-348) with the
-// channel table in LDS (lanes index different channels).
+// Full RGB eval for one local direction (sunsky.cpp:317-323).
 template <bool FAST>
-__device__ __forceinline__ float eval_spec_one(const SunskyKArgs& K, const SkyChannel* sky, const DirTerms& t,
+__device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const float* sun_tab, float3_ wo, bool mask,
+                                               float out[3]) {
+    DirTerms t = dir_terms<FAST>(K, wo, mask);
+    if constexpr (FAST) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) out[c] = sky_fast(K.fsky[c], t);   // sky_scale and CIE folded
+        if (t.hit_sun) {
+            float xs;
+            int pos = sun_segment(t.cos_theta, &xs);
+            float cpsi = cos_psi(t.gamma, K.inv_sin2_half_ap);
+#pragma unroll 1
+            for (int c = 0; c < 3; ++c) out[c] += K.sun_mul * render_sun_rgb_compact(sun_tab, pos, c, xs, cpsi);
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) out[c] = t.active ? out[c] : 0.f;
+    } else {
+        const float cie = (float)kCieYNormalization;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) out[c] = sky_ref(K.sky[c], t, K.sky_scale);
+        if (t.hit_sun) {
+            float xs;
+            int pos = sun_segment(t.cos_theta, &xs);
+            float cpsi = cos_psi(t.gamma, K.inv_sin2_half_ap);
+            const float conv = (float)kSpecToRgbSunConv;
+#pragma unroll 1
+            for (int c = 0; c < 3; ++c)
+                out[c] += K.sun_scale * render_sun_rgb(sun_tab, pos, c, xs, cpsi) * K.area_ratio * conv;
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) out[c] = t.active ? out[c] * cie : 0.f;
+    }
+}
+
+// Spectral sun disc term for channel pair (lo, hi, f): lerp(sun) x limb darkening
+// (sunsky.cpp:341-347); hi = 11 at exactly 720 nm carries weight 0.
+template <bool FAST>
+__device__ __forceinline__ float sun_spec_term(const SunskyKArgs& K, const float* sun_tab, const float* ld_tab,
+                                               const DirTerms& t, int lo, float f) {
+    const int hi = lo + 1;
+    float xs;
+    int pos = sun_segment(t.cos_theta, &xs);
+    float sa = render_sun_spec(sun_tab, pos, lo, xs), sun = sa;
+    if (f != 0.f) sun = lerpf_(sa, hi < kNbWavelengths ? render_sun_spec(sun_tab, pos, hi, xs) : 0.f, f);
+    float ld = sun_limb_darkening(ld_tab, lo, hi, f, cos_psi(t.gamma, K.inv_sin2_half_ap));
+    return FAST ? K.sun_mul * (sun * ld) : K.sun_scale * sun * ld * K.area_ratio;
+}
+
+// Spectral eval of one per-lane wavelength (sunsky.cpp:325-348); `chans` is
+// indexed by a per-lane channel, so it lives in LDS.
+template <bool FAST>
+__device__ __forceinline__ float eval_spec_one(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
+                                               const float* sun_tab, const float* ld_tab, const DirTerms& t,
                                                float lambda) {
     float nw = (lambda - kWavelength0) / kWavelengthStep;
     bool valid = (0.f <= nw) && (nw <= (float)(kNbWavelengths - 1));
     if (!(t.active && valid)) return 0.f;
     int lo = (int)floorf(nw), hi = lo + 1;
     float f = nw - (float)lo;
-    float a = sky_channel<FAST>(sky[lo], t);
-    float res = a;
-    if (f != 0.f) res = lerpf_(a, hi < kNbWavelengths ? sky_channel<FAST>(sky[hi], t) : 0.f, f);
-    res = K.sky_scale * res;
-    if (t.hit_sun) {
-        float xs;
-        int pos = sun_segment(t.cos_theta, &xs);
-        float sa = render_sun_spec(K.sun_table, pos, lo, xs);
-        float sun = sa;
-        if (f != 0.f) sun = lerpf_(sa, hi < kNbWavelengths ? render_sun_spec(K.sun_table, pos, hi, xs) : 0.f, f);
-        float cpsi = cos_psi(t.gamma, K.inv_sin2_half_ap);
-        float ld = sun_limb_darkening(K.sun_ld, lo, hi, f, cpsi);
-        res += K.sun_scale * sun * ld * K.area_ratio;
-    }
+    float res = sky_eval<FAST>(chans[lo], t, K.sky_scale);
+    if (f != 0.f) res = lerpf_(res, hi < kNbWavelengths ? sky_eval<FAST>(chans[hi], t, K.sky_scale) : 0.f, f);
+    if (t.hit_sun) res += sun_spec_term<FAST>(K, sun_tab, ld_tab, t, lo, f);
     return res;
 }
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
+// ------------------------------------------------------------ memory helpers
 template <int VEC>
 __device__ __forceinline__ void load_vec(const float* p, size_t i, float v[VEC]) {
     if constexpr (VEC == 4) {
-        f32x4 q = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + i));
+        f32x4 q = *reinterpret_cast<const f32x4*>(p + i);
         v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+    } else if constexpr (VEC == 2) {
+        f32x2 q = *reinterpret_cast<const f32x2*>(p + i);
+        v[0] = q.x; v[1] = q.y;
     } else {
-        v[0] = __builtin_nontemporal_load(p + i);
+        v[0] = p[i];
     }
 }
 
+// Outputs are written once and not re-read by this kernel: non-temporal.
 template <int VEC>
 __device__ __forceinline__ void store_vec(float* p, size_t i, const float v[VEC]) {
     if constexpr (VEC == 4) {
         f32x4 q = {v[0], v[1], v[2], v[3]};
         __builtin_nontemporal_store(q, reinterpret_cast<f32x4*>(p + i));
+    } else if constexpr (VEC == 2) {
+        f32x2 q = {v[0], v[1]};
+        __builtin_nontemporal_store(q, reinterpret_cast<f32x2*>(p + i));
     } else {
         __builtin_nontemporal_store(v[0], p + i);
     }
@@ -176,9 +240,22 @@ __device__ __forceinline__ void load_mask(const uint8_t* m, size_t i, bool v[VEC
         uint32_t q = *reinterpret_cast<const uint32_t*>(m + i);
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = ((q >> (8 * j)) & 0xFF) != 0;
+    } else if constexpr (VEC == 2) {
+        uint16_t q = *reinterpret_cast<const uint16_t*>(m + i);
+        v[0] = (q & 0xFF) != 0;
+        v[1] = (q >> 8) != 0;
     } else {
         v[0] = m[i] != 0;
     }
+}
+
+template <int VEC>
+__device__ __forceinline__ void load_dirs(const float* wx, const float* wy, const float* wz, const uint8_t* active,
+                                          size_t i, float x[VEC], float y[VEC], float z[VEC], bool m[VEC]) {
+    load_vec<VEC>(wx, i, x);
+    load_vec<VEC>(wy, i, y);
+    load_vec<VEC>(wz, i, z);
+    load_mask<VEC>(active, i, m);
 }
 
 // ======================================================================
@@ -196,14 +273,11 @@ __device__ __forceinline__ void eval_rgb_body(const SunskyKArgs& K, const float*
         const size_t i = v * VEC;
         float x[VEC], y[VEC], z[VEC], r[VEC], g[VEC], b[VEC];
         bool m[VEC];
-        load_vec<VEC>(wx, i, x);
-        load_vec<VEC>(wy, i, y);
-        load_vec<VEC>(wz, i, z);
-        load_mask<VEC>(active, i, m);
+        load_dirs<VEC>(wx, wy, wz, active, i, x, y, z, m);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
             float o[3];
-            eval_rgb_local<FAST>(K, to_local(K, mk3(sign * x[j], sign * y[j], sign * z[j])), m[j], o);
+            eval_rgb_local<FAST>(K, K.sun_table, to_local(K, mk3(sign * x[j], sign * y[j], sign * z[j])), m[j], o);
             r[j] = o[0]; g[j] = o[1]; b[j] = o[2];
         }
         store_vec<VEC>(out, i, r);
@@ -214,9 +288,9 @@ __device__ __forceinline__ void eval_rgb_body(const SunskyKArgs& K, const float*
 
 // ======================================================================
 // eval(): spectral, one wavelength set broadcast to every direction (the
-// test02/03 eval_full_spec layout and the C3 bench workload).  Wavelength k
-// maps to channels (lo[k], hi[k], f[k]) computed on the host: wave-uniform,
-// so the channel constants come from SGPRs.  out plane k at out + k*ostride.
+// test02/03 eval_full_spec layout and the C3 workload).  Wavelength k maps
+// to channels (lo[k], lo[k] + 1, f[k]) computed on the host: wave-uniform, so
+// the channel constants come from SGPRs.  out plane k at out + k * ostride.
 // ======================================================================
 struct LambdaSet {
     int m;
@@ -229,16 +303,14 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
                                                      const float* __restrict__ wx, const float* __restrict__ wy,
                                                      const float* __restrict__ wz, const uint8_t* __restrict__ active,
                                                      size_t n, float* __restrict__ out, size_t ostride, float sign) {
+    const auto* chans = chan_table<FAST>(K);
     const size_t nvec = n / VEC;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
         const size_t i = v * VEC;
         float x[VEC], y[VEC], z[VEC];
         bool m[VEC];
-        load_vec<VEC>(wx, i, x);
-        load_vec<VEC>(wy, i, y);
-        load_vec<VEC>(wz, i, z);
-        load_mask<VEC>(active, i, m);
+        load_dirs<VEC>(wx, wy, wz, active, i, x, y, z, m);
         DirTerms t[VEC];
         bool any_sun = false;
 #pragma unroll
@@ -254,40 +326,21 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o[j] = 0.f;
             } else {
-                const SkyChannel& cl = K.sky[lo];
 #pragma unroll
-                for (int j = 0; j < VEC; ++j) {
-                    float a = sky_channel<FAST>(cl, t[j]);
-                    o[j] = a;
-                }
+                for (int j = 0; j < VEC; ++j) o[j] = sky_eval<FAST>(chans[lo], t[j], K.sky_scale);
                 if (f != 0.f) {
-                    const int hi = lo + 1;
-                    if (hi < kNbWavelengths) {
-                        const SkyChannel& ch = K.sky[hi];
+                    if (lo + 1 < kNbWavelengths) {
 #pragma unroll
-                        for (int j = 0; j < VEC; ++j) o[j] = lerpf_(o[j], sky_channel<FAST>(ch, t[j]), f);
+                        for (int j = 0; j < VEC; ++j) o[j] = lerpf_(o[j], sky_eval<FAST>(chans[lo + 1], t[j], K.sky_scale), f);
                     } else {
 #pragma unroll
                         for (int j = 0; j < VEC; ++j) o[j] = lerpf_(o[j], 0.f, f);
                     }
                 }
-#pragma unroll
-                for (int j = 0; j < VEC; ++j) o[j] = K.sky_scale * o[j];
                 if (any_sun) {
 #pragma unroll
-                    for (int j = 0; j < VEC; ++j) {
-                        if (t[j].hit_sun) {
-                            const int hi = lo + 1;
-                            float xs;
-                            int pos = sun_segment(t[j].cos_theta, &xs);
-                            float sa = render_sun_spec(K.sun_table, pos, lo, xs), sun = sa;
-                            if (f != 0.f)
-                                sun = lerpf_(sa, hi < kNbWavelengths ? render_sun_spec(K.sun_table, pos, hi, xs) : 0.f, f);
-                            float cpsi = cos_psi(t[j].gamma, K.inv_sin2_half_ap);
-                            float ld = sun_limb_darkening(K.sun_ld, lo, hi, f, cpsi);
-                            o[j] += K.sun_scale * sun * ld * K.area_ratio;
-                        }
-                    }
+                    for (int j = 0; j < VEC; ++j)
+                        if (t[j].hit_sun) o[j] += sun_spec_term<FAST>(K, K.sun_table, K.sun_ld, t[j], lo, f);
                 }
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o[j] = t[j].active ? o[j] : 0.f;
@@ -297,51 +350,117 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
     }
 }
 
-// ======================================================================
-// eval(): spectral with per-ray wavelengths (Mitsuba Spectrum<Float, k>):
-// lambda plane k at lam + k*lstride, out plane k at out + k*ostride.
-// ======================================================================
-__device__ __forceinline__ void stage_sky_lds(const SunskyKArgs& K, SkyChannel* sky) {
-    const int nwords = (int)(kNbWavelengths * sizeof(SkyChannel) / 4);
-    const float* src = reinterpret_cast<const float*>(K.sky);
-    float* dst = reinterpret_cast<float*>(sky);
-    for (int w = threadIdx.x; w < nwords; w += blockDim.x) dst[w] = src[w];
-    __syncthreads();
+// Broadcast at exactly the 11 model wavelengths 320:40:720 nm (lerp factor 0,
+// sunsky.cpp:332-343): channel c -> plane c with compile-time channel indices.
+template <int VEC, bool FAST>
+__device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const float* __restrict__ wx,
+                                                     const float* __restrict__ wy, const float* __restrict__ wz,
+                                                     const uint8_t* __restrict__ active, size_t n,
+                                                     float* __restrict__ out, size_t ostride, float sign) {
+    const auto* chans = chan_table<FAST>(K);
+    const size_t nvec = n / VEC;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+        const size_t i = v * VEC;
+        float x[VEC], y[VEC], z[VEC];
+        bool m[VEC];
+        load_dirs<VEC>(wx, wy, wz, active, i, x, y, z, m);
+        DirTerms t[VEC];
+        bool any_sun = false;
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            t[j] = dir_terms<FAST>(K, to_local(K, mk3(sign * x[j], sign * y[j], sign * z[j])), m[j]);
+            any_sun |= t[j].hit_sun;
+        }
+#pragma unroll
+        for (int c = 0; c < kNbWavelengths; ++c) {
+            float o[VEC];
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) o[j] = sky_eval<FAST>(chans[c], t[j], K.sky_scale);
+            if (any_sun) {
+#pragma unroll
+                for (int j = 0; j < VEC; ++j)
+                    if (t[j].hit_sun) o[j] += sun_spec_term<FAST>(K, K.sun_table, K.sun_ld, t[j], c, 0.f);
+            }
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) o[j] = t[j].active ? o[j] : 0.f;
+            store_vec<VEC>(out + (size_t)c * ostride, i, o);
+        }
+    }
 }
 
+// ======================================================================
+// Tables staged in LDS once per workgroup
+// ======================================================================
+struct SpecLds {
+    FastChannel fast[kNbWavelengths];
+    SkyChannel ref[kNbWavelengths];
+};
+
+template <typename T>
+__device__ __forceinline__ void lds_copy(T* dst, const T* src, int count) {
+    const int nwords = (int)(count * sizeof(T) / 4);
+    const float* s = reinterpret_cast<const float*>(src);
+    float* d = reinterpret_cast<float*>(dst);
+    for (int w = threadIdx.x; w < nwords; w += blockDim.x) d[w] = s[w];
+}
+
+template <bool FAST>
+__device__ __forceinline__ const typename ChanSel<FAST>::T* stage_chans(const SunskyKArgs& K, SpecLds* s) {
+    if constexpr (FAST) { lds_copy(s->fast, K.fsky, kNbWavelengths); return s->fast; }
+    else { lds_copy(s->ref, K.sky, kNbWavelengths); return s->ref; }
+}
+
+// ======================================================================
+// eval(): spectral with per-ray wavelengths (Mitsuba Spectrum<Float, k>):
+// lambda plane k at lam + k * lstride, out plane k at out + k * ostride.
+// ======================================================================
 template <bool FAST>
 __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                                     const float* __restrict__ wy, const float* __restrict__ wz,
                                                     const float* __restrict__ lam, size_t lstride, int nlam,
                                                     const uint8_t* __restrict__ active, size_t n,
                                                     float* __restrict__ out, size_t ostride, float sign) {
-    __shared__ SkyChannel sky[kNbWavelengths];
-    stage_sky_lds(K, sky);
+    __shared__ SpecLds S;
+    const auto* chans = stage_chans<FAST>(K, &S);
+    __syncthreads();
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool m = active ? active[i] != 0 : true;
         DirTerms t = dir_terms<FAST>(K, to_local(K, mk3(sign * wx[i], sign * wy[i], sign * wz[i])), m);
-        for (int k = 0; k < nlam; ++k) out[(size_t)k * ostride + i] = eval_spec_one<FAST>(K, sky, t, lam[(size_t)k * lstride + i]);
+        for (int k = 0; k < nlam; ++k)
+            __builtin_nontemporal_store(eval_spec_one<FAST>(K, chans, K.sun_table, K.sun_ld, t, lam[(size_t)k * lstride + i]),
+                                        out + (size_t)k * ostride + i);
     }
 }
 
 // ======================================================================
-// Sampling: TGMM sky + uniform-cone sun (sunsky.cpp:399-451, 661-763)
+// Sampling: TGMM sky + uniform-cone sun (sunsky.cpp:354-451, 661-763)
 // ======================================================================
 struct SamplerLds {
     Gaussian gauss[kNbMixture];
-    SkyChannel sky[kNbWavelengths];
+    FastChannel fast[kNbWavelengths];
+    SkyChannel ref[kNbWavelengths];
+    float sun[kSunRgbTableSize];                 // RGB 3240 / spectral 1980 used
+    float ld[kNbWavelengths * kNbSunLdParams];
 };
 
+template <bool FAST>
 __device__ __forceinline__ void stage_sampler_lds(const SunskyKArgs& K, SamplerLds* s) {
-    const int ng = (int)(sizeof(K.gauss) / 4), ns = (int)(sizeof(K.sky) / 4);
-    const float* gsrc = reinterpret_cast<const float*>(K.gauss);
-    const float* ssrc = reinterpret_cast<const float*>(K.sky);
-    float* gdst = reinterpret_cast<float*>(s->gauss);
-    float* sdst = reinterpret_cast<float*>(s->sky);
-    for (int w = threadIdx.x; w < ng; w += blockDim.x) gdst[w] = gsrc[w];
-    for (int w = threadIdx.x; w < ns; w += blockDim.x) sdst[w] = ssrc[w];
+    lds_copy(s->gauss, K.gauss, kNbMixture);
+    if (K.variant == kSpectral) {
+        if constexpr (FAST) lds_copy(s->fast, K.fsky, kNbWavelengths);
+        else lds_copy(s->ref, K.sky, kNbWavelengths);
+        lds_copy(s->ld, K.sun_ld, kNbWavelengths * kNbSunLdParams);
+    }
+    lds_copy(s->sun, K.sun_table, K.variant == kSpectral ? kSunSpecTableSize : kSunRgbTableSize);
     __syncthreads();
+}
+
+template <bool FAST>
+__device__ __forceinline__ const typename ChanSel<FAST>::T* sampler_chans(SamplerLds* s) {
+    if constexpr (FAST) return s->fast;
+    else return s->ref;
 }
 
 // DiscreteDistribution::sample_reuse (distr_1d.h:173-183): JIT predicate
@@ -376,6 +495,14 @@ __device__ __forceinline__ int discrete_sample_reuse(const SunskyKArgs& K, float
     return idx;
 }
 
+// sphdir(theta, phi) with shared sin/cos reductions
+__device__ __forceinline__ float3_ sphdir_dev(float theta, float phi) {
+    float st, ct, sp, cp;
+    sincosf(theta, &st, &ct);
+    sincosf(phi, &sp, &cp);
+    return mk3(cp * st, sp * st, ct);
+}
+
 // sample_sky, sunsky.cpp:661-689
 __device__ __forceinline__ float3_ sample_sky(const SunskyKArgs& K, const Gaussian* G, float ux, float uy) {
     float temp;
@@ -389,16 +516,37 @@ __device__ __forceinline__ float3_ sample_sky(const SunskyKArgs& K, const Gaussi
     float theta = kSqrtTwo * erfinvf_(2.f * sy - 1.f) * g.sigma_theta + g.mu_theta;
     phi += K.sun_phi - 0.5f * kPi;
     theta = fminf(theta, 0.5f * kPi - kEpsilon);
-    return sphdir(theta, phi);
+    return sphdir_dev(theta, phi);
+}
+
+// square_to_uniform_cone (warp.h:533-551) with the concentric disk of
+// warp.h:54-90 using one shared sin/cos reduction.
+__device__ __forceinline__ float3_ uniform_cone_dev(float sx, float sy, float cos_cutoff) {
+    float x = fmaf(2.f, sx, -1.f), y = fmaf(2.f, sy, -1.f);
+    bool is_zero = (x == 0.f) && (y == 0.f);
+    bool q13 = fabsf(x) < fabsf(y);
+    float r = q13 ? y : x, rp = q13 ? x : y;
+    float phi = 0.25f * kPi * rp / r;
+    if (q13) phi = 0.5f * kPi - phi;
+    if (is_zero) phi = 0.f;
+    float s, c;
+    sincosf(phi, &s, &c);
+    float px = r * c, py = r * s;
+    float omc = 1.f - cos_cutoff;
+    float pn = fmaf(px, px, py * py);
+    float z = cos_cutoff + omc * (1.f - pn);
+    float sc = safe_sqrtf_(omc * (2.f - omc * pn));
+    return mk3(px * sc, py * sc, z);
 }
 
 // sample_sun, sunsky.cpp:697-701
 __device__ __forceinline__ float3_ sample_sun(const SunskyKArgs& K, float ux, float uy) {
     return frame_to_world(mk3(K.sun_s[0], K.sun_s[1], K.sun_s[2]), mk3(K.sun_t[0], K.sun_t[1], K.sun_t[2]),
-                          mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), uniform_cone(ux, uy, K.cos_cutoff));
+                          mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), uniform_cone_dev(ux, uy, K.cos_cutoff));
 }
 
-// tgmm_pdf, sunsky.cpp:732-763, with the truncation volume hoisted to the host.
+// tgmm_pdf, sunsky.cpp:732-763, with the per-gaussian truncation volume hoisted
+// to the host (coef = weight / volume).
 template <bool FAST>
 __device__ __forceinline__ float tgmm_pdf(const SunskyKArgs& K, float phi, float theta, bool active) {
     phi -= K.sun_phi - 0.5f * kPi;
@@ -430,8 +578,7 @@ __device__ __forceinline__ void compute_pdfs(const SunskyKArgs& K, float3_ d, bo
     *sun_pdf = (!check_sun || cosg >= K.cos_cutoff) ? K.sun_pdf : 0.f;
 }
 
-// sample_direction, sunsky.cpp:399-441.  nw = 3 (RGB) or the number of
-// per-ray wavelengths (spectral).
+// sample_direction, sunsky.cpp:399-441.  Weight planes: 3 (RGB) or nlam (spectral).
 template <bool FAST>
 __device__ __forceinline__ void sample_direction_body(
     const SunskyKArgs& K, const float* __restrict__ ux, const float* __restrict__ uy,
@@ -441,7 +588,8 @@ __device__ __forceinline__ void sample_direction_body(
     float* __restrict__ dist, float* __restrict__ opx, float* __restrict__ opy, float* __restrict__ opz,
     float* __restrict__ weight, size_t wstride) {
     __shared__ SamplerLds S;
-    stage_sampler_lds(K, &S);
+    stage_sampler_lds<FAST>(K, &S);
+    const auto* chans = sampler_chans<FAST>(&S);
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool act = active ? active[i] != 0 : true;
@@ -451,32 +599,35 @@ __device__ __forceinline__ void sample_direction_body(
         if (pick_sky) sd = sample_sky(K, S.gauss, sx / K.w_sky, sy);
         else sd = sample_sun(K, (sx - K.w_sky) / (1.f - K.w_sky), sy);
         act = act && (sd.z >= 0.f);
-        float3_ itp = mk3(px ? px[i] : 0.f, py ? py[i] : 0.f, pz ? pz[i] : 0.f);
-        float3_ rel = mk3(itp.x - K.bs_center[0], itp.y - K.bs_center[1], itp.z - K.bs_center[2]);
-        float radius = fmaxf(K.bs_radius, sqrtf(dot3(rel, rel)));
-        float dd = 2.f * radius;
         float3_ d = to_world(K, sd);
         float skyp, sunp;
         compute_pdfs<FAST>(K, sd, pick_sky, act, &skyp, &sunp);
         float pd = lerpf_(sunp, skyp, K.w_sky);
-        dx[i] = d.x; dy[i] = d.y; dz[i] = d.z;
-        pdf[i] = pd;
-        if (dist) dist[i] = dd;
-        if (opx) { opx[i] = fmaf(d.x, dd, itp.x); opy[i] = fmaf(d.y, dd, itp.y); opz[i] = fmaf(d.z, dd, itp.z); }
-        // weight = eval(si{wi = -d}) / pdf, zeroed when not finite
+        __builtin_nontemporal_store(d.x, dx + i);
+        __builtin_nontemporal_store(d.y, dy + i);
+        __builtin_nontemporal_store(d.z, dz + i);
+        __builtin_nontemporal_store(pd, pdf + i);
+        if (dist || opx) {
+            float3_ itp = mk3(px ? px[i] : 0.f, py ? py[i] : 0.f, pz ? pz[i] : 0.f);
+            float3_ rel = mk3(itp.x - K.bs_center[0], itp.y - K.bs_center[1], itp.z - K.bs_center[2]);
+            float dd = 2.f * fmaxf(K.bs_radius, sqrtf(dot3(rel, rel)));
+            if (dist) dist[i] = dd;
+            if (opx) { opx[i] = fmaf(d.x, dd, itp.x); opy[i] = fmaf(d.y, dd, itp.y); opz[i] = fmaf(d.z, dd, itp.z); }
+        }
+        // weight = eval(si{wi = -d}) / pdf, zeroed when not finite (sunsky.cpp:430-439)
         float3_ wo = to_local(K, d);
         if (K.variant == kRGB) {
             float e[3];
-            eval_rgb_local<FAST>(K, wo, act, e);
+            eval_rgb_local<FAST>(K, S.sun, wo, act, e);
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 float w = e[c] / pd;
-                weight[(size_t)c * wstride + i] = isfinite(w) ? w : 0.f;
+                __builtin_nontemporal_store(isfinite(w) ? w : 0.f, weight + (size_t)c * wstride + i);
             }
         } else {
             DirTerms t = dir_terms<FAST>(K, wo, act);
             for (int k = 0; k < nlam; ++k) {
-                float e = t.active ? eval_spec_one<FAST>(K, S.sky, t, lam[(size_t)k * lstride + i]) : 0.f;
+                float e = eval_spec_one<FAST>(K, chans, S.sun, S.ld, t, lam[(size_t)k * lstride + i]);
                 float w = e / pd;
                 weight[(size_t)k * wstride + i] = isfinite(w) ? w : 0.f;
             }
@@ -538,7 +689,8 @@ __device__ __forceinline__ float spectral_sample_pdf(const SunskyKArgs& K, float
 
 // sample_wavelengths, sunsky.cpp:463-480 (spectral: 4 shifted samples, Spectrum<Float, 4>)
 template <bool FAST>
-__device__ __forceinline__ void sample_wavelengths_one(const SunskyKArgs& K, const SkyChannel* sky, const DirTerms& t,
+__device__ __forceinline__ void sample_wavelengths_one(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
+                                                       const float* sun_tab, const float* ld_tab, const DirTerms& t,
                                                        float sample, float lam[4], float w[4]) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -546,7 +698,7 @@ __device__ __forceinline__ void sample_wavelengths_one(const SunskyKArgs& K, con
         s = s > 1.f ? s - 1.f : s;
         float lpdf;
         lam[k] = spectral_sample_pdf(K, s, &lpdf);
-        w[k] = eval_spec_one<FAST>(K, sky, t, lam[k]) / lpdf;
+        w[k] = eval_spec_one<FAST>(K, chans, sun_tab, ld_tab, t, lam[k]) / lpdf;
     }
 }
 
@@ -556,21 +708,22 @@ __device__ __forceinline__ void sample_wavelengths_body(const SunskyKArgs& K, co
                                                         const float* __restrict__ sample, const uint8_t* __restrict__ active,
                                                         size_t n, float* __restrict__ lam_out, size_t lstride,
                                                         float* __restrict__ weight, size_t wstride) {
-    __shared__ SkyChannel sky[kNbWavelengths];
-    stage_sky_lds(K, sky);
+    __shared__ SpecLds S;
+    const auto* chans = stage_chans<FAST>(K, &S);
+    __syncthreads();
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool act = active ? active[i] != 0 : true;
         float3_ wo = to_local(K, mk3(-wx[i], -wy[i], -wz[i]));
         if (K.variant == kRGB) {
             float e[3];
-            eval_rgb_local<FAST>(K, wo, act, e);
+            eval_rgb_local<FAST>(K, K.sun_table, wo, act, e);
             for (int c = 0; c < 3; ++c) weight[(size_t)c * wstride + i] = e[c];
             for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = 0.f;
         } else {
             DirTerms t = dir_terms<FAST>(K, wo, act);
             float lam[4], w[4];
-            sample_wavelengths_one<FAST>(K, sky, t, sample[i], lam, w);
+            sample_wavelengths_one<FAST>(K, chans, K.sun_table, K.sun_ld, t, sample[i], lam, w);
             for (int k = 0; k < 4; ++k) {
                 lam_out[(size_t)k * lstride + i] = lam[k];
                 weight[(size_t)k * wstride + i] = w[k];
@@ -590,7 +743,8 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
                                                 float* __restrict__ lam_out, size_t lstride,
                                                 float* __restrict__ weight, size_t wstride) {
     __shared__ SamplerLds S;
-    stage_sampler_lds(K, &S);
+    stage_sampler_lds<FAST>(K, &S);
+    const auto* chans = sampler_chans<FAST>(&S);
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool act = active ? active[i] != 0 : true;
@@ -612,13 +766,13 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
         float w[4];
         int nw;
         if (K.variant == kRGB) {
-            eval_rgb_local<FAST>(K, wo, act, w);
+            eval_rgb_local<FAST>(K, S.sun, wo, act, w);
             nw = 3;
             for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = 0.f;
         } else {
             DirTerms t = dir_terms<FAST>(K, wo, act);
             float lam[4];
-            sample_wavelengths_one<FAST>(K, S.sky, t, wls[i], lam, w);
+            sample_wavelengths_one<FAST>(K, chans, S.sun, S.ld, t, wls[i], lam, w);
             for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = lam[k];
             nw = 4;
         }
@@ -656,10 +810,20 @@ SS_EVAL_RGB(sunsky_eval_rgb_v1_ref, 1, false)
         size_t n, float* out, size_t ostride, float sign) {                                                    \
         eval_spec_bcast_body<VEC, FAST>(K, L, wx, wy, wz, active, n, out, ostride, sign);                      \
     }
-SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v4_fast, 4, true)
+SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v2_fast, 2, true)
 SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v1_fast, 1, true)
-SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v4_ref, 4, false)
+SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v2_ref, 2, false)
 SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v1_ref, 1, false)
+
+#define SS_EVAL_SPEC_NODES(NAME, VEC, FAST)                                                                   \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
+        SunskyKArgs K, LambdaSet L, const float* wx, const float* wy, const float* wz, const uint8_t* active,  \
+        size_t n, float* out, size_t ostride, float sign) {                                                    \
+        (void)L;                                                                                               \
+        eval_spec_nodes_body<VEC, FAST>(K, wx, wy, wz, active, n, out, ostride, sign);                         \
+    }
+SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v2_fast, 2, true)
+SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v2_ref, 2, false)
 
 #define SS_EVAL_SPEC_RAYS(NAME, FAST)                                                                         \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \

@@ -117,6 +117,7 @@ SS_HD inline float render_sun_rgb(const float* table, int pos, int c, float x, f
 SS_HD inline float render_sun_spec(const float* table, int pos, int c, float x) {
     const float* s = table + pos * (kNbWavelengths * kNbSunCtrlPts) + c * kNbSunCtrlPts;
     float res = 0.f;
+SS_NO_UNROLL
     for (int k = 0; k < kNbSunCtrlPts; ++k) res += powif_(x, k) * s[k];
     return res;
 }
@@ -124,6 +125,7 @@ SS_HD inline float render_sun_spec(const float* table, int pos, int c, float x) 
 // compute_sun_ld, sunsky.cpp:631-650 (hi channel 11 at lambda = 720 nm carries weight 0)
 SS_HD inline float sun_limb_darkening(const float* ld, int lo, int hi, float f, float cpsi) {
     float res = 0.f;
+SS_NO_UNROLL
     for (int j = 0; j < kNbSunLdParams; ++j) {
         float a = ld[lo * kNbSunLdParams + j];
         float coef = a;

@@ -383,7 +383,14 @@ void SunskyModel::stage() {
         ch.El2 = (float)((double)ch.E * 1.4426950408889634074);
         ch.Q = -2.f * ch.I;
         ch.pad[0] = ch.pad[1] = 0.f;
+        const float Rs = variant_ == kRGB ? ch.rad * sky_scale_ * (float)kCieYNormalization : ch.rad * sky_scale_;
+        FastChannel& f = k_.fsky[c];
+        f.A = ch.A; f.Bl2 = ch.Bl2; f.El2 = ch.El2; f.P = ch.P; f.Q = ch.Q;
+        f.Cs = ch.C * Rs; f.Ds = ch.D * Rs; f.Fs = ch.F * Rs; f.Gs = ch.G * Rs; f.Hs = ch.H * Rs;
     }
+    k_.sun_mul = variant_ == kRGB
+                     ? sun_scale_ * k_.area_ratio * (float)kSpecToRgbSunConv * (float)kCieYNormalization
+                     : sun_scale_ * k_.area_ratio;
     // ---------------- sun radiance (compute_sun_params)
     compute_sun_params(sun_rad_ds_, spec ? kSunSpecTableSize : kSunRgbTableSize, turbidity_, &sun_table_);
 

@@ -10,8 +10,10 @@
 
 #if defined(__HIPCC__)
 #define SS_HD __host__ __device__
+#define SS_NO_UNROLL _Pragma("unroll 1")
 #else
 #define SS_HD
+#define SS_NO_UNROLL
 #endif
 
 namespace sunsky {
@@ -57,6 +59,14 @@ struct SkyChannel {
     float pad[2];
 };
 
+// The same channel with the output scale folded in for the FAST kernels:
+// Rs = rad * sky_scale (* MI_CIE_Y_NORMALIZATION for RGB) multiplies C..H, so
+// L = (1 + A exp2(Bl2 r)) (Cs + Ds exp2(El2 g) + Fs cos^2 g + Gs chi + Hs sqrt(cos_theta)).
+struct FastChannel {
+    float A, Bl2, El2, P, Q;
+    float Cs, Ds, Fs, Gs, Hs;
+};
+
 // One truncated Gaussian of the TGMM (sunsky.cpp:661-689, :732-763) with
 // its per-gaussian truncation constants hoisted out of the per-lane loop.
 struct Gaussian {
@@ -85,6 +95,8 @@ struct SunskyKArgs {
     int   identity_xform;      // to_world linear part == I: skip the 3x3 products
     // -------- radiance
     SkyChannel sky[kNbWavelengths];
+    FastChannel fsky[kNbWavelengths];
+    float sun_mul;           // sun_scale * area_ratio (* SPEC_TO_RGB_SUN_CONV * CIE_Y_NORMALIZATION for RGB)
     const float* sun_table;  // device: 45x3x4x6 (RGB) or 45x11x4 (spectral), turbidity-lerped
     const float* sun_ld;     // device: 11x6 limb darkening (spectral only)
     // -------- sky sampling (TGMM + DiscreteDistribution)
@@ -99,6 +111,6 @@ struct SunskyKArgs {
     float spec_integral, spec_norm, spec_interval, spec_inv_interval;
 };
 
-static_assert(sizeof(SunskyKArgs) < 3072, "kernarg segment budget");
+static_assert(sizeof(SunskyKArgs) < 3584, "kernarg segment budget");
 
 }  // namespace sunsky

@@ -151,8 +151,11 @@ class SunskyEmitter:
     def __del__(self):
         h = getattr(self, "_h", None)
         if h:
-            lib().sunsky_emitter_destroy(h)
             self._h = None
+            try:
+                lib().sunsky_emitter_destroy(h)
+            except Exception:   # interpreter shutdown: the library may already be gone
+                pass
 
     # ------------------------------------------------------------ state
     def _refresh_info(self):

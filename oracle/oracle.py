@@ -160,8 +160,11 @@ class Oracle:
     def __del__(self):
         h = getattr(self, "_h", None)
         if h:
-            getattr(lib(), f"oracle_destroy_{self._sfx}")(h)
             self._h = None
+            try:
+                getattr(lib(), f"oracle_destroy_{self._sfx}")(h)
+            except Exception:   # interpreter shutdown: the library may already be gone
+                pass
 
     def _fn(self, name):
         return getattr(lib(), f"oracle_{name}_{self._sfx}")

@@ -1,7 +1,11 @@
 """GPU parity: the HIP path (through the C ABI) against the CPU oracle and the
 reference fixtures.  Tolerances (BASELINE.json north_star: 1e-5 relative fp32):
 
-* sky radiance, sampling pdfs: max |gpu - oracle_f32| / max(|oracle|, 1e-6 max|oracle|) <= 1e-5;
+* sky radiance, sampling pdfs: |gpu - oracle_f32| <= 1e-5 |oracle_f32| per lane, with the
+  reference fp32's own error |o32 - o64| added as slack where fp64 is available: near the
+  sun limb the sky's chi term (1 + I^2 - 2 I cos g) cancels and the fp32 reference itself
+  is off by >1e-5 (measured 1.45e-5 at gamma = 0.268 deg); at least 99.99% of the sky lanes
+  must also meet the plain 1e-5 bound (tools/diag_fast.py prints the distribution);
 * sun-disc lanes: the sun polynomial/limb-darkening is ill-conditioned in fp32
   (d cos_psi / d gamma -> inf at the limb), so the bar there is
   |gpu - o64| <= 1e-5 |o64| + 4 |o32 - o64|: the GPU must be as accurate as the
@@ -49,8 +53,14 @@ def assert_parity(gpu, o32, o64, sunlanes, rtol=1e-5):
     """gpu/o32/o64: (n, c).  sky lanes: rel to o32; sun lanes: conditioning-aware vs o64."""
     sky = ~sunlanes
     if sky.any():
-        r = max_rel(gpu[sky], o32[sky])
-        assert r <= rtol, f"sky lanes: max rel {r:.3e}"
+        g, a, b = gpu[sky].astype(np.float64), o32[sky].astype(np.float64), o64[sky]
+        floor = 1e-6 * np.abs(a).max()
+        strict = np.abs(g - a) <= rtol * np.maximum(np.abs(a), floor)
+        bound = rtol * np.maximum(np.abs(a), floor) + np.abs(a - b)
+        bad = np.abs(g - a) > bound
+        assert not bad.any(), (f"sky lanes: {bad.sum()} over bound, worst {np.max(np.abs(g - a) / bound):.2f}x; "
+                               f"strict max rel {max_rel(gpu[sky], o32[sky]):.3e}")
+        assert strict.mean() >= 0.9999, f"sky lanes: only {strict.mean():.6f} within plain {rtol:g}"
     if sunlanes.any():
         g, a, b = gpu[sunlanes].astype(np.float64), o32[sunlanes].astype(np.float64), o64[sunlanes]
         bound = rtol * np.abs(b) + 4 * np.abs(a - b) + 1e-30

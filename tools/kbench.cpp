@@ -1,0 +1,142 @@
+// kbench.cpp -- native kernel micro-benchmark for tuning (no Python, no torch).
+//
+// Stages a sunsky emitter with the product's host code (SunskyModel), uploads
+// n uniform upper-hemisphere directions, and times kernels of the code object
+// by name with hipEvents over back-to-back launches, for several grid sizes.
+//
+//   kbench <hsaco> <rgb|spec> <n> <iters> <blocks_per_cu,...> <kernel> [kernel ...]
+//
+// Build: make -C tools kbench
+#include <hip/hip_runtime_api.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "sunsky_model.h"
+
+using namespace sunsky;
+
+#define CK(x)                                                                              \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            std::exit(1);                                                                  \
+        }                                                                                  \
+    } while (0)
+
+struct LambdaSet {
+    int m;
+    int lo[kMaxBroadcastLambda];
+    float f[kMaxBroadcastLambda];
+};
+
+int main(int argc, char** argv) {
+    if (argc < 7) {
+        std::fprintf(stderr, "usage: kbench <hsaco> <rgb|spec> <n> <iters> <bpcu,...> <kernel>...\n");
+        return 2;
+    }
+    std::string hsaco = argv[1], mode = argv[2];
+    size_t n = std::strtoull(argv[3], nullptr, 10);
+    int iters = std::atoi(argv[4]);
+    std::vector<int> bpcu;
+    {
+        std::stringstream ss(argv[5]);
+        std::string tok;
+        while (std::getline(ss, tok, ',')) bpcu.push_back(std::atoi(tok.c_str()));
+    }
+    const bool spec = mode == "spec";
+    const char* pack = std::getenv("SUNSKY_AMD_DATASET");
+    std::string pack_path = pack ? pack : "mitsuba3-sunsky_amd/data/sunsky_datasets.pack";
+
+    Properties props;
+    props.set_float("turbidity", spec ? 3.0 : 2.0);
+    props.set_float("albedo", spec ? 0.3 : 0.1);
+    double th = (90.0 - 45.0) * M_PI / 180.0;
+    props.set_vector3("sun_direction", (float)std::sin(th), 0.f, (float)std::cos(th));
+    SunskyModel model(props, spec ? kSpectral : kRGB, kJit, pack_path);
+
+    int cu = 0;
+    CK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0));
+    float *d_sun, *d_ld;
+    CK(hipMalloc(&d_sun, sizeof(float) * kSunRgbTableSize));
+    CK(hipMalloc(&d_ld, sizeof(float) * 66));
+    CK(hipMemcpy(d_sun, model.sun_table().data(), sizeof(float) * model.sun_table().size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_ld, model.sun_ld().data(), sizeof(float) * 66, hipMemcpyHostToDevice));
+    SunskyKArgs K = model.kargs();
+    K.sun_table = d_sun;
+    K.sun_ld = d_ld;
+
+    // directions: cos theta = u1, phi = 2 pi u2; wi = -wo
+    std::vector<float> hx(n), hy(n), hz(n);
+    std::mt19937 rng(7);
+    std::uniform_real_distribution<float> U(0.f, 1.f);
+    for (size_t i = 0; i < n; ++i) {
+        float ct = U(rng), ph = 2.f * (float)M_PI * U(rng), st = std::sqrt(std::max(0.f, 1 - ct * ct));
+        hx[i] = -st * std::cos(ph); hy[i] = -st * std::sin(ph); hz[i] = -ct;
+    }
+    const int nout = spec ? 11 : 3;
+    float *wx, *wy, *wz, *out;
+    CK(hipMalloc(&wx, n * 4)); CK(hipMalloc(&wy, n * 4)); CK(hipMalloc(&wz, n * 4));
+    CK(hipMalloc(&out, n * 4 * nout));
+    CK(hipMemcpy(wx, hx.data(), n * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(wy, hy.data(), n * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(wz, hz.data(), n * 4, hipMemcpyHostToDevice));
+
+    hipModule_t mod;
+    CK(hipModuleLoad(&mod, hsaco.c_str()));
+    LambdaSet L;
+    std::memset(&L, 0, sizeof(L));
+    L.m = 11;
+    for (int k = 0; k < 11; ++k) { L.lo[k] = k; L.f[k] = 0.f; }
+    const uint8_t* active = nullptr;
+    size_t ostride = n;
+    float sign = -1.f;
+    const double bytes = spec ? (12.0 + 44.0) * n : 24.0 * n;
+    std::vector<float> ref;
+    for (int a = 6; a < argc; ++a) {
+        hipFunction_t f;
+        CK(hipModuleGetFunction(&f, mod, argv[a]));
+        std::string name = argv[a];
+        int vec = name.find("_v4") != std::string::npos ? 4 : (name.find("_v2") != std::string::npos ? 2 : 1);
+        for (int mult : bpcu) {
+            size_t items = n / vec;
+            unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((items + 255) / 256, (size_t)cu * mult));
+            void* args_rgb[] = {&K, &wx, &wy, &wz, &active, &n, &out, &ostride, &sign};
+            void* args_spec[] = {&K, &L, &wx, &wy, &wz, &active, &n, &out, &ostride, &sign};
+            void** args = spec ? args_spec : args_rgb;
+            for (int w = 0; w < 3; ++w) CK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
+            hipEvent_t e0, e1;
+            CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+            CK(hipEventRecord(e0, nullptr));
+            for (int it = 0; it < iters; ++it)
+                CK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
+            CK(hipEventRecord(e1, nullptr));
+            CK(hipEventSynchronize(e1));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            double us = 1e3 * ms / iters;
+            // checksum against the first kernel
+            std::vector<float> h((size_t)nout * n);
+            CK(hipMemcpy(h.data(), out, h.size() * 4, hipMemcpyDeviceToHost));
+            double maxrel = 0;
+            if (ref.empty()) ref = h;
+            else
+                for (size_t i = 0; i < h.size(); ++i) {
+                    double d = std::fabs((double)h[i] - ref[i]) / std::max(1e-6, std::fabs((double)ref[i]));
+                    if (d > maxrel) maxrel = d;
+                }
+            std::printf("%-36s bpcu=%-4d grid=%-6u %9.2f us  %7.1f GB/s  %.3e evals/s  maxrel-vs-first=%.2e\n",
+                        argv[a], mult, grid, us, bytes / (us * 1e-6) / 1e9, (spec ? 11.0 : 1.0) * n / (us * 1e-6),
+                        maxrel);
+            std::fflush(stdout);
+        }
+    }
+    return 0;
+}

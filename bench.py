@@ -79,27 +79,20 @@ class KernelTimer:
         return self.t0.elapsed_time(self.t1) / max(self.launches, 1)
 
 
-def pmc_traffic(path, kernel_prefix):
-    """HBM bytes per launch from a rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE CSV pair
-    (MI355X_MICROARCH.md §HBM: FETCH_SIZE reads 1/2 of a wide streaming read on gfx950)."""
-    try:
-        import csv
-        fetch, write = [], []
-        for f in path.split(","):
-            with open(f) as fh:
-                for row in csv.DictReader(fh):
-                    if not row.get("Kernel_Name", "").startswith(kernel_prefix):
-                        continue
-                    name, val = row.get("Counter_Name"), float(row.get("Counter_Value", "nan"))
-                    if name == "FETCH_SIZE":
-                        fetch.append(val)
-                    elif name == "WRITE_SIZE":
-                        write.append(val)
-        if fetch and write:
-            return (2.0 * np.mean(fetch) + np.mean(write)) * 1024.0
-    except Exception:
-        pass
-    return None
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/rNN_*pmc_traffic.json, written by tools/gpu_pmc.sh: separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench command,
+    corrected per MI355X_MICROARCH.md "HBM").  None when no summary exists."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        rec = json.load(fh).get(kernel)
+    if not rec:
+        return None, None
+    return rec["traffic_bytes"], os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(wi_host, budget_s=12.0):
@@ -157,14 +150,14 @@ def parity_check(ems, wi, outs, n_check=1 << 20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--n", type=int, default=N_DIRS, help="directions per GPU")
     ap.add_argument("--precision", default=os.environ.get("SUNSKY_BENCH_PRECISION", "fast"))
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather of the radiance to rank 0")
-    ap.add_argument("--pmc", default=os.environ.get("SUNSKY_PMC_CSV"), help="rocprofv3 --pmc CSV(s) for traffic")
+    ap.add_argument("--no-pmc", action="store_true", help="do not read the committed PMC traffic summary")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,6 +182,13 @@ def main():
             if rc:
                 raise RuntimeError(lib.sunsky_last_error().decode())
 
+    # Untimed settle: bring the GPU out of its idle clock state before the
+    # W warmup steps (a step is ~0.2 ms, so a handful of warmups alone is too short).
+    torch.cuda.synchronize()
+    t_settle = time.perf_counter()
+    while time.perf_counter() - t_settle < 0.5:
+        step()
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     timer = KernelTimer()
@@ -215,7 +215,8 @@ def main():
     result = None
     if rank == 0:
         achieved = BYTES_RGB * n / (kernel_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(args.pmc, "sunsky_eval_rgb_v4") if args.pmc else None
+        kname = "sunsky_eval_rgb_v4_" + ("ref" if args.precision == "reference" else "fast")
+        traffic, traffic_src = (None, None) if args.no_pmc else pmc_traffic(kname)
         parity = parity_check(ems, wi, outs)
         result = {
             "metric": "sky-radiance evals/sec (ray-dir x lambda)", "value": value, "unit": "evals/s",
@@ -227,8 +228,8 @@ def main():
                        "albedo": 0.1, "precision": args.precision, "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": traffic / 1.0 if traffic else None,
-                         "kernel": "sunsky_eval_rgb_v4_" + args.precision[:4].replace("refe", "ref"),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": kname,
                          "kernel_ms": kernel_ms, "bytes_per_launch": BYTES_RGB * n},
             "parity": dict(parity, checked_dirs=min(n, 1 << 20) * len(TURBIDITIES), sun_disc_lanes="excluded"),
         }

@@ -134,15 +134,27 @@ DeviceModule* module_for_device(int dev) {
 
 constexpr int kBlock = 256;
 
-// Memory-bound streaming launch: enough workgroups to fill every CU several
-// times over, grid-striding beyond (cdna_hip_programming.md Guideline 11).
-unsigned grid_for(const DeviceModule* m, size_t work_items) {
-    static const int mult = [] {
+// Grid-stride launches sized to fill every CU several times over
+// (cdna_hip_programming.md Guideline 11).  Workgroups per CU from the
+// tools/kbench.cpp sweep on MI355X (profiles/r01_v2_kbench_grid_sweep.log):
+// RGB eval 64 (60.4 us vs 64.9 us at 16 for 16M directions), spectral 32.
+// SUNSKY_AMD_BLOCKS_PER_CU overrides every kernel class.
+int blocks_per_cu(KernelId k) {
+    static const int env = [] {
         const char* e = std::getenv("SUNSKY_AMD_BLOCKS_PER_CU");
-        return e ? std::max(1, std::atoi(e)) : 16;
+        return e ? std::max(1, std::atoi(e)) : 0;
     }();
+    if (env) return env;
+    switch (k) {
+        case K_EVAL_RGB_V4: case K_EVAL_RGB_V1: return 64;
+        case K_EVAL_SPEC_BCAST_V2: case K_EVAL_SPEC_BCAST_V1: case K_EVAL_SPEC_NODES_V2: return 32;
+        default: return 16;
+    }
+}
+
+unsigned grid_for(const DeviceModule* m, KernelId k, size_t work_items) {
     size_t need = (work_items + kBlock - 1) / kBlock;
-    size_t cap = (size_t)m->cu_count * (size_t)mult;
+    size_t cap = (size_t)m->cu_count * (size_t)blocks_per_cu(k);
     return (unsigned)std::max<size_t>(1, std::min(need, cap));
 }
 
@@ -397,7 +409,7 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
             if (n4) {
                 const float *x = w.x, *y = w.y, *z = w.z;
                 void* args[] = {&K, &x, &y, &z, &active, &n4, &out, &ostride, &sign};
-                launch(e->fn(K_EVAL_RGB_V4), grid_for(e->mod, n4 / 4), s, args);
+                launch(e->fn(K_EVAL_RGB_V4), grid_for(e->mod, K_EVAL_RGB_V4, n4 / 4), s, args);
             }
             if (n4 < n) {
                 const float *x = w.x + n4, *y = w.y + n4, *z = w.z + n4;
@@ -405,13 +417,13 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
                 float* o = out + n4;
                 size_t rem = n - n4;
                 void* args[] = {&K, &x, &y, &z, &a, &rem, &o, &ostride, &sign};
-                launch(e->fn(K_EVAL_RGB_V1), grid_for(e->mod, rem), s, args);
+                launch(e->fn(K_EVAL_RGB_V1), grid_for(e->mod, K_EVAL_RGB_V1, rem), s, args);
             }
         } else {
             const float *x = w.x, *y = w.y, *z = w.z;
             int nl = nlam;
             void* args[] = {&K, &x, &y, &z, &lam, &lstride, &nl, &active, &n, &out, &ostride, &sign};
-            launch(e->fn(K_EVAL_SPEC_RAYS), grid_for(e->mod, n), s, args);
+            launch(e->fn(K_EVAL_SPEC_RAYS), grid_for(e->mod, K_EVAL_SPEC_RAYS, n), s, args);
         }
     });
 }
@@ -461,7 +473,7 @@ int sunsky_eval_spectral_broadcast(const sunsky_emitter* e, sunsky_vec3_in w, co
         if (n2) {
             const float *x = w.x, *y = w.y, *z = w.z;
             void* args[] = {&K, &L, &x, &y, &z, &active, &n2, &out, &ostride, &sign};
-            launch(e->fn(nodes ? K_EVAL_SPEC_NODES_V2 : K_EVAL_SPEC_BCAST_V2), grid_for(e->mod, n2 / 2), s, args);
+            launch(e->fn(nodes ? K_EVAL_SPEC_NODES_V2 : K_EVAL_SPEC_BCAST_V2), grid_for(e->mod, K_EVAL_SPEC_BCAST_V2, n2 / 2), s, args);
         }
         if (n2 < n) {
             const float *x = w.x + n2, *y = w.y + n2, *z = w.z + n2;
@@ -469,7 +481,7 @@ int sunsky_eval_spectral_broadcast(const sunsky_emitter* e, sunsky_vec3_in w, co
             float* o = out + n2;
             size_t rem = n - n2;
             void* args[] = {&K, &L, &x, &y, &z, &a, &rem, &o, &ostride, &sign};
-            launch(e->fn(K_EVAL_SPEC_BCAST_V1), grid_for(e->mod, rem), s, args);
+            launch(e->fn(K_EVAL_SPEC_BCAST_V1), grid_for(e->mod, K_EVAL_SPEC_BCAST_V1, rem), s, args);
         }
     });
 }
@@ -495,7 +507,7 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
         int nl = spec ? nlam : 0;
         void* args[] = {&K, &ux, &uy, (void*)&it_p.x, (void*)&it_p.y, (void*)&it_p.z, &lam, &lstride, &nl, &active, &n,
                         &ds_d.x, &ds_d.y, &ds_d.z, &ds_pdf, &ds_dist, &ds_p.x, &ds_p.y, &ds_p.z, &weight, &wstride};
-        launch(e->fn(K_SAMPLE_DIRECTION), grid_for(e->mod, n), (hipStream_t)stream, args);
+        launch(e->fn(K_SAMPLE_DIRECTION), grid_for(e->mod, K_SAMPLE_DIRECTION, n), (hipStream_t)stream, args);
     });
 }
 
@@ -507,7 +519,7 @@ int sunsky_pdf_direction(const sunsky_emitter* e, sunsky_vec3_in d, const uint8_
     return guarded([&] {
         SunskyKArgs K = e->kargs;
         void* args[] = {&K, (void*)&d.x, (void*)&d.y, (void*)&d.z, &active, &n, &pdf};
-        launch(e->fn(K_PDF_DIRECTION), grid_for(e->mod, n), (hipStream_t)stream, args);
+        launch(e->fn(K_PDF_DIRECTION), grid_for(e->mod, K_PDF_DIRECTION, n), (hipStream_t)stream, args);
     });
 }
 
@@ -524,7 +536,7 @@ int sunsky_sample_ray(const sunsky_emitter* e, const float* wls, const float* s2
         SunskyKArgs K = e->kargs;
         void* args[] = {&K, &wls, &s2x, &s2y, &s3x, &s3y, &active, &n, &o.x, &o.y, &o.z,
                         &d.x, &d.y, &d.z, &lam, &lstride, &weight, &wstride};
-        launch(e->fn(K_SAMPLE_RAY), grid_for(e->mod, n), (hipStream_t)stream, args);
+        launch(e->fn(K_SAMPLE_RAY), grid_for(e->mod, K_SAMPLE_RAY, n), (hipStream_t)stream, args);
     });
 }
 
@@ -538,7 +550,7 @@ int sunsky_sample_wavelengths(const sunsky_emitter* e, sunsky_vec3_in w, const f
     return guarded([&] {
         SunskyKArgs K = e->kargs;
         void* args[] = {&K, (void*)&w.x, (void*)&w.y, (void*)&w.z, &sample, &active, &n, &lam, &lstride, &weight, &wstride};
-        launch(e->fn(K_SAMPLE_WAVELENGTHS), grid_for(e->mod, n), (hipStream_t)stream, args);
+        launch(e->fn(K_SAMPLE_WAVELENGTHS), grid_for(e->mod, K_SAMPLE_WAVELENGTHS, n), (hipStream_t)stream, args);
     });
 }
 

@@ -307,17 +307,20 @@ def main():
 
     # ----------------------------------------------------------- optional gather
     if args.gather and world > 1:
-        buf = outs[0]
-        gl = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+        # configs[4]'s final step: the radiance shards gathered to rank 0 over RCCL
+        # (sunsky_amd.sharding.gather_radiance); reported beside `value`, never in it.
+        from sunsky_amd.sharding import gather_radiance
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        dist.gather(buf, gl, dst=0)
+        full = gather_radiance(outs[0], n * world)
         torch.cuda.synchronize()
         gt = time.perf_counter() - t0
         if rank == 0:
-            result["gather"] = {"seconds": gt, "bytes_to_root": buf.numel() * 4 * (world - 1),
-                                "GBps": buf.numel() * 4 * (world - 1) / gt / 1e9}
+            nbytes = outs[0].numel() * 4 * (world - 1)
+            result["gather"] = {"seconds": gt, "bytes_to_root": nbytes, "GBps": nbytes / gt / 1e9,
+                                "bitwise_own_shard": bool(torch.equal(full[:, :n], outs[0]))}
+        del full
 
     if rank == 0:
         if not args.no_cpu:

@@ -1,0 +1,134 @@
+// facade_check.cpp -- drives the C++ facade (include/sunsky_amd.hpp) the way a
+// C++ renderer would.  Test program for tests/test_cpp_facade.py:
+//   facade_check host            host-only staging, errors, flags (no GPU)
+//   facade_check gpu <out_dir>   eval / sample_direction / pdf_direction on the
+//                                current HIP device; raw fp32 planes written to
+//                                <out_dir> for the oracle comparison in pytest.
+#include <hip/hip_runtime_api.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "sunsky_amd.hpp"
+
+using namespace sunsky_amd;
+
+#define HIPCK(x)                                                                     \
+    do {                                                                             \
+        hipError_t e_ = (x);                                                         \
+        if (e_ != hipSuccess) {                                                      \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));             \
+            return 3;                                                                \
+        }                                                                            \
+    } while (0)
+
+static void fill_props(Properties& p) {
+    const double th = (90.0 - 45.0) * M_PI / 180.0;
+    p.set_float("turbidity", 4.0).set_float("albedo", 0.2);
+    p.set_vector3("sun_direction", (float)std::sin(th), 0.f, (float)std::cos(th));
+}
+
+static int host_mode() {
+    Properties p;
+    fill_props(p);
+    SunskyEmitter em = SunskyEmitter::host_only(p, Variant::RGB);
+    sunsky_info info = em.info();
+    if (!em.is_environment() || info.nb_channels != 3) { std::puts("FAIL flags/channels"); return 1; }
+    if (em.bbox().valid()) { std::puts("FAIL bbox should be invalid"); return 1; }
+    if (em.table(SUNSKY_TABLE_SKY_PARAMS).size() != 27) { std::puts("FAIL sky params size"); return 1; }
+    std::printf("to_string: %s\n", em.to_string().c_str());
+    std::printf("w_sky=%.9g\n", info.sky_sampling_w);
+    // reference error text: sunsky.cpp:889-948
+    try {
+        Properties bad;
+        bad.set_float("turbidity", 12.0);
+        SunskyEmitter::host_only(bad, Variant::RGB);
+        std::puts("FAIL no error for turbidity 12");
+        return 1;
+    } catch (const Error& e) {
+        std::printf("error: %s\n", e.what());
+    }
+    try {
+        em.sample_position();
+    } catch (const NotImplementedError& e) {
+        std::printf("not implemented: %s\n", e.what());
+    }
+    std::puts("host ok");
+    return 0;
+}
+
+static bool write_file(const std::string& path, const std::vector<float>& v) {
+    FILE* f = std::fopen(path.c_str(), "wb");
+    if (!f) return false;
+    std::fwrite(v.data(), sizeof(float), v.size(), f);
+    std::fclose(f);
+    return true;
+}
+
+static int gpu_mode(const std::string& dir) {
+    const size_t n = 8192;
+    std::vector<float> wi(3 * n), u(2 * n);
+    std::mt19937 rng(11);
+    std::uniform_real_distribution<float> U(0.f, 1.f);
+    for (size_t i = 0; i < n; ++i) {
+        float ct = U(rng), ph = 2.f * (float)M_PI * U(rng), st = std::sqrt(std::max(0.f, 1.f - ct * ct));
+        wi[i] = -st * std::cos(ph); wi[n + i] = -st * std::sin(ph); wi[2 * n + i] = -ct;
+        u[i] = U(rng); u[n + i] = U(rng);
+    }
+    float *d_wi, *d_u, *d_rgb, *d_d, *d_pdf, *d_w, *d_pdf2;
+    HIPCK(hipMalloc(&d_wi, 3 * n * 4)); HIPCK(hipMalloc(&d_u, 2 * n * 4)); HIPCK(hipMalloc(&d_rgb, 3 * n * 4));
+    HIPCK(hipMalloc(&d_d, 3 * n * 4)); HIPCK(hipMalloc(&d_pdf, n * 4)); HIPCK(hipMalloc(&d_w, 3 * n * 4));
+    HIPCK(hipMalloc(&d_pdf2, n * 4));
+    HIPCK(hipMemcpy(d_wi, wi.data(), 3 * n * 4, hipMemcpyHostToDevice));
+    HIPCK(hipMemcpy(d_u, u.data(), 2 * n * 4, hipMemcpyHostToDevice));
+
+    Properties p;
+    fill_props(p);
+    SunskyEmitter em(p, Variant::RGB);
+
+    SurfaceInteraction si;
+    si.wi = {d_wi, d_wi + n, d_wi + 2 * n};
+    si.n = n;
+    em.eval(si, {d_rgb, n});
+
+    Interaction it;
+    it.n = n;
+    DirectionSample ds;
+    ds.d = {d_d, d_d + n, d_d + 2 * n};
+    ds.pdf = d_pdf;
+    em.sample_direction(it, {d_u, d_u + n}, ds, {d_w, n});
+    DirectionSampleIn dsi;
+    dsi.d = {d_d, d_d + n, d_d + 2 * n};
+    em.pdf_direction(n, dsi, d_pdf2);
+    HIPCK(hipDeviceSynchronize());
+
+    std::vector<float> rgb(3 * n), dd(3 * n), pdf(n), w(3 * n), pdf2(n);
+    HIPCK(hipMemcpy(rgb.data(), d_rgb, 3 * n * 4, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpy(dd.data(), d_d, 3 * n * 4, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpy(pdf.data(), d_pdf, n * 4, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpy(w.data(), d_w, 3 * n * 4, hipMemcpyDeviceToHost));
+    HIPCK(hipMemcpy(pdf2.data(), d_pdf2, n * 4, hipMemcpyDeviceToHost));
+    bool ok = write_file(dir + "/wi.f32", wi) && write_file(dir + "/u.f32", u) && write_file(dir + "/rgb.f32", rgb) &&
+              write_file(dir + "/d.f32", dd) && write_file(dir + "/pdf.f32", pdf) && write_file(dir + "/w.f32", w) &&
+              write_file(dir + "/pdf2.f32", pdf2);
+    for (float* ptr : {d_wi, d_u, d_rgb, d_d, d_pdf, d_w, d_pdf2}) (void)hipFree(ptr);
+    if (!ok) { std::puts("FAIL writing outputs"); return 1; }
+    std::printf("gpu ok w_sky=%.9g\n", em.info().sky_sampling_w);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    try {
+        if (argc >= 2 && std::strcmp(argv[1], "host") == 0) return host_mode();
+        if (argc >= 3 && std::strcmp(argv[1], "gpu") == 0) return gpu_mode(argv[2]);
+    } catch (const Error& e) {
+        std::fprintf(stderr, "sunsky_amd::Error(%d): %s\n", e.status, e.what());
+        return 2;
+    }
+    std::fprintf(stderr, "usage: facade_check host | gpu <out_dir>\n");
+    return 2;
+}

@@ -77,3 +77,22 @@ def max_rel(x, ref, floor_frac=1e-6):
     ref = np.asarray(ref, dtype=np.float64)
     floor = floor_frac * max(np.abs(ref).max(), 1e-30)
     return float(np.max(np.abs(x - ref) / np.maximum(np.abs(ref), floor)))
+
+
+def assert_parity(gpu, o32, o64, sunlanes, rtol=1e-5):
+    """gpu/o32/o64: (n, c).  sky lanes: rel to o32; sun lanes: conditioning-aware vs o64."""
+    sky = ~sunlanes
+    if sky.any():
+        g, a, b = gpu[sky].astype(np.float64), o32[sky].astype(np.float64), o64[sky]
+        floor = 1e-6 * np.abs(a).max()
+        strict = np.abs(g - a) <= rtol * np.maximum(np.abs(a), floor)
+        bound = rtol * np.maximum(np.abs(a), floor) + np.abs(a - b)
+        bad = np.abs(g - a) > bound
+        assert not bad.any(), (f"sky lanes: {bad.sum()} over bound, worst {np.max(np.abs(g - a) / bound):.2f}x; "
+                               f"strict max rel {max_rel(gpu[sky], o32[sky]):.3e}")
+        assert strict.mean() >= 0.9999, f"sky lanes: only {strict.mean():.6f} within plain {rtol:g}"
+    if sunlanes.any():
+        g, a, b = gpu[sunlanes].astype(np.float64), o32[sunlanes].astype(np.float64), o64[sunlanes]
+        bound = rtol * np.abs(b) + 4 * np.abs(a - b) + 1e-30
+        bad = np.abs(g - b) > bound
+        assert not bad.any(), f"sun lanes: {bad.sum()} over bound, worst {np.max(np.abs(g - b) / bound):.2f}x"

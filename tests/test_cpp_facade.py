@@ -1,0 +1,64 @@
+"""The C++ facade (include/sunsky_amd.hpp) driven by a compiled C++ program,
+tests/cpp/facade_check.cpp: what a C++ renderer linking libsunsky_amd.so sees.
+CPU: host-only staging, error mapping, flags.  GPU: eval / sample_direction /
+pdf_direction through the facade against the oracle."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import assert_parity, max_rel
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "cpp", "build", "facade_check")
+SUN45 = {"type": "sunsky", "turbidity": 4.0, "albedo": 0.2,
+         "sun_direction": [float(np.sin(np.pi / 4)), 0.0, float(np.cos(np.pi / 4))]}
+
+
+@pytest.fixture(scope="module")
+def exe():
+    if not os.path.exists(EXE):
+        if shutil.which("g++") is None:
+            pytest.skip("no g++ to build the facade check")
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "cpp")], check=True, capture_output=True)
+    return EXE
+
+
+def test_facade_host_mode(exe):
+    r = subprocess.run([exe, "host"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "host ok" in r.stdout
+    assert "Turbidity value 12.000000 is out of range [1, 10]" in r.stdout
+    assert "not implemented: sample_position" in r.stdout
+    w = float(r.stdout.split("w_sky=")[1].split()[0])
+    o = O.Oracle(SUN45, "rgb", "jit", "f32")
+    assert abs(w - o.info()["w_sky"]) < 1e-5
+
+
+@pytest.mark.gpu
+def test_facade_gpu_mode(exe, tmp_path):
+    r = subprocess.run([exe, "gpu", str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    n = 8192
+
+    def load(name, rows):
+        a = np.fromfile(tmp_path / name, dtype=np.float32)
+        return a.reshape(rows, n).T if rows > 1 else a
+
+    wi, u, rgb = load("wi.f32", 3), load("u.f32", 2), load("rgb.f32", 3)
+    d, pdf, w, pdf2 = load("d.f32", 3), load("pdf.f32", 1), load("w.f32", 3), load("pdf2.f32", 1)
+    o32, o64 = O.Oracle(SUN45, "rgb", "jit", "f32"), O.Oracle(SUN45, "rgb", "jit", "f64")
+    info = o32.info()
+    wo = -wi
+    sun = (wo @ info["sun_dir_local"] >= info["cos_cutoff"]) & (wo[:, 2] >= 0)
+    assert_parity(rgb, o32.eval(wi), o64.eval(wi), sun)
+    # sampling through the facade: pdf_direction of the sampled directions vs the oracle
+    assert np.all(np.isfinite(w)) and np.all(pdf >= 0)
+    assert max_rel(pdf2, o32.pdf_direction(d)) < 1e-5
+    w_gpu = float(r.stdout.split("w_sky=")[1].split()[0])
+    o32.override_w_sky(w_gpu)
+    ref = o32.sample_direction(u)
+    assert np.quantile(np.abs(d - ref["d"]).max(axis=1), 0.999) < 2e-6

@@ -19,8 +19,8 @@ import torch
 
 import oracle as O
 import sunsky_amd as ss
-from helpers import (EXR_WAVELENGTHS, SPECIAL_ALBEDO, angles_dict, exr_grid_wi, hemisphere_wo, hour_dict,
-                     max_rel, mean_rel, sphere_wo, sun_cone_wo)
+from helpers import (EXR_WAVELENGTHS, SPECIAL_ALBEDO, angles_dict, assert_parity, exr_grid_wi, hemisphere_wo,
+                     hour_dict, max_rel, mean_rel, sphere_wo, sun_cone_wo)
 
 pytestmark = pytest.mark.gpu
 
@@ -47,25 +47,6 @@ def sun_mask(o, wo):
     info = o.info()
     s = info["sun_dir_local"]
     return (wo @ s >= info["cos_cutoff"]) & (wo[:, 2] >= 0)
-
-
-def assert_parity(gpu, o32, o64, sunlanes, rtol=1e-5):
-    """gpu/o32/o64: (n, c).  sky lanes: rel to o32; sun lanes: conditioning-aware vs o64."""
-    sky = ~sunlanes
-    if sky.any():
-        g, a, b = gpu[sky].astype(np.float64), o32[sky].astype(np.float64), o64[sky]
-        floor = 1e-6 * np.abs(a).max()
-        strict = np.abs(g - a) <= rtol * np.maximum(np.abs(a), floor)
-        bound = rtol * np.maximum(np.abs(a), floor) + np.abs(a - b)
-        bad = np.abs(g - a) > bound
-        assert not bad.any(), (f"sky lanes: {bad.sum()} over bound, worst {np.max(np.abs(g - a) / bound):.2f}x; "
-                               f"strict max rel {max_rel(gpu[sky], o32[sky]):.3e}")
-        assert strict.mean() >= 0.9999, f"sky lanes: only {strict.mean():.6f} within plain {rtol:g}"
-    if sunlanes.any():
-        g, a, b = gpu[sunlanes].astype(np.float64), o32[sunlanes].astype(np.float64), o64[sunlanes]
-        bound = rtol * np.abs(b) + 4 * np.abs(a - b) + 1e-30
-        bad = np.abs(g - b) > bound
-        assert not bad.any(), f"sun lanes: {bad.sum()} over bound, worst {np.max(np.abs(g - b) / bound):.2f}x"
 
 
 # ----------------------------------------------------------------- eval RGB
@@ -339,3 +320,40 @@ def test_full_size_rgb_16M_against_oracle():
         sm = sun_mask(o32, wo)
         assert max_rel(out[~sm], ref[~sm]) < 1e-5
         assert np.all(np.isfinite(out))
+
+
+# ------------------------------------------------------------- sharding
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+def test_sharded_eval_bitwise_equals_whole_batch(variant):
+    """the per-rank slices (sunsky_amd.sharding.shard_range) evaluated
+    separately reproduce the one-GPU result bit for bit, including ragged slices
+    that take the VEC=1 tail kernel."""
+    from sunsky_amd.sharding import shard_range
+    d = angles_dict(5.0, 0.4, np.deg2rad(35), 0.2, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, variant)
+    n = (1 << 16) + 3
+    wi = soa(-hemisphere_wo(n, seed=8))
+    lam = [float(x) for x in range(320, 721, 40)]
+    if variant == "rgb":
+        whole = host(em.eval(ss.SurfaceInteraction3f(wi=wi)))
+    else:
+        whole = host(em.eval_spectral_broadcast(wi, lam))
+    for world in (2, 3, 8):
+        parts = []
+        for r in range(world):
+            a, b = shard_range(n, r, world)
+            if variant == "rgb":
+                parts.append(host(em.eval(ss.SurfaceInteraction3f(wi=wi[:, a:b].contiguous()))))
+            else:
+                parts.append(host(em.eval_spectral_broadcast(wi[:, a:b].contiguous(), lam)))
+        assert np.array_equal(np.concatenate(parts, axis=1), whole), f"world {world}"
+    # the same rays at a 4-byte offset: every plane misaligned -> VEC=1 kernels on every lane
+    flat = torch.empty(3 * n + 1, dtype=torch.float32, device=wi.device)
+    wi_odd = flat[1:].view(3, n)
+    wi_odd.copy_(wi)
+    assert wi_odd.data_ptr() % 16 != 0
+    if variant == "rgb":
+        odd = host(em.eval(ss.SurfaceInteraction3f(wi=wi_odd)))
+    else:
+        odd = host(em.eval_spectral_broadcast(wi_odd, lam))
+    assert np.array_equal(odd, whole)

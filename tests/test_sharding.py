@@ -1,0 +1,68 @@
+"""Multi-rank path on CPU: world_size-2 gloo.  Each rank
+evaluates its slice of one ray batch and rank 0 gathers; the gathered buffer
+must equal the single-process result bit for bit.  The per-rank compute here
+is the oracle (no GPU in this container) -- what is under test is the
+partitioning and the gather, which the GPU path (bench.py --gather) shares."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from sunsky_amd.sharding import gather_radiance, shard_range, shard_sizes
+
+from helpers import angles_dict, hemisphere_wo
+
+SCENE = angles_dict(6.0, 0.3, np.deg2rad(40), 0.1, 1.0, 1.0)
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 4, 5, 17, 1000, 1 << 16, (1 << 16) + 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shard_range_partitions(n, world):
+    spans = [shard_range(n, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    for (a0, a1), (b0, b1) in zip(spans, spans[1:]):
+        assert a1 == b0
+    for a, b in spans:
+        assert (a % 4 == 0 or a == b == n) and b >= a   # 16-byte aligned starts (empty tail shards excepted)
+    sizes = shard_sizes(n, world)
+    assert sum(sizes) == n and max(sizes) - min(sizes) <= 7   # one 4-ray block + a partial tail
+
+
+def test_shard_range_errors():
+    with pytest.raises(ValueError):
+        shard_range(10, 2, 2)
+    with pytest.raises(ValueError):
+        shard_range(10, 0, 0)
+
+
+def _worker(rank, world, port, n, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle as O
+        wi = -hemisphere_wo(n, seed=5)          # every rank can regenerate the batch
+        a, b = shard_range(n, rank, world)
+        local = O.Oracle(SCENE, "rgb", "jit", "f32").eval(wi[a:b])
+        full = gather_radiance(torch.from_numpy(np.ascontiguousarray(local.T)), n)
+        if rank == 0:
+            np.save(out_path, full.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [4096 + 3, 10000])
+def test_gloo_world2_gather_matches_single_process(tmp_path, n):
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "full.npy")
+    mp.start_processes(_worker, args=(2, port, n, out), nprocs=2, join=True, start_method="spawn")
+    import oracle as O
+    ref = O.Oracle(SCENE, "rgb", "jit", "f32").eval(-hemisphere_wo(n, seed=5)).T
+    got = np.load(out)
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref)

@@ -219,7 +219,7 @@ def main():
         traffic, traffic_src = (None, None) if args.no_pmc else pmc_traffic(kname)
         parity = parity_check(ems, wi, outs)
         result = {
-            "metric": "sky-radiance evals/sec (ray-dir x lambda)", "value": value, "unit": "evals/s",
+            "metric": "sky-radiance evals/sec (ray-dir \u00d7 \u03bb) at 1/2/4/8 GPU; max-abs \u0394 vs scalar ref", "value": value, "unit": "evals/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",

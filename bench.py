@@ -237,6 +237,31 @@ def main():
     # ---------------------------------------------------------------- secondary
     if not args.no_secondary:
         sec = {}
+        # Headline kernel with the Infinity Cache defeated: 4 distinct 16M-direction
+        # batches (805 MB of inputs > 256 MiB L3) evaluated round-robin.
+        cold_in = [-hemisphere_dirs(n, seed=777 + 13 * k + rank, device=dev) for k in range(4)]
+        cold_v = [ss._capi.Vec3In(c[0].data_ptr(), c[1].data_ptr(), c[2].data_ptr()) for c in cold_in]
+
+        def cold_step():
+            for k, v in enumerate(cold_v):
+                rc = lib.sunsky_eval(ems[0]._h, v, None, 0, 0, None, n, outs[k % 3].data_ptr(), n, stream)
+                if rc:
+                    raise RuntimeError(lib.sunsky_last_error().decode())
+
+        for _ in range(2):
+            cold_step()
+        tm = KernelTimer()
+        reps = max(3, args.steps // 4)
+        tm.begin()
+        for _ in range(reps):
+            cold_step()
+        tm.end(reps * len(cold_v))
+        ms = tm.mean_ms()
+        sec["rgb_eval_cold_inputs"] = {"kernel_ms": ms, "evals_per_s": n / (ms * 1e-3),
+                                       "achieved_GBps": BYTES_RGB * n / (ms * 1e-3) / 1e9,
+                                       "note": "headline kernel, 4 distinct input batches round-robin so "
+                                               "inputs cannot stay in the 256 MiB Infinity Cache"}
+        del cold_in, cold_v
         # C3: spectral eval, 11 model wavelengths broadcast
         spec = ss.SunskyEmitter(dict(sun_dict(3.0), albedo=0.3), "spectral", precision=args.precision, device=dev)
         lams = [float(x) for x in range(320, 721, 40)]

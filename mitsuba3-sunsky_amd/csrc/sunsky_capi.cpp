@@ -94,14 +94,18 @@ std::string code_object_path() {
 }
 
 // ---------------------------------------------------------------- kernels
+// The sampling kernels are instantiated per variant (RGB / spectral) so each
+// carries only its own tables and registers.
 enum KernelId {
     K_EVAL_RGB_V4, K_EVAL_RGB_V1, K_EVAL_SPEC_BCAST_V2, K_EVAL_SPEC_BCAST_V1, K_EVAL_SPEC_NODES_V2,
-    K_EVAL_SPEC_RAYS, K_SAMPLE_DIRECTION, K_PDF_DIRECTION, K_SAMPLE_WAVELENGTHS, K_SAMPLE_RAY, K_COUNT
+    K_EVAL_SPEC_RAYS, K_SAMPLE_DIRECTION_RGB, K_SAMPLE_DIRECTION_SPEC, K_PDF_DIRECTION, K_SAMPLE_WAVELENGTHS_RGB,
+    K_SAMPLE_WAVELENGTHS_SPEC, K_SAMPLE_RAY_RGB, K_SAMPLE_RAY_SPEC, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v2", "sunsky_eval_spec_bcast_v1",
-    "sunsky_eval_spec_nodes_v2", "sunsky_eval_spec_rays", "sunsky_sample_direction", "sunsky_pdf_direction",
-    "sunsky_sample_wavelengths", "sunsky_sample_ray"};
+    "sunsky_eval_spec_nodes_v2", "sunsky_eval_spec_rays", "sunsky_sample_direction_rgb",
+    "sunsky_sample_direction_spec", "sunsky_pdf_direction", "sunsky_sample_wavelengths_rgb",
+    "sunsky_sample_wavelengths_spec", "sunsky_sample_ray_rgb", "sunsky_sample_ray_spec"};
 
 struct DeviceModule {
     hipModule_t module = nullptr;
@@ -137,7 +141,8 @@ constexpr int kBlock = 256;
 // Grid-stride launches sized to fill every CU several times over
 // (cdna_hip_programming.md Guideline 11).  Workgroups per CU from the
 // tools/kbench.cpp sweep on MI355X (profiles/r01_v2_kbench_grid_sweep.log):
-// RGB eval 64 (60.4 us vs 64.9 us at 16 for 16M directions), spectral 32.
+// RGB eval 64 (60.4 us vs 64.9 us at 16 for 16M directions), spectral 64,
+// sampling 64 (profiles/r01_v5_kbench.log).
 // SUNSKY_AMD_BLOCKS_PER_CU overrides every kernel class.
 int blocks_per_cu(KernelId k) {
     static const int env = [] {
@@ -147,7 +152,8 @@ int blocks_per_cu(KernelId k) {
     if (env) return env;
     switch (k) {
         case K_EVAL_RGB_V4: case K_EVAL_RGB_V1: return 64;
-        case K_EVAL_SPEC_BCAST_V2: case K_EVAL_SPEC_BCAST_V1: case K_EVAL_SPEC_NODES_V2: return 32;
+        case K_EVAL_SPEC_BCAST_V2: case K_EVAL_SPEC_BCAST_V1: case K_EVAL_SPEC_NODES_V2: return 64;
+        case K_SAMPLE_DIRECTION_RGB: case K_SAMPLE_DIRECTION_SPEC: case K_PDF_DIRECTION: return 64;
         default: return 16;
     }
 }
@@ -507,7 +513,8 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
         int nl = spec ? nlam : 0;
         void* args[] = {&K, &ux, &uy, (void*)&it_p.x, (void*)&it_p.y, (void*)&it_p.z, &lam, &lstride, &nl, &active, &n,
                         &ds_d.x, &ds_d.y, &ds_d.z, &ds_pdf, &ds_dist, &ds_p.x, &ds_p.y, &ds_p.z, &weight, &wstride};
-        launch(e->fn(K_SAMPLE_DIRECTION), grid_for(e->mod, K_SAMPLE_DIRECTION, n), (hipStream_t)stream, args);
+        const KernelId k = spec ? K_SAMPLE_DIRECTION_SPEC : K_SAMPLE_DIRECTION_RGB;
+        launch(e->fn(k), grid_for(e->mod, k, n), (hipStream_t)stream, args);
     });
 }
 
@@ -536,7 +543,8 @@ int sunsky_sample_ray(const sunsky_emitter* e, const float* wls, const float* s2
         SunskyKArgs K = e->kargs;
         void* args[] = {&K, &wls, &s2x, &s2y, &s3x, &s3y, &active, &n, &o.x, &o.y, &o.z,
                         &d.x, &d.y, &d.z, &lam, &lstride, &weight, &wstride};
-        launch(e->fn(K_SAMPLE_RAY), grid_for(e->mod, K_SAMPLE_RAY, n), (hipStream_t)stream, args);
+        const KernelId k = e->kargs.variant == kSpectral ? K_SAMPLE_RAY_SPEC : K_SAMPLE_RAY_RGB;
+        launch(e->fn(k), grid_for(e->mod, k, n), (hipStream_t)stream, args);
     });
 }
 
@@ -550,7 +558,8 @@ int sunsky_sample_wavelengths(const sunsky_emitter* e, sunsky_vec3_in w, const f
     return guarded([&] {
         SunskyKArgs K = e->kargs;
         void* args[] = {&K, (void*)&w.x, (void*)&w.y, (void*)&w.z, &sample, &active, &n, &lam, &lstride, &weight, &wstride};
-        launch(e->fn(K_SAMPLE_WAVELENGTHS), grid_for(e->mod, K_SAMPLE_WAVELENGTHS, n), (hipStream_t)stream, args);
+        const KernelId k = e->kargs.variant == kSpectral ? K_SAMPLE_WAVELENGTHS_SPEC : K_SAMPLE_WAVELENGTHS_RGB;
+        launch(e->fn(k), grid_for(e->mod, k, n), (hipStream_t)stream, args);
     });
 }
 

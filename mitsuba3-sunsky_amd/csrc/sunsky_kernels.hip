@@ -49,6 +49,10 @@ struct DirTerms {
     float r;        // 1 / (cos_theta + 0.01)
     float sq;       // safe_sqrt(cos_theta)
     bool active, hit_sun;
+    // sun-disc terms, filled by add_sun_terms() for hit_sun lanes only
+    int sun_pos;    // elevation segment (sunsky.cpp:579-587)
+    float sun_x;    // elevation within the segment
+    float sun_cpsi; // compute_cos_psi (sunsky.h:385-392)
 };
 
 // Shared per-direction terms of eval(), sunsky.cpp:309-314.
@@ -77,7 +81,20 @@ __device__ __forceinline__ DirTerms dir_terms(const SunskyKArgs& K, float3_ wo, 
     t.u = 1.f + t.cg2;
     t.active = mask && (t.cos_theta >= 0.f);
     t.hit_sun = t.active && (d >= K.cos_cutoff);
+    t.sun_pos = 0;
+    t.sun_x = t.sun_cpsi = 0.f;
     return t;
+}
+
+// Sun-disc terms of a direction, once per ray and only on lanes inside the disc.
+// Computed here rather than inside the per-wavelength loops: those calls are
+// loop-invariant, and the compiler would otherwise hoist the acos / cbrt /
+// divisions / sin out of both the loop and the hit_sun branch onto every lane.
+__device__ __forceinline__ void add_sun_terms(const SunskyKArgs& K, DirTerms& t) {
+    if (t.hit_sun) {
+        t.sun_pos = sun_segment(t.cos_theta, &t.sun_x);
+        t.sun_cpsi = cos_psi(t.gamma, K.inv_sin2_half_ap);
+    }
 }
 
 // render_sky (sunsky.cpp:538-555) with the output scale folded in (FastChannel)
@@ -176,16 +193,14 @@ template <bool FAST>
 __device__ __forceinline__ float sun_spec_term(const SunskyKArgs& K, const float* sun_tab, const float* ld_tab,
                                                const DirTerms& t, int lo, float f) {
     const int hi = lo + 1;
-    float xs;
-    int pos = sun_segment(t.cos_theta, &xs);
-    float sa = render_sun_spec(sun_tab, pos, lo, xs), sun = sa;
-    if (f != 0.f) sun = lerpf_(sa, hi < kNbWavelengths ? render_sun_spec(sun_tab, pos, hi, xs) : 0.f, f);
-    float ld = sun_limb_darkening(ld_tab, lo, hi, f, cos_psi(t.gamma, K.inv_sin2_half_ap));
+    float sa = render_sun_spec(sun_tab, t.sun_pos, lo, t.sun_x), sun = sa;
+    if (f != 0.f) sun = lerpf_(sa, hi < kNbWavelengths ? render_sun_spec(sun_tab, t.sun_pos, hi, t.sun_x) : 0.f, f);
+    float ld = sun_limb_darkening(ld_tab, lo, hi, f, t.sun_cpsi);
     return FAST ? K.sun_mul * (sun * ld) : K.sun_scale * sun * ld * K.area_ratio;
 }
 
 // Spectral eval of one per-lane wavelength (sunsky.cpp:325-348); `chans` is
-// indexed by a per-lane channel, so it lives in LDS.
+// indexed by a per-lane channel, so it lives in LDS.  `t` carries add_sun_terms().
 template <bool FAST>
 __device__ __forceinline__ float eval_spec_one(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
                                                const float* sun_tab, const float* ld_tab, const DirTerms& t,
@@ -218,6 +233,9 @@ __device__ __forceinline__ void load_vec(const float* p, size_t i, float v[VEC])
 // Outputs are written once and not re-read by this kernel: non-temporal.
 template <int VEC>
 __device__ __forceinline__ void store_vec(float* p, size_t i, const float v[VEC]) {
+#ifdef SS_PROBE_NOSTORE   // tools/gpu_quick.sh compute-only probe build; never in the product
+    if (v[0] != -1234.5f) return;
+#endif
     if constexpr (VEC == 4) {
         f32x4 q = {v[0], v[1], v[2], v[3]};
         __builtin_nontemporal_store(q, reinterpret_cast<f32x4*>(p + i));
@@ -287,10 +305,42 @@ __device__ __forceinline__ void eval_rgb_body(const SunskyKArgs& K, const float*
 }
 
 // ======================================================================
+// Tables staged in LDS once per workgroup.  Constants that every lane reads
+// with the same index could live in SGPRs, but 11 spectral channels (110
+// floats), 20 TGMM gaussians or a CDF exceed the SGPR file: the compiler then
+// spills them through v_writelane / v_readlane + s_nop hazards inside the hot
+// loop (measured: 696 readlanes in the first sample_direction kernel).  LDS
+// reads with one address per wave are broadcasts, cheap and conflict-free.
+// ======================================================================
+template <typename T>
+__device__ __forceinline__ void lds_copy(T* dst, const T* src, int count) {
+    const int nwords = (int)(count * sizeof(T) / 4);
+    const float* s = reinterpret_cast<const float*>(src);
+    float* d = reinterpret_cast<float*>(dst);
+    for (int w = threadIdx.x; w < nwords; w += blockDim.x) d[w] = s[w];
+}
+
+template <bool FAST> struct ChanLds { typename ChanSel<FAST>::T c[kNbWavelengths]; };
+
+template <bool FAST>
+__device__ __forceinline__ const typename ChanSel<FAST>::T* stage_chans(const SunskyKArgs& K, ChanLds<FAST>* s) {
+    lds_copy(s->c, chan_table<FAST>(K), kNbWavelengths);
+    return s->c;
+}
+
+// ContinuousDistribution over [360, 720] (JIT: 10 nodes, scalar: 2)
+struct SpecDistLds { float pdf[10]; float cdf[9]; float pad; };
+
+__device__ __forceinline__ void stage_spec_dist(const SunskyKArgs& K, SpecDistLds* s) {
+    lds_copy(s->pdf, K.spec_pdf, 10);
+    lds_copy(s->cdf, K.spec_cdf, 9);
+}
+
+// ======================================================================
 // eval(): spectral, one wavelength set broadcast to every direction (the
 // test02/03 eval_full_spec layout and the C3 workload).  Wavelength k maps
-// to channels (lo[k], lo[k] + 1, f[k]) computed on the host: wave-uniform, so
-// the channel constants come from SGPRs.  out plane k at out + k * ostride.
+// to channels (lo[k], lo[k] + 1, f[k]) computed on the host (wave-uniform).
+// out plane k at out + k * ostride.
 // ======================================================================
 struct LambdaSet {
     int m;
@@ -303,7 +353,9 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
                                                      const float* __restrict__ wx, const float* __restrict__ wy,
                                                      const float* __restrict__ wz, const uint8_t* __restrict__ active,
                                                      size_t n, float* __restrict__ out, size_t ostride, float sign) {
-    const auto* chans = chan_table<FAST>(K);
+    __shared__ ChanLds<FAST> S;
+    const auto* chans = stage_chans<FAST>(K, &S);
+    __syncthreads();
     const size_t nvec = n / VEC;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
@@ -318,6 +370,10 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
             t[j] = dir_terms<FAST>(K, to_local(K, mk3(sign * x[j], sign * y[j], sign * z[j])), m[j]);
             any_sun |= t[j].hit_sun;
         }
+        if (any_sun) {
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) add_sun_terms(K, t[j]);
+        }
         for (int k = 0; k < L.m; ++k) {
             const int lo = L.lo[k];
             const float f = L.f[k];
@@ -326,12 +382,14 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o[j] = 0.f;
             } else {
+                const auto ca = chans[lo];
 #pragma unroll
-                for (int j = 0; j < VEC; ++j) o[j] = sky_eval<FAST>(chans[lo], t[j], K.sky_scale);
+                for (int j = 0; j < VEC; ++j) o[j] = sky_eval<FAST>(ca, t[j], K.sky_scale);
                 if (f != 0.f) {
                     if (lo + 1 < kNbWavelengths) {
+                        const auto cb = chans[lo + 1];
 #pragma unroll
-                        for (int j = 0; j < VEC; ++j) o[j] = lerpf_(o[j], sky_eval<FAST>(chans[lo + 1], t[j], K.sky_scale), f);
+                        for (int j = 0; j < VEC; ++j) o[j] = lerpf_(o[j], sky_eval<FAST>(cb, t[j], K.sky_scale), f);
                     } else {
 #pragma unroll
                         for (int j = 0; j < VEC; ++j) o[j] = lerpf_(o[j], 0.f, f);
@@ -357,7 +415,9 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
                                                      const float* __restrict__ wy, const float* __restrict__ wz,
                                                      const uint8_t* __restrict__ active, size_t n,
                                                      float* __restrict__ out, size_t ostride, float sign) {
-    const auto* chans = chan_table<FAST>(K);
+    __shared__ ChanLds<FAST> S;
+    const auto* chans = stage_chans<FAST>(K, &S);
+    __syncthreads();
     const size_t nvec = n / VEC;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
@@ -372,11 +432,18 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
             t[j] = dir_terms<FAST>(K, to_local(K, mk3(sign * x[j], sign * y[j], sign * z[j])), m[j]);
             any_sun |= t[j].hit_sun;
         }
+        if (any_sun) {
 #pragma unroll
+            for (int j = 0; j < VEC; ++j) add_sun_terms(K, t[j]);
+        }
+        // Rolled: one channel's constants (LDS broadcast reads) live at a time;
+        // unrolling lets the compiler hoist all 110 out of the ray loop (184 VGPRs).
+#pragma unroll 1
         for (int c = 0; c < kNbWavelengths; ++c) {
+            const auto ch = chans[c];
             float o[VEC];
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) o[j] = sky_eval<FAST>(chans[c], t[j], K.sky_scale);
+            for (int j = 0; j < VEC; ++j) o[j] = sky_eval<FAST>(ch, t[j], K.sky_scale);
             if (any_sun) {
 #pragma unroll
                 for (int j = 0; j < VEC; ++j)
@@ -390,28 +457,6 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
 }
 
 // ======================================================================
-// Tables staged in LDS once per workgroup
-// ======================================================================
-struct SpecLds {
-    FastChannel fast[kNbWavelengths];
-    SkyChannel ref[kNbWavelengths];
-};
-
-template <typename T>
-__device__ __forceinline__ void lds_copy(T* dst, const T* src, int count) {
-    const int nwords = (int)(count * sizeof(T) / 4);
-    const float* s = reinterpret_cast<const float*>(src);
-    float* d = reinterpret_cast<float*>(dst);
-    for (int w = threadIdx.x; w < nwords; w += blockDim.x) d[w] = s[w];
-}
-
-template <bool FAST>
-__device__ __forceinline__ const typename ChanSel<FAST>::T* stage_chans(const SunskyKArgs& K, SpecLds* s) {
-    if constexpr (FAST) { lds_copy(s->fast, K.fsky, kNbWavelengths); return s->fast; }
-    else { lds_copy(s->ref, K.sky, kNbWavelengths); return s->ref; }
-}
-
-// ======================================================================
 // eval(): spectral with per-ray wavelengths (Mitsuba Spectrum<Float, k>):
 // lambda plane k at lam + k * lstride, out plane k at out + k * ostride.
 // ======================================================================
@@ -421,13 +466,14 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
                                                     const float* __restrict__ lam, size_t lstride, int nlam,
                                                     const uint8_t* __restrict__ active, size_t n,
                                                     float* __restrict__ out, size_t ostride, float sign) {
-    __shared__ SpecLds S;
+    __shared__ ChanLds<FAST> S;
     const auto* chans = stage_chans<FAST>(K, &S);
     __syncthreads();
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool m = active ? active[i] != 0 : true;
         DirTerms t = dir_terms<FAST>(K, to_local(K, mk3(sign * wx[i], sign * wy[i], sign * wz[i])), m);
+        add_sun_terms(K, t);
         for (int k = 0; k < nlam; ++k)
             __builtin_nontemporal_store(eval_spec_one<FAST>(K, chans, K.sun_table, K.sun_ld, t, lam[(size_t)k * lstride + i]),
                                         out + (size_t)k * ostride + i);
@@ -437,60 +483,75 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
 // ======================================================================
 // Sampling: TGMM sky + uniform-cone sun (sunsky.cpp:354-451, 661-763)
 // ======================================================================
-struct SamplerLds {
+// TGMM tables in LDS.  tg/tc are the FAST form of tgmm_pdf's per-gaussian
+// terms: tg = {mu_phi, mu_theta, c / sigma_phi, c / sigma_theta} with
+// c = sqrt(log2(e) / 2), tc = weight / (volume * 2 pi), so that a gaussian
+// costs exp2(-(sx^2 + sy^2)) and one fma.
+struct TgmmLds {
     Gaussian gauss[kNbMixture];
-    FastChannel fast[kNbWavelengths];
-    SkyChannel ref[kNbWavelengths];
-    float sun[kSunRgbTableSize];                 // RGB 3240 / spectral 1980 used
+    float4 tg[kNbMixture];
+    float tc[kNbMixture];
+    float cdf[kNbMixture], pmf[kNbMixture];
+};
+
+__device__ __forceinline__ void stage_tgmm(const SunskyKArgs& K, TgmmLds* s) {
+    lds_copy(s->gauss, K.gauss, kNbMixture);
+    lds_copy(s->cdf, K.gauss_cdf, kNbMixture);
+    lds_copy(s->pmf, K.gauss_pmf, kNbMixture);
+    const int i = threadIdx.x;
+    if (i < kNbMixture) {
+        const float c = 0.84932180028801904272f;   // sqrt(log2(e) / 2)
+        const Gaussian& g = K.gauss[i];
+        s->tg[i] = make_float4(g.mu_phi, g.mu_theta, g.inv_sigma_phi * c, g.inv_sigma_theta * c);
+        s->tc[i] = g.coef * kInvTwoPi;
+    }
+}
+
+template <bool FAST, bool SPEC>
+struct SamplerLds {
+    TgmmLds tgmm;
+    ChanLds<FAST> chans;                          // spectral weights (per-lane channel index)
+    SpecDistLds sdist;
+    float sun[SPEC ? kSunSpecTableSize : kSunRgbTableSize];
     float ld[kNbWavelengths * kNbSunLdParams];
 };
 
-template <bool FAST>
-__device__ __forceinline__ void stage_sampler_lds(const SunskyKArgs& K, SamplerLds* s) {
-    lds_copy(s->gauss, K.gauss, kNbMixture);
-    if (K.variant == kSpectral) {
-        if constexpr (FAST) lds_copy(s->fast, K.fsky, kNbWavelengths);
-        else lds_copy(s->ref, K.sky, kNbWavelengths);
+template <bool FAST, bool SPEC>
+__device__ __forceinline__ void stage_sampler_lds(const SunskyKArgs& K, SamplerLds<FAST, SPEC>* s) {
+    stage_tgmm(K, &s->tgmm);
+    if (SPEC) {
+        stage_chans<FAST>(K, &s->chans);
+        stage_spec_dist(K, &s->sdist);
         lds_copy(s->ld, K.sun_ld, kNbWavelengths * kNbSunLdParams);
     }
-    lds_copy(s->sun, K.sun_table, K.variant == kSpectral ? kSunSpecTableSize : kSunRgbTableSize);
+    lds_copy(s->sun, K.sun_table, SPEC ? kSunSpecTableSize : kSunRgbTableSize);
     __syncthreads();
-}
-
-template <bool FAST>
-__device__ __forceinline__ const typename ChanSel<FAST>::T* sampler_chans(SamplerLds* s) {
-    if constexpr (FAST) return s->fast;
-    else return s->ref;
 }
 
 // DiscreteDistribution::sample_reuse (distr_1d.h:173-183): JIT predicate
 // ((cdf < s) || cdf == 0) && cdf != sum over [0, n-1] (:116-136) -- a prefix
-// count against the SGPR-resident CDF; scalar variants search [first, last].
-__device__ __forceinline__ int discrete_sample_reuse(const SunskyKArgs& K, float value, float* reused) {
+// count against the broadcast CDF; scalar variants search [first, last].
+__device__ __forceinline__ int discrete_sample_reuse(const SunskyKArgs& K, const TgmmLds& T, float value,
+                                                     float* reused) {
     const float s = value * K.gauss_sum;
     int idx;
     if (K.semantics == kJit) {
         idx = 0;
         bool run = true;
-#pragma unroll
+#pragma unroll 4
         for (int i = 0; i < kNbMixture - 1; ++i) {
-            const float c = K.gauss_cdf[i];
+            const float c = T.cdf[i];
             run = run && ((c < s) || c == 0.f) && (c != K.gauss_sum);
             idx += run ? 1 : 0;
         }
     } else {
         idx = K.gauss_first;
-#pragma unroll
+#pragma unroll 4
         for (int i = 0; i < kNbMixture; ++i)
-            if (i >= K.gauss_first && i < K.gauss_last && K.gauss_cdf[i] < s) idx = i + 1;
+            if (i >= K.gauss_first && i < K.gauss_last && T.cdf[i] < s) idx = i + 1;
     }
-    // pmf / cdf gathers by a per-lane index: select chain over the SGPR table
-    float pmf = 0.f, cdf_prev = 0.f;
-#pragma unroll
-    for (int i = 0; i < kNbMixture; ++i) {
-        pmf = (idx == i) ? K.gauss_pmf[i] : pmf;
-        cdf_prev = (idx == i + 1) ? K.gauss_cdf[i] : cdf_prev;
-    }
+    const float pmf = T.pmf[idx];
+    const float cdf_prev = idx > 0 ? T.cdf[idx - 1] : 0.f;
     *reused = (value - cdf_prev * K.gauss_norm) / (pmf * K.gauss_norm);
     return idx;
 }
@@ -504,10 +565,10 @@ __device__ __forceinline__ float3_ sphdir_dev(float theta, float phi) {
 }
 
 // sample_sky, sunsky.cpp:661-689
-__device__ __forceinline__ float3_ sample_sky(const SunskyKArgs& K, const Gaussian* G, float ux, float uy) {
+__device__ __forceinline__ float3_ sample_sky(const SunskyKArgs& K, const TgmmLds& T, float ux, float uy) {
     float temp;
-    int idx = discrete_sample_reuse(K, ux, &temp);
-    const Gaussian& g = G[idx];
+    int idx = discrete_sample_reuse(K, T, ux, &temp);
+    const Gaussian& g = T.gauss[idx];
     float sx = lerpf_(g.cdf_a_phi, g.cdf_b_phi, temp);
     float sy = lerpf_(g.cdf_a_theta, g.cdf_b_theta, uy);
     sx = fminf(fmaxf(sx, kEpsilon), kOneMinusEpsilon);
@@ -546,40 +607,98 @@ __device__ __forceinline__ float3_ sample_sun(const SunskyKArgs& K, float ux, fl
 }
 
 // tgmm_pdf, sunsky.cpp:732-763, with the per-gaussian truncation volume hoisted
-// to the host (coef = weight / volume).
+// to the host (coef = weight / volume); same summation order as the reference.
 template <bool FAST>
-__device__ __forceinline__ float tgmm_pdf(const SunskyKArgs& K, float phi, float theta, bool active) {
+__device__ __forceinline__ float tgmm_pdf(const SunskyKArgs& K, const TgmmLds& T, float phi, float theta,
+                                          bool active) {
     phi -= K.sun_phi - 0.5f * kPi;
     phi = phi < 0.f ? phi + kTwoPi : phi;
     phi = phi > kTwoPi ? phi - kTwoPi : phi;
     active = active && (theta >= 0.f) && (theta <= 0.5f * kPi);
     float pdf = 0.f;
-#pragma unroll
-    for (int i = 0; i < kNbMixture; ++i) {
-        const Gaussian& g = K.gauss[i];
-        float sx = (phi - g.mu_phi) * g.inv_sigma_phi, sy = (theta - g.mu_theta) * g.inv_sigma_theta;
-        float q = fmaf(sy, sy, sx * sx);
-        float e = FAST ? fast_exp2((-0.5f * kLog2e) * q) : expf(-0.5f * q);
-        pdf = fmaf(g.coef, kInvTwoPi * e, pdf);
+    // Partially unrolled so the 20 gaussians' LDS reads are not hoisted out of
+    // the ray loop into ~100 VGPRs.
+    if constexpr (FAST) {
+#pragma unroll 4
+        for (int i = 0; i < kNbMixture; ++i) {
+            const float4 a = T.tg[i];
+            float sx = (phi - a.x) * a.z, sy = (theta - a.y) * a.w;
+            pdf = fmaf(T.tc[i], fast_exp2(-fmaf(sy, sy, sx * sx)), pdf);
+        }
+    } else {
+#pragma unroll 4
+        for (int i = 0; i < kNbMixture; ++i) {
+            const Gaussian& g = T.gauss[i];
+            float sx = (phi - g.mu_phi) * g.inv_sigma_phi, sy = (theta - g.mu_theta) * g.inv_sigma_theta;
+            float q = fmaf(sy, sy, sx * sx);
+            pdf = fmaf(g.coef, kInvTwoPi * expf(-0.5f * q), pdf);
+        }
     }
     return active ? pdf : 0.f;
 }
 
 // compute_pdfs, sunsky.cpp:711-723
 template <bool FAST>
-__device__ __forceinline__ void compute_pdfs(const SunskyKArgs& K, float3_ d, bool check_sun, bool active,
-                                             float* sky_pdf, float* sun_pdf) {
+__device__ __forceinline__ void compute_pdfs(const SunskyKArgs& K, const TgmmLds& T, float3_ d, bool check_sun,
+                                             bool active, float* sky_pdf, float* sun_pdf) {
     float sin_theta = safe_sqrtf_(fmaf(d.x, d.x, d.y * d.y));
     active = active && (d.z >= 0.f) && (sin_theta != 0.f);
     sin_theta = fmaxf(sin_theta, kEpsilon);
     float phi = atan2f(d.y, d.x), theta = unit_angle_z(d);
-    *sky_pdf = tgmm_pdf<FAST>(K, phi, theta, active) / sin_theta;
+    *sky_pdf = tgmm_pdf<FAST>(K, T, phi, theta, active) / sin_theta;
     float cosg = dot3(mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), d);
     *sun_pdf = (!check_sun || cosg >= K.cos_cutoff) ? K.sun_pdf : 0.f;
 }
 
-// sample_direction, sunsky.cpp:399-441.  Weight planes: 3 (RGB) or nlam (spectral).
+// ContinuousDistribution::sample_pdf (distr_1d.h:468-499) over [360, 720]
+__device__ __forceinline__ float spectral_sample_pdf(const SunskyKArgs& K, const SpecDistLds& D, float sample,
+                                                     float* pdf_out) {
+    sample *= K.spec_integral;
+    const int nint = K.spec_size - 1;
+    int idx = 0;
+    if (K.semantics == kJit) {
+        bool run = true;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (i < nint - 1) {
+                const float c = D.cdf[i];
+                run = run && ((c < sample) || c == 0.f) && (c != K.spec_integral);
+                idx += run ? 1 : 0;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (i < nint - 1 && D.cdf[i] < sample) idx = i + 1;
+    }
+    const float y0 = D.pdf[idx], y1 = D.pdf[idx + 1];
+    const float c0 = idx > 0 ? D.cdf[idx - 1] : 0.f;
+    sample = (sample - c0) * K.spec_inv_interval;
+    float t_linear = (y0 - safe_sqrtf_(fmaf(y0, y0, 2.f * sample * (y1 - y0)))) * (1.f / (y0 - y1));
+    float t_const = sample * (1.f / y0);
+    float t = (y0 == y1) ? t_const : t_linear;
+    *pdf_out = fmaf(t, y1 - y0, y0) * K.spec_norm;
+    return fmaf((float)idx + t, K.spec_interval, 360.f);
+}
+
+// sample_wavelengths, sunsky.cpp:463-480 (spectral: 4 shifted samples, Spectrum<Float, 4>)
 template <bool FAST>
+__device__ __forceinline__ void sample_wavelengths_one(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
+                                                       const SpecDistLds& D, const float* sun_tab,
+                                                       const float* ld_tab, const DirTerms& t, float sample,
+                                                       float lam[4], float w[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float s = sample + (float)k / 4.f;   // math::sample_shifted, math.h:408-431
+        s = s > 1.f ? s - 1.f : s;
+        float lpdf;
+        lam[k] = spectral_sample_pdf(K, D, s, &lpdf);
+        w[k] = eval_spec_one<FAST>(K, chans, sun_tab, ld_tab, t, lam[k]) / lpdf;
+    }
+}
+
+// sample_direction, sunsky.cpp:399-441.  Weight planes: 3 (RGB) or nlam (spectral).
+template <bool FAST, bool SPEC>
 __device__ __forceinline__ void sample_direction_body(
     const SunskyKArgs& K, const float* __restrict__ ux, const float* __restrict__ uy,
     const float* __restrict__ px, const float* __restrict__ py, const float* __restrict__ pz,
@@ -587,21 +706,20 @@ __device__ __forceinline__ void sample_direction_body(
     float* __restrict__ dx, float* __restrict__ dy, float* __restrict__ dz, float* __restrict__ pdf,
     float* __restrict__ dist, float* __restrict__ opx, float* __restrict__ opy, float* __restrict__ opz,
     float* __restrict__ weight, size_t wstride) {
-    __shared__ SamplerLds S;
-    stage_sampler_lds<FAST>(K, &S);
-    const auto* chans = sampler_chans<FAST>(&S);
+    __shared__ SamplerLds<FAST, SPEC> S;
+    stage_sampler_lds<FAST, SPEC>(K, &S);
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool act = active ? active[i] != 0 : true;
         const float sx = ux[i], sy = uy[i];
         const bool pick_sky = sx < K.w_sky;
         float3_ sd;
-        if (pick_sky) sd = sample_sky(K, S.gauss, sx / K.w_sky, sy);
+        if (pick_sky) sd = sample_sky(K, S.tgmm, sx / K.w_sky, sy);
         else sd = sample_sun(K, (sx - K.w_sky) / (1.f - K.w_sky), sy);
         act = act && (sd.z >= 0.f);
         float3_ d = to_world(K, sd);
         float skyp, sunp;
-        compute_pdfs<FAST>(K, sd, pick_sky, act, &skyp, &sunp);
+        compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
         float pd = lerpf_(sunp, skyp, K.w_sky);
         __builtin_nontemporal_store(d.x, dx + i);
         __builtin_nontemporal_store(d.y, dy + i);
@@ -616,7 +734,7 @@ __device__ __forceinline__ void sample_direction_body(
         }
         // weight = eval(si{wi = -d}) / pdf, zeroed when not finite (sunsky.cpp:430-439)
         float3_ wo = to_local(K, d);
-        if (K.variant == kRGB) {
+        if constexpr (!SPEC) {
             float e[3];
             eval_rgb_local<FAST>(K, S.sun, wo, act, e);
 #pragma unroll
@@ -626,8 +744,9 @@ __device__ __forceinline__ void sample_direction_body(
             }
         } else {
             DirTerms t = dir_terms<FAST>(K, wo, act);
+            add_sun_terms(K, t);
             for (int k = 0; k < nlam; ++k) {
-                float e = eval_spec_one<FAST>(K, chans, S.sun, S.ld, t, lam[(size_t)k * lstride + i]);
+                float e = eval_spec_one<FAST>(K, S.chans.c, S.sun, S.ld, t, lam[(size_t)k * lstride + i]);
                 float w = e / pd;
                 weight[(size_t)k * wstride + i] = isfinite(w) ? w : 0.f;
             }
@@ -641,89 +760,47 @@ __device__ __forceinline__ void pdf_direction_body(const SunskyKArgs& K, const f
                                                    const float* __restrict__ dy, const float* __restrict__ dz,
                                                    const uint8_t* __restrict__ active, size_t n,
                                                    float* __restrict__ pdf) {
+    __shared__ TgmmLds T;
+    stage_tgmm(K, &T);
+    __syncthreads();
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool act = active ? active[i] != 0 : true;
         float3_ l = to_local(K, mk3(dx[i], dy[i], dz[i]));
         float skyp, sunp;
-        compute_pdfs<FAST>(K, l, true, true, &skyp, &sunp);
+        compute_pdfs<FAST>(K, T, l, true, true, &skyp, &sunp);
         float pd = lerpf_(sunp, skyp, K.w_sky);
         __builtin_nontemporal_store(act ? pd : 0.f, pdf + i);
     }
 }
 
-// ContinuousDistribution::sample_pdf (distr_1d.h:468-499) over [360, 720]
-__device__ __forceinline__ float spectral_sample_pdf(const SunskyKArgs& K, float sample, float* pdf_out) {
-    sample *= K.spec_integral;
-    const int nint = K.spec_size - 1;
-    int idx = 0;
-    if (K.semantics == kJit) {
-        bool run = true;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            if (i < nint - 1) {
-                const float c = K.spec_cdf[i];
-                run = run && ((c < sample) || c == 0.f) && (c != K.spec_integral);
-                idx += run ? 1 : 0;
-            }
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            if (i < nint - 1 && K.spec_cdf[i] < sample) idx = i + 1;
-    }
-    float y0 = 0.f, y1 = 0.f, c0 = 0.f;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) {
-        y0 = idx == i ? K.spec_pdf[i] : y0;
-        y1 = idx == i ? K.spec_pdf[i + 1] : y1;
-        c0 = idx == i + 1 ? K.spec_cdf[i] : c0;
-    }
-    sample = (sample - c0) * K.spec_inv_interval;
-    float t_linear = (y0 - safe_sqrtf_(fmaf(y0, y0, 2.f * sample * (y1 - y0)))) * (1.f / (y0 - y1));
-    float t_const = sample * (1.f / y0);
-    float t = (y0 == y1) ? t_const : t_linear;
-    *pdf_out = fmaf(t, y1 - y0, y0) * K.spec_norm;
-    return fmaf((float)idx + t, K.spec_interval, 360.f);
-}
-
-// sample_wavelengths, sunsky.cpp:463-480 (spectral: 4 shifted samples, Spectrum<Float, 4>)
-template <bool FAST>
-__device__ __forceinline__ void sample_wavelengths_one(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
-                                                       const float* sun_tab, const float* ld_tab, const DirTerms& t,
-                                                       float sample, float lam[4], float w[4]) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        float s = sample + (float)k / 4.f;   // math::sample_shifted, math.h:408-431
-        s = s > 1.f ? s - 1.f : s;
-        float lpdf;
-        lam[k] = spectral_sample_pdf(K, s, &lpdf);
-        w[k] = eval_spec_one<FAST>(K, chans, sun_tab, ld_tab, t, lam[k]) / lpdf;
-    }
-}
-
-template <bool FAST>
+template <bool FAST, bool SPEC>
 __device__ __forceinline__ void sample_wavelengths_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                                         const float* __restrict__ wy, const float* __restrict__ wz,
                                                         const float* __restrict__ sample, const uint8_t* __restrict__ active,
                                                         size_t n, float* __restrict__ lam_out, size_t lstride,
                                                         float* __restrict__ weight, size_t wstride) {
-    __shared__ SpecLds S;
-    const auto* chans = stage_chans<FAST>(K, &S);
+    __shared__ ChanLds<FAST> S;
+    __shared__ SpecDistLds D;
+    if (SPEC) {
+        stage_chans<FAST>(K, &S);
+        stage_spec_dist(K, &D);
+    }
     __syncthreads();
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool act = active ? active[i] != 0 : true;
         float3_ wo = to_local(K, mk3(-wx[i], -wy[i], -wz[i]));
-        if (K.variant == kRGB) {
+        if constexpr (!SPEC) {
             float e[3];
             eval_rgb_local<FAST>(K, K.sun_table, wo, act, e);
             for (int c = 0; c < 3; ++c) weight[(size_t)c * wstride + i] = e[c];
             for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = 0.f;
         } else {
             DirTerms t = dir_terms<FAST>(K, wo, act);
+            add_sun_terms(K, t);
             float lam[4], w[4];
-            sample_wavelengths_one<FAST>(K, chans, K.sun_table, K.sun_ld, t, sample[i], lam, w);
+            sample_wavelengths_one<FAST>(K, S.c, D, K.sun_table, K.sun_ld, t, sample[i], lam, w);
             for (int k = 0; k < 4; ++k) {
                 lam_out[(size_t)k * lstride + i] = lam[k];
                 weight[(size_t)k * wstride + i] = w[k];
@@ -733,7 +810,7 @@ __device__ __forceinline__ void sample_wavelengths_body(const SunskyKArgs& K, co
 }
 
 // sample_ray, sunsky.cpp:354-397
-template <bool FAST>
+template <bool FAST, bool SPEC>
 __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const float* __restrict__ wls,
                                                 const float* __restrict__ s2x, const float* __restrict__ s2y,
                                                 const float* __restrict__ s3x, const float* __restrict__ s3y,
@@ -742,9 +819,8 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
                                                 float* __restrict__ dxo, float* __restrict__ dyo, float* __restrict__ dzo,
                                                 float* __restrict__ lam_out, size_t lstride,
                                                 float* __restrict__ weight, size_t wstride) {
-    __shared__ SamplerLds S;
-    stage_sampler_lds<FAST>(K, &S);
-    const auto* chans = sampler_chans<FAST>(&S);
+    __shared__ SamplerLds<FAST, SPEC> S;
+    stage_sampler_lds<FAST, SPEC>(K, &S);
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool act = active ? active[i] != 0 : true;
@@ -753,26 +829,27 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
         const float sx = s3x[i], sy = s3y[i];
         const bool pick_sky = sx < K.w_sky;
         float3_ d;
-        if (pick_sky) d = sample_sky(K, S.gauss, sx / K.w_sky, sy);
+        if (pick_sky) d = sample_sky(K, S.tgmm, sx / K.w_sky, sy);
         else d = sample_sun(K, (sx - K.w_sky) / (1.f - K.w_sky), sy);
         float3_ dw = to_world(K, mk3(-d.x, -d.y, -d.z));
         act = act && (d.z >= 0.f);
         float skyp, sunp;
-        compute_pdfs<FAST>(K, d, pick_sky, act, &skyp, &sunp);
+        compute_pdfs<FAST>(K, S.tgmm, d, pick_sky, act, &skyp, &sunp);
         float pd = lerpf_(sunp, skyp, K.w_sky);
         pd *= kInvPi * (1.f / (K.bs_radius * K.bs_radius));
         act = act && pd > 0.f;
         float3_ wo = to_local(K, mk3(-dw.x, -dw.y, -dw.z));
         float w[4];
         int nw;
-        if (K.variant == kRGB) {
+        if constexpr (!SPEC) {
             eval_rgb_local<FAST>(K, S.sun, wo, act, w);
             nw = 3;
             for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = 0.f;
         } else {
             DirTerms t = dir_terms<FAST>(K, wo, act);
+            add_sun_terms(K, t);
             float lam[4];
-            sample_wavelengths_one<FAST>(K, chans, S.sun, S.ld, t, wls[i], lam, w);
+            sample_wavelengths_one<FAST>(K, S.chans.c, S.sdist, S.sun, S.ld, t, wls[i], lam, w);
             for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = lam[k];
             nw = 4;
         }
@@ -834,16 +911,18 @@ SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v2_ref, 2, false)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_fast, true)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_ref, false)
 
-#define SS_SAMPLE_DIRECTION(NAME, FAST)                                                                       \
+#define SS_SAMPLE_DIRECTION(NAME, FAST, SPEC)                                                                 \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
         SunskyKArgs K, const float* ux, const float* uy, const float* px, const float* py, const float* pz,   \
         const float* lam, size_t lstride, int nlam, const uint8_t* active, size_t n, float* dx, float* dy,     \
         float* dz, float* pdf, float* dist, float* opx, float* opy, float* opz, float* weight, size_t wstride) { \
-        sample_direction_body<FAST>(K, ux, uy, px, py, pz, lam, lstride, nlam, active, n, dx, dy, dz, pdf,     \
-                                    dist, opx, opy, opz, weight, wstride);                                     \
+        sample_direction_body<FAST, SPEC>(K, ux, uy, px, py, pz, lam, lstride, nlam, active, n, dx, dy, dz,    \
+                                          pdf, dist, opx, opy, opz, weight, wstride);                          \
     }
-SS_SAMPLE_DIRECTION(sunsky_sample_direction_fast, true)
-SS_SAMPLE_DIRECTION(sunsky_sample_direction_ref, false)
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_fast, true, false)
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_ref, false, false)
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_fast, true, true)
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_ref, false, true)
 
 #define SS_PDF_DIRECTION(NAME, FAST)                                                                          \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
@@ -854,22 +933,26 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_ref, false)
 SS_PDF_DIRECTION(sunsky_pdf_direction_fast, true)
 SS_PDF_DIRECTION(sunsky_pdf_direction_ref, false)
 
-#define SS_SAMPLE_WAVELENGTHS(NAME, FAST)                                                                     \
+#define SS_SAMPLE_WAVELENGTHS(NAME, FAST, SPEC)                                                               \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
         SunskyKArgs K, const float* wx, const float* wy, const float* wz, const float* sample,                 \
         const uint8_t* active, size_t n, float* lam, size_t lstride, float* weight, size_t wstride) {          \
-        sample_wavelengths_body<FAST>(K, wx, wy, wz, sample, active, n, lam, lstride, weight, wstride);        \
+        sample_wavelengths_body<FAST, SPEC>(K, wx, wy, wz, sample, active, n, lam, lstride, weight, wstride);  \
     }
-SS_SAMPLE_WAVELENGTHS(sunsky_sample_wavelengths_fast, true)
-SS_SAMPLE_WAVELENGTHS(sunsky_sample_wavelengths_ref, false)
+SS_SAMPLE_WAVELENGTHS(sunsky_sample_wavelengths_rgb_fast, true, false)
+SS_SAMPLE_WAVELENGTHS(sunsky_sample_wavelengths_rgb_ref, false, false)
+SS_SAMPLE_WAVELENGTHS(sunsky_sample_wavelengths_spec_fast, true, true)
+SS_SAMPLE_WAVELENGTHS(sunsky_sample_wavelengths_spec_ref, false, true)
 
-#define SS_SAMPLE_RAY(NAME, FAST)                                                                             \
+#define SS_SAMPLE_RAY(NAME, FAST, SPEC)                                                                       \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
         SunskyKArgs K, const float* wls, const float* s2x, const float* s2y, const float* s3x,                 \
         const float* s3y, const uint8_t* active, size_t n, float* ox, float* oy, float* oz, float* dx,         \
         float* dy, float* dz, float* lam, size_t lstride, float* weight, size_t wstride) {                     \
-        sample_ray_body<FAST>(K, wls, s2x, s2y, s3x, s3y, active, n, ox, oy, oz, dx, dy, dz, lam, lstride,     \
-                              weight, wstride);                                                                \
+        sample_ray_body<FAST, SPEC>(K, wls, s2x, s2y, s3x, s3y, active, n, ox, oy, oz, dx, dy, dz, lam,        \
+                                    lstride, weight, wstride);                                                 \
     }
-SS_SAMPLE_RAY(sunsky_sample_ray_fast, true)
-SS_SAMPLE_RAY(sunsky_sample_ray_ref, false)
+SS_SAMPLE_RAY(sunsky_sample_ray_rgb_fast, true, false)
+SS_SAMPLE_RAY(sunsky_sample_ray_rgb_ref, false, false)
+SS_SAMPLE_RAY(sunsky_sample_ray_spec_fast, true, true)
+SS_SAMPLE_RAY(sunsky_sample_ray_spec_ref, false, true)

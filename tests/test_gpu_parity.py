@@ -357,3 +357,20 @@ def test_sharded_eval_bitwise_equals_whole_batch(variant):
     else:
         odd = host(em.eval_spectral_broadcast(wi_odd, lam))
     assert np.array_equal(odd, whole)
+
+
+def test_config1_scalar_rgb_grid_at_solar_noon():
+    """BASELINE configs[0]: 256x256 (theta, phi) grid, T = 3, albedo 0.1, solar noon in
+    time mode (hour 11.7753, default Tokyo location / date), scalar_rgb semantics."""
+    d = {"type": "sunsky", "turbidity": 3.0, "albedo": 0.1, "hour": 11.7753}
+    em = ss.load_dict(d, variant="rgb", semantics="scalar")
+    o32, o64 = O.Oracle(d, "rgb", "scalar", "f32"), O.Oracle(d, "rgb", "scalar", "f64")
+    info = o32.info()
+    # the sun of SURVEY.md §8d: elevation ~76.57 deg (survey rounding)
+    assert abs(np.degrees(np.arcsin(info["sun_dir_world"][2])) - 76.568) < 5e-2
+    ph, th = np.meshgrid(np.linspace(0, 2 * np.pi, 256, dtype=np.float32),
+                         np.linspace(0, np.pi / 2, 256, dtype=np.float32))
+    wo = np.stack([np.cos(ph) * np.sin(th), np.sin(ph) * np.sin(th), np.cos(th)], -1).reshape(-1, 3)
+    wo = wo.astype(np.float32)
+    out = host(em.eval(ss.SurfaceInteraction3f(wi=soa(-wo)))).T
+    assert_parity(out, o32.eval(-wo), o64.eval(-wo), sun_mask(o32, wo))

@@ -4,7 +4,9 @@
 // n uniform upper-hemisphere directions, and times kernels of the code object
 // by name with hipEvents over back-to-back launches, for several grid sizes.
 //
-//   kbench <hsaco> <rgb|spec> <n> <iters> <blocks_per_cu,...> <kernel> [kernel ...]
+//   kbench <hsaco> <rgb|spec|sample|pdf> <n> <iters> <blocks_per_cu,...> <kernel> [kernel ...]
+// rgb / spec: eval kernels on uniform upper-hemisphere directions (C2 / C3 emitters);
+// sample / pdf: sample_direction (ds.dist, ds.p not requested) / pdf_direction (C4 emitter).
 //
 // Build: make -C tools kbench
 #include <hip/hip_runtime_api.h>
@@ -52,13 +54,14 @@ int main(int argc, char** argv) {
         while (std::getline(ss, tok, ',')) bpcu.push_back(std::atoi(tok.c_str()));
     }
     const bool spec = mode == "spec";
+    const bool sampling = mode == "sample" || mode == "pdf";
     const char* pack = std::getenv("SUNSKY_AMD_DATASET");
     std::string pack_path = pack ? pack : "mitsuba3-sunsky_amd/data/sunsky_datasets.pack";
 
     Properties props;
-    props.set_float("turbidity", spec ? 3.0 : 2.0);
-    props.set_float("albedo", spec ? 0.3 : 0.1);
-    double th = (90.0 - 45.0) * M_PI / 180.0;
+    props.set_float("turbidity", spec || sampling ? 3.0 : 2.0);
+    props.set_float("albedo", spec || sampling ? 0.3 : 0.1);
+    double th = (90.0 - (sampling ? 30.0 : 45.0)) * M_PI / 180.0;
     props.set_vector3("sun_direction", (float)std::sin(th), 0.f, (float)std::cos(th));
     SunskyModel model(props, spec ? kSpectral : kRGB, kJit, pack_path);
 
@@ -81,7 +84,7 @@ int main(int argc, char** argv) {
         float ct = U(rng), ph = 2.f * (float)M_PI * U(rng), st = std::sqrt(std::max(0.f, 1 - ct * ct));
         hx[i] = -st * std::cos(ph); hy[i] = -st * std::sin(ph); hz[i] = -ct;
     }
-    const int nout = spec ? 11 : 3;
+    const int nout = spec ? 11 : (mode == "pdf" ? 1 : 3);
     float *wx, *wy, *wz, *out;
     CK(hipMalloc(&wx, n * 4)); CK(hipMalloc(&wy, n * 4)); CK(hipMalloc(&wz, n * 4));
     CK(hipMalloc(&out, n * 4 * nout));
@@ -98,7 +101,30 @@ int main(int argc, char** argv) {
     const uint8_t* active = nullptr;
     size_t ostride = n;
     float sign = -1.f;
-    const double bytes = spec ? (12.0 + 44.0) * n : 24.0 * n;
+    const double bytes = spec ? (12.0 + 44.0) * n : mode == "sample" ? 36.0 * n : mode == "pdf" ? 16.0 * n : 24.0 * n;
+    // sampling inputs: u in [0,1)^2 (reuses wx / wy), outputs d (3 planes), pdf, RGB weight
+    float *dd = nullptr, *pdf = nullptr, *wgt = nullptr;
+    if (sampling) {
+        std::vector<float> u(2 * n);
+        for (auto& v : u) v = U(rng);
+        CK(hipMemcpy(wx, u.data(), n * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(wy, u.data() + n, n * 4, hipMemcpyHostToDevice));
+        CK(hipMalloc(&dd, 3 * n * 4)); CK(hipMalloc(&pdf, n * 4)); CK(hipMalloc(&wgt, 3 * n * 4));
+        if (mode == "pdf") {   // directions on the whole sphere
+            for (size_t i = 0; i < n; ++i) {
+                float ct = 2 * U(rng) - 1, ph = 2.f * (float)M_PI * U(rng), st = std::sqrt(std::max(0.f, 1 - ct * ct));
+                hx[i] = st * std::cos(ph); hy[i] = st * std::sin(ph); hz[i] = ct;
+            }
+            CK(hipMemcpy(dd, hx.data(), n * 4, hipMemcpyHostToDevice));
+            CK(hipMemcpy(dd + n, hy.data(), n * 4, hipMemcpyHostToDevice));
+            CK(hipMemcpy(dd + 2 * n, hz.data(), n * 4, hipMemcpyHostToDevice));
+        }
+    }
+    const float* nullf = nullptr;
+    float* nullo = nullptr;
+    size_t zero = 0;
+    int nl0 = 0;
+    float *ddy = dd ? dd + n : nullptr, *ddz = dd ? dd + 2 * n : nullptr;
     std::vector<float> ref;
     for (int a = 6; a < argc; ++a) {
         hipFunction_t f;
@@ -110,7 +136,10 @@ int main(int argc, char** argv) {
             unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((items + 255) / 256, (size_t)cu * mult));
             void* args_rgb[] = {&K, &wx, &wy, &wz, &active, &n, &out, &ostride, &sign};
             void* args_spec[] = {&K, &L, &wx, &wy, &wz, &active, &n, &out, &ostride, &sign};
-            void** args = spec ? args_spec : args_rgb;
+            void* args_sample[] = {&K, &wx, &wy, &nullf, &nullf, &nullf, &nullf, &zero, &nl0, &active, &n,
+                                   &dd, &ddy, &ddz, &pdf, &nullo, &nullo, &nullo, &nullo, &wgt, &n};
+            void* args_pdf[] = {&K, &dd, &ddy, &ddz, &active, &n, &pdf};
+            void** args = spec ? args_spec : mode == "sample" ? args_sample : mode == "pdf" ? args_pdf : args_rgb;
             for (int w = 0; w < 3; ++w) CK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
             hipEvent_t e0, e1;
             CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -124,7 +153,7 @@ int main(int argc, char** argv) {
             double us = 1e3 * ms / iters;
             // checksum against the first kernel
             std::vector<float> h((size_t)nout * n);
-            CK(hipMemcpy(h.data(), out, h.size() * 4, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(h.data(), sampling ? (mode == "pdf" ? pdf : wgt) : out, h.size() * 4, hipMemcpyDeviceToHost));
             double maxrel = 0;
             if (ref.empty()) ref = h;
             else

@@ -48,6 +48,7 @@ struct DirTerms {
     float cos_theta, gamma, cg, cg2, u;   // u = 1 + cos^2 gamma
     float r;        // 1 / (cos_theta + 0.01)
     float sq;       // safe_sqrt(cos_theta)
+    float h;        // |wo -/+ n| / 2, so gamma = 2 asin(h) or pi - 2 asin(h)
     bool active, hit_sun;
     // sun-disc terms, filled by add_sun_terms() for hit_sun lanes only
     int sun_pos;    // elevation segment (sunsky.cpp:579-587)
@@ -65,6 +66,7 @@ __device__ __forceinline__ DirTerms dir_terms(const SunskyKArgs& K, float3_ wo, 
     // unit_angle(n, wo) = 2 asin(|wo -/+ n| / 2)
     float3_ v = mk3(wo.x - mulsignf_(sn.x, d), wo.y - mulsignf_(sn.y, d), wo.z - mulsignf_(sn.z, d));
     float h = 0.5f * (FAST ? fast_sqrt(dot3(v, v)) : sqrtf(dot3(v, v)));
+    t.h = h;
     float temp = 2.f * asinf(h);
     t.gamma = d >= 0.f ? temp : kPi - temp;
     if (FAST) {
@@ -90,11 +92,36 @@ __device__ __forceinline__ DirTerms dir_terms(const SunskyKArgs& K, float3_ wo, 
 // Computed here rather than inside the per-wavelength loops: those calls are
 // loop-invariant, and the compiler would otherwise hoist the acos / cbrt /
 // divisions / sin out of both the loop and the hit_sun branch onto every lane.
+//
+// FAST: sin(gamma) from the half chord, sin(2 asin h) = sin(pi - 2 asin h) = 2h sqrt(1 - h^2),
+// instead of sin() of the reconstructed angle; the segment fraction pos / 45 as a
+// product with 1/45.
+template <bool FAST>
 __device__ __forceinline__ void add_sun_terms(const SunskyKArgs& K, DirTerms& t) {
     if (t.hit_sun) {
-        t.sun_pos = sun_segment(t.cos_theta, &t.sun_x);
-        t.sun_cpsi = cos_psi(t.gamma, K.inv_sin2_half_ap);
+        if constexpr (FAST) {
+            float elevation = kHalfPi - acosf(t.cos_theta);
+            float seg = cbrtf(2.f * elevation * kInvPi) * (float)kNbSunSegments;
+            int pos = seg > 0.f ? (int)floorf(seg) : 0;
+            pos = pos < kNbSunSegments - 1 ? pos : kNbSunSegments - 1;
+            float frac = (float)pos * (1.f / (float)kNbSunSegments);
+            t.sun_pos = pos;
+            t.sun_x = elevation - kHalfPi * (frac * frac * frac);
+            float h2 = t.h * t.h;
+            float sg2 = 4.f * h2 * (1.f - h2);                    // sin^2(gamma)
+            t.sun_cpsi = safe_sqrtf_(fmaf(-K.inv_sin2_half_ap, sg2, 1.f));
+        } else {
+            t.sun_pos = sun_segment(t.cos_theta, &t.sun_x);
+            t.sun_cpsi = cos_psi(t.gamma, K.inv_sin2_half_ap);
+        }
     }
+}
+
+// Division: correctly rounded in the reference kernels, v_rcp_f32 (1 ulp) in FAST.
+template <bool FAST>
+__device__ __forceinline__ float fdiv(float a, float b) {
+    if constexpr (FAST) return a * fast_rcp(b);
+    else return a / b;
 }
 
 // render_sky (sunsky.cpp:538-555) with the output scale folded in (FastChannel)
@@ -161,11 +188,10 @@ __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const float
 #pragma unroll
         for (int c = 0; c < 3; ++c) out[c] = sky_fast(K.fsky[c], t);   // sky_scale and CIE folded
         if (t.hit_sun) {
-            float xs;
-            int pos = sun_segment(t.cos_theta, &xs);
-            float cpsi = cos_psi(t.gamma, K.inv_sin2_half_ap);
+            add_sun_terms<true>(K, t);
 #pragma unroll 1
-            for (int c = 0; c < 3; ++c) out[c] += K.sun_mul * render_sun_rgb_compact(sun_tab, pos, c, xs, cpsi);
+            for (int c = 0; c < 3; ++c)
+                out[c] += K.sun_mul * render_sun_rgb_compact(sun_tab, t.sun_pos, c, t.sun_x, t.sun_cpsi);
         }
 #pragma unroll
         for (int c = 0; c < 3; ++c) out[c] = t.active ? out[c] : 0.f;
@@ -372,7 +398,7 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
         }
         if (any_sun) {
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) add_sun_terms(K, t[j]);
+            for (int j = 0; j < VEC; ++j) add_sun_terms<FAST>(K, t[j]);
         }
         for (int k = 0; k < L.m; ++k) {
             const int lo = L.lo[k];
@@ -434,7 +460,7 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
         }
         if (any_sun) {
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) add_sun_terms(K, t[j]);
+            for (int j = 0; j < VEC; ++j) add_sun_terms<FAST>(K, t[j]);
         }
         // Rolled: one channel's constants (LDS broadcast reads) live at a time;
         // unrolling lets the compiler hoist all 110 out of the ray loop (184 VGPRs).
@@ -473,7 +499,7 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool m = active ? active[i] != 0 : true;
         DirTerms t = dir_terms<FAST>(K, to_local(K, mk3(sign * wx[i], sign * wy[i], sign * wz[i])), m);
-        add_sun_terms(K, t);
+        add_sun_terms<FAST>(K, t);
         for (int k = 0; k < nlam; ++k)
             __builtin_nontemporal_store(eval_spec_one<FAST>(K, chans, K.sun_table, K.sun_ld, t, lam[(size_t)k * lstride + i]),
                                         out + (size_t)k * ostride + i);
@@ -531,6 +557,7 @@ __device__ __forceinline__ void stage_sampler_lds(const SunskyKArgs& K, SamplerL
 // DiscreteDistribution::sample_reuse (distr_1d.h:173-183): JIT predicate
 // ((cdf < s) || cdf == 0) && cdf != sum over [0, n-1] (:116-136) -- a prefix
 // count against the broadcast CDF; scalar variants search [first, last].
+template <bool FAST>
 __device__ __forceinline__ int discrete_sample_reuse(const SunskyKArgs& K, const TgmmLds& T, float value,
                                                      float* reused) {
     const float s = value * K.gauss_sum;
@@ -552,7 +579,7 @@ __device__ __forceinline__ int discrete_sample_reuse(const SunskyKArgs& K, const
     }
     const float pmf = T.pmf[idx];
     const float cdf_prev = idx > 0 ? T.cdf[idx - 1] : 0.f;
-    *reused = (value - cdf_prev * K.gauss_norm) / (pmf * K.gauss_norm);
+    *reused = (value - cdf_prev * K.gauss_norm) / (pmf * K.gauss_norm);   // exact: see sample_direction_body
     return idx;
 }
 
@@ -565,9 +592,10 @@ __device__ __forceinline__ float3_ sphdir_dev(float theta, float phi) {
 }
 
 // sample_sky, sunsky.cpp:661-689
+template <bool FAST>
 __device__ __forceinline__ float3_ sample_sky(const SunskyKArgs& K, const TgmmLds& T, float ux, float uy) {
     float temp;
-    int idx = discrete_sample_reuse(K, T, ux, &temp);
+    int idx = discrete_sample_reuse<FAST>(K, T, ux, &temp);
     const Gaussian& g = T.gauss[idx];
     float sx = lerpf_(g.cdf_a_phi, g.cdf_b_phi, temp);
     float sy = lerpf_(g.cdf_a_theta, g.cdf_b_theta, uy);
@@ -582,12 +610,13 @@ __device__ __forceinline__ float3_ sample_sky(const SunskyKArgs& K, const TgmmLd
 
 // square_to_uniform_cone (warp.h:533-551) with the concentric disk of
 // warp.h:54-90 using one shared sin/cos reduction.
+template <bool FAST>
 __device__ __forceinline__ float3_ uniform_cone_dev(float sx, float sy, float cos_cutoff) {
     float x = fmaf(2.f, sx, -1.f), y = fmaf(2.f, sy, -1.f);
     bool is_zero = (x == 0.f) && (y == 0.f);
     bool q13 = fabsf(x) < fabsf(y);
     float r = q13 ? y : x, rp = q13 ? x : y;
-    float phi = 0.25f * kPi * rp / r;
+    float phi = fdiv<FAST>(0.25f * kPi * rp, r);
     if (q13) phi = 0.5f * kPi - phi;
     if (is_zero) phi = 0.f;
     float s, c;
@@ -601,9 +630,10 @@ __device__ __forceinline__ float3_ uniform_cone_dev(float sx, float sy, float co
 }
 
 // sample_sun, sunsky.cpp:697-701
+template <bool FAST>
 __device__ __forceinline__ float3_ sample_sun(const SunskyKArgs& K, float ux, float uy) {
     return frame_to_world(mk3(K.sun_s[0], K.sun_s[1], K.sun_s[2]), mk3(K.sun_t[0], K.sun_t[1], K.sun_t[2]),
-                          mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), uniform_cone_dev(ux, uy, K.cos_cutoff));
+                          mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), uniform_cone_dev<FAST>(ux, uy, K.cos_cutoff));
 }
 
 // tgmm_pdf, sunsky.cpp:732-763, with the per-gaussian truncation volume hoisted
@@ -645,7 +675,7 @@ __device__ __forceinline__ void compute_pdfs(const SunskyKArgs& K, const TgmmLds
     active = active && (d.z >= 0.f) && (sin_theta != 0.f);
     sin_theta = fmaxf(sin_theta, kEpsilon);
     float phi = atan2f(d.y, d.x), theta = unit_angle_z(d);
-    *sky_pdf = tgmm_pdf<FAST>(K, T, phi, theta, active) / sin_theta;
+    *sky_pdf = fdiv<FAST>(tgmm_pdf<FAST>(K, T, phi, theta, active), sin_theta);
     float cosg = dot3(mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), d);
     *sun_pdf = (!check_sun || cosg >= K.cos_cutoff) ? K.sun_pdf : 0.f;
 }
@@ -714,12 +744,22 @@ __device__ __forceinline__ void sample_direction_body(
         const float sx = ux[i], sy = uy[i];
         const bool pick_sky = sx < K.w_sky;
         float3_ sd;
-        if (pick_sky) sd = sample_sky(K, S.tgmm, sx / K.w_sky, sy);
-        else sd = sample_sun(K, (sx - K.w_sky) / (1.f - K.w_sky), sy);
+#ifndef SS_PROBE_NO_SKY_SAMPLE   // probe builds (tools/Makefile) only: cost ablations
+        // sx / w and the reused sample stay correctly rounded even in FAST: the
+        // discrete-distribution reuse divides by the picked gaussian's pmf, so one
+        // ulp here moves sky directions by up to ~1e-5 (measured).
+        if (pick_sky) sd = sample_sky<FAST>(K, S.tgmm, sx / K.w_sky, sy);
+        else
+#endif
+            sd = sample_sun<FAST>(K, (sx - K.w_sky) / (1.f - K.w_sky), sy);
         act = act && (sd.z >= 0.f);
         float3_ d = to_world(K, sd);
         float skyp, sunp;
+#ifndef SS_PROBE_NO_PDF
         compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+#else
+        skyp = sd.z; sunp = K.sun_pdf;
+#endif
         float pd = lerpf_(sunp, skyp, K.w_sky);
         __builtin_nontemporal_store(d.x, dx + i);
         __builtin_nontemporal_store(d.y, dy + i);
@@ -736,15 +776,20 @@ __device__ __forceinline__ void sample_direction_body(
         float3_ wo = to_local(K, d);
         if constexpr (!SPEC) {
             float e[3];
+#ifndef SS_PROBE_NO_WEIGHT
             eval_rgb_local<FAST>(K, S.sun, wo, act, e);
+#else
+            e[0] = wo.x; e[1] = wo.y; e[2] = wo.z;
+#endif
+            const float inv_pd = fdiv<FAST>(1.f, pd);
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                float w = e[c] / pd;
+                float w = FAST ? e[c] * inv_pd : e[c] / pd;
                 __builtin_nontemporal_store(isfinite(w) ? w : 0.f, weight + (size_t)c * wstride + i);
             }
         } else {
             DirTerms t = dir_terms<FAST>(K, wo, act);
-            add_sun_terms(K, t);
+            add_sun_terms<FAST>(K, t);
             for (int k = 0; k < nlam; ++k) {
                 float e = eval_spec_one<FAST>(K, S.chans.c, S.sun, S.ld, t, lam[(size_t)k * lstride + i]);
                 float w = e / pd;
@@ -798,7 +843,7 @@ __device__ __forceinline__ void sample_wavelengths_body(const SunskyKArgs& K, co
             for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = 0.f;
         } else {
             DirTerms t = dir_terms<FAST>(K, wo, act);
-            add_sun_terms(K, t);
+            add_sun_terms<FAST>(K, t);
             float lam[4], w[4];
             sample_wavelengths_one<FAST>(K, S.c, D, K.sun_table, K.sun_ld, t, sample[i], lam, w);
             for (int k = 0; k < 4; ++k) {
@@ -829,8 +874,8 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
         const float sx = s3x[i], sy = s3y[i];
         const bool pick_sky = sx < K.w_sky;
         float3_ d;
-        if (pick_sky) d = sample_sky(K, S.tgmm, sx / K.w_sky, sy);
-        else d = sample_sun(K, (sx - K.w_sky) / (1.f - K.w_sky), sy);
+        if (pick_sky) d = sample_sky<FAST>(K, S.tgmm, sx / K.w_sky, sy);
+        else d = sample_sun<FAST>(K, (sx - K.w_sky) / (1.f - K.w_sky), sy);
         float3_ dw = to_world(K, mk3(-d.x, -d.y, -d.z));
         act = act && (d.z >= 0.f);
         float skyp, sunp;
@@ -847,7 +892,7 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
             for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = 0.f;
         } else {
             DirTerms t = dir_terms<FAST>(K, wo, act);
-            add_sun_terms(K, t);
+            add_sun_terms<FAST>(K, t);
             float lam[4];
             sample_wavelengths_one<FAST>(K, S.chans.c, S.sdist, S.sun, S.ld, t, wls[i], lam, w);
             for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = lam[k];

@@ -97,13 +97,13 @@ std::string code_object_path() {
 // The sampling kernels are instantiated per variant (RGB / spectral) so each
 // carries only its own tables and registers.
 enum KernelId {
-    K_EVAL_RGB_V4, K_EVAL_RGB_V1, K_EVAL_SPEC_BCAST_V2, K_EVAL_SPEC_BCAST_V1, K_EVAL_SPEC_NODES_V2,
+    K_EVAL_RGB_V4, K_EVAL_RGB_V1, K_EVAL_SPEC_BCAST_V4, K_EVAL_SPEC_BCAST_V1, K_EVAL_SPEC_NODES_V4,
     K_EVAL_SPEC_RAYS, K_SAMPLE_DIRECTION_RGB, K_SAMPLE_DIRECTION_SPEC, K_PDF_DIRECTION, K_SAMPLE_WAVELENGTHS_RGB,
     K_SAMPLE_WAVELENGTHS_SPEC, K_SAMPLE_RAY_RGB, K_SAMPLE_RAY_SPEC, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
-    "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v2", "sunsky_eval_spec_bcast_v1",
-    "sunsky_eval_spec_nodes_v2", "sunsky_eval_spec_rays", "sunsky_sample_direction_rgb",
+    "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
+    "sunsky_eval_spec_nodes_v4", "sunsky_eval_spec_rays", "sunsky_sample_direction_rgb",
     "sunsky_sample_direction_spec", "sunsky_pdf_direction", "sunsky_sample_wavelengths_rgb",
     "sunsky_sample_wavelengths_spec", "sunsky_sample_ray_rgb", "sunsky_sample_ray_spec"};
 
@@ -142,7 +142,7 @@ constexpr int kBlock = 256;
 // (cdna_hip_programming.md Guideline 11).  Workgroups per CU from the
 // tools/kbench.cpp sweep on MI355X (profiles/r01_v2_kbench_grid_sweep.log):
 // RGB eval 64 (60.4 us vs 64.9 us at 16 for 16M directions), spectral 64,
-// sampling 64 (profiles/r01_v5_kbench.log).
+// sampling 64 (profiles/r01_v5_kbench.log, r01_v7_tune.log).
 // SUNSKY_AMD_BLOCKS_PER_CU overrides every kernel class.
 int blocks_per_cu(KernelId k) {
     static const int env = [] {
@@ -152,7 +152,7 @@ int blocks_per_cu(KernelId k) {
     if (env) return env;
     switch (k) {
         case K_EVAL_RGB_V4: case K_EVAL_RGB_V1: return 64;
-        case K_EVAL_SPEC_BCAST_V2: case K_EVAL_SPEC_BCAST_V1: case K_EVAL_SPEC_NODES_V2: return 64;
+        case K_EVAL_SPEC_BCAST_V4: case K_EVAL_SPEC_BCAST_V1: case K_EVAL_SPEC_NODES_V4: return 64;
         case K_SAMPLE_DIRECTION_RGB: case K_SAMPLE_DIRECTION_SPEC: case K_PDF_DIRECTION: return 64;
         default: return 16;
     }
@@ -170,7 +170,6 @@ void launch(hipFunction_t f, unsigned grid, hipStream_t stream, void** args) {
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
-bool aligned8(const void* p) { return ((uintptr_t)p & 7u) == 0; }
 
 struct LambdaSet {   // mirrors the kernel-side struct
     int m;
@@ -471,21 +470,19 @@ int sunsky_eval_spectral_broadcast(const sunsky_emitter* e, sunsky_vec3_in w, co
         hipStream_t s = (hipStream_t)stream;
         SunskyKArgs K = e->kargs;
         float sign = -1.f;
-        // VEC = 2 (8-byte lanes): the spectral kernels are VALU-bound, so the
-        // smaller vector keeps more waves resident (DESIGN.md "Kernels").
-        bool vec = n >= 2 && aligned8(w.x) && aligned8(w.y) && aligned8(w.z) && aligned8(out) &&
-                   (ostride % 2) == 0 && (!active || ((uintptr_t)active & 1u) == 0);
-        size_t n2 = vec ? (n & ~(size_t)1) : 0;
-        if (n2) {
+        bool vec = n >= 4 && aligned16(w.x) && aligned16(w.y) && aligned16(w.z) && aligned16(out) &&
+                   (ostride % 4) == 0 && (!active || ((uintptr_t)active & 3u) == 0);
+        size_t n4 = vec ? (n & ~(size_t)3) : 0;
+        if (n4) {
             const float *x = w.x, *y = w.y, *z = w.z;
-            void* args[] = {&K, &L, &x, &y, &z, &active, &n2, &out, &ostride, &sign};
-            launch(e->fn(nodes ? K_EVAL_SPEC_NODES_V2 : K_EVAL_SPEC_BCAST_V2), grid_for(e->mod, K_EVAL_SPEC_BCAST_V2, n2 / 2), s, args);
+            void* args[] = {&K, &L, &x, &y, &z, &active, &n4, &out, &ostride, &sign};
+            launch(e->fn(nodes ? K_EVAL_SPEC_NODES_V4 : K_EVAL_SPEC_BCAST_V4), grid_for(e->mod, K_EVAL_SPEC_BCAST_V4, n4 / 4), s, args);
         }
-        if (n2 < n) {
-            const float *x = w.x + n2, *y = w.y + n2, *z = w.z + n2;
-            const uint8_t* a = active ? active + n2 : nullptr;
-            float* o = out + n2;
-            size_t rem = n - n2;
+        if (n4 < n) {
+            const float *x = w.x + n4, *y = w.y + n4, *z = w.z + n4;
+            const uint8_t* a = active ? active + n4 : nullptr;
+            float* o = out + n4;
+            size_t rem = n - n4;
             void* args[] = {&K, &L, &x, &y, &z, &a, &rem, &o, &ostride, &sign};
             launch(e->fn(K_EVAL_SPEC_BCAST_V1), grid_for(e->mod, K_EVAL_SPEC_BCAST_V1, rem), s, args);
         }

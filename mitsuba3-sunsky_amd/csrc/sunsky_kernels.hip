@@ -5,8 +5,8 @@
 //
 // Design (DESIGN.md "Kernels"; numbers from tools/kbench.cpp on MI355X):
 //  * SoA fp32 rays in HBM (x[], y[], z[] planes) and SoA outputs (one plane per
-//    channel / wavelength); VEC consecutive directions per lane so global
-//    accesses are 16 B (RGB, VEC = 4) or 8 B (spectral, VEC = 2) per lane.
+//    channel / wavelength); VEC = 4 consecutive directions per lane so global
+//    accesses are 16 B per lane (VEC = 1 kernels take tails / unaligned rays).
 //    Plain loads + non-temporal stores measured fastest (RGB eval 68 us for
 //    16M directions = 5.9 TB/s);
 //  * every per-emitter constant arrives in the by-value SunskyKArgs kernarg
@@ -932,9 +932,9 @@ SS_EVAL_RGB(sunsky_eval_rgb_v1_ref, 1, false)
         size_t n, float* out, size_t ostride, float sign) {                                                    \
         eval_spec_bcast_body<VEC, FAST>(K, L, wx, wy, wz, active, n, out, ostride, sign);                      \
     }
-SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v2_fast, 2, true)
+SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v4_fast, 4, true)
 SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v1_fast, 1, true)
-SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v2_ref, 2, false)
+SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v4_ref, 4, false)
 SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v1_ref, 1, false)
 
 #define SS_EVAL_SPEC_NODES(NAME, VEC, FAST)                                                                   \
@@ -944,8 +944,8 @@ SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v1_ref, 1, false)
         (void)L;                                                                                               \
         eval_spec_nodes_body<VEC, FAST>(K, wx, wy, wz, active, n, out, ostride, sign);                         \
     }
-SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v2_fast, 2, true)
-SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v2_ref, 2, false)
+SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v4_fast, 4, true)
+SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v4_ref, 4, false)
 
 #define SS_EVAL_SPEC_RAYS(NAME, FAST)                                                                         \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \

@@ -15,8 +15,8 @@ cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 120 rocprofv3 -L > $O/counters_list.txt 2>&1 && \
 pmc() { local nm=$1 mode=$2 n=$3 k=$4 bp=$5; shift 5
   timeout -k 10 180 rocprofv3 --pmc "$@" -d $O/$nm -o $nm --output-format csv -- $KB $H $mode $n 3 $bp $k > $O/$nm.log 2>&1; } && \
-pmc spec_sq1 spec 16777216 sunsky_eval_spec_nodes_v2_fast 32 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES && \
-pmc spec_sq2 spec 16777216 sunsky_eval_spec_nodes_v2_fast 32 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE && \
+pmc spec_sq1 spec 16777216 sunsky_eval_spec_nodes_v4_fast 32 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES && \
+pmc spec_sq2 spec 16777216 sunsky_eval_spec_nodes_v4_fast 32 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE && \
 pmc sample_sq1 sample 67108864 sunsky_sample_direction_rgb_fast 16 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES && \
 pmc sample_sq2 sample 67108864 sunsky_sample_direction_rgb_fast 16 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE && \
 pmc pdf_sq1 pdf 67108864 sunsky_pdf_direction_fast 16 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES && \

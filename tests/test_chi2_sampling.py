@@ -101,3 +101,15 @@ def test07_spectral_and_scalar_variants(semantics):
     ok = t.run()
     print(t.messages)
     assert ok, t.messages
+
+
+def test_two_sample_chi2_self_check():
+    from chi2 import two_sample_chi2
+    rng = np.random.default_rng(4)
+    p = rng.dirichlet(np.ones(400))
+    a = rng.multinomial(2_000_000, p)
+    b = rng.multinomial(300_000, p)
+    assert two_sample_chi2(a, b)[2] > 0.01
+    q = p * (1 + 0.05 * np.sin(np.arange(400)))
+    c = rng.multinomial(300_000, q / q.sum())
+    assert two_sample_chi2(a, c)[2] < 1e-6

@@ -1,0 +1,119 @@
+"""Counterparts of the reference's sunsky-testing checks:
+sun_rad_test.py:37-93 (plugin sun vs the Hosek-Wilkie solar radiance sweep),
+sampling_test.py:20-58 (no sky sample below the horizon at 2.5e8 samples + chi^2
+on the full sphere) and sampling_test.py:61-82 (the sky/sun sampling weight map)."""
+import itertools
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+import sunsky_amd as ss
+from chi2 import ChiSquareTest, SphericalDomain, emitter_adapter, two_sample_chi2
+from helpers import angles_dict
+
+PHI = math.pi / 5
+SUN_HALF_APP = math.radians(0.5358 / 2.0)
+
+
+def _range(nb, a, b):
+    return [(i / (nb - 1)) * (b - a) + a for i in range(nb)]
+
+
+def _sampling_dict(t, a, eta, sky_scale=1.0, sun_scale=0.0, phi=-4 * math.pi / 5):
+    """get_dict of sampling_test.py:7-19."""
+    st, ct = math.sin(math.pi / 2 - eta), math.cos(math.pi / 2 - eta)
+    return {"type": "sunsky", "sun_direction": [math.cos(phi) * st, math.sin(phi) * st, ct],
+            "sky_scale": sky_scale, "sun_scale": sun_scale, "turbidity": t, "albedo": a}
+
+
+@pytest.mark.gpu
+def test_sun_radiance_sweep_vs_hosek():
+    """sun_rad_test.py:62-93: 5 elevations x 7 turbidities x 4 in-disc gammas x 20 wavelengths.
+    The reference prints the worst mean relative error; we require <= 1e-4 (the fp32
+    oracle's own worst is 2.5e-5) and the reference tests' 1e-2 bar a fortiori."""
+    eps = 1e-3
+    step = (720 - 320) / 20
+    wavs = np.array([320 + step / 2 + i * step for i in range(20)], np.float32)
+    wl = torch.from_numpy(wavs).cuda()
+    worst = 0.0
+    for eta, turb, gamma in itertools.product(_range(5, eps, math.pi / 2 - eps), _range(7, 1, 10),
+                                              _range(4, 0, SUN_HALF_APP - eps)):
+        theta_sun = math.pi / 2 - eta - gamma
+        if theta_sun < 0:
+            theta_sun = math.pi / 2 - eta + gamma
+        d = angles_dict(turb, PHI, theta_sun, 0.0, 0.0, 1.0)
+        em = ss.load_dict(d, variant="spectral")
+        st, ct = math.sin(math.pi / 2 - eta), math.cos(math.pi / 2 - eta)
+        wi = -np.array([[math.cos(PHI) * st, math.sin(PHI) * st, ct]] * 20, np.float32)
+        res = em.eval(ss.SurfaceInteraction3f(wi=torch.from_numpy(wi.T.copy()).cuda(), wavelengths=wl))
+        res = res.cpu().numpy()[0]
+        o = O.Oracle(d, "spectral", "jit", "f64")
+        ref = np.array([o.hw_sun_radiance(turb, float(w), eta, gamma) for w in wavs])
+        err = float(np.mean(np.abs(res - ref) / (ref + 1e-6)))
+        worst = max(worst, err)
+        assert err <= 1e-4, (eta, turb, gamma, err)
+    print(f"sun sweep worst mean-rel {worst:.3e}")
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_sky_samples_stay_above_horizon_and_match_reference_sampler():
+    """sampling_test.py:20-58: T = 6, albedo 0.5, elevation 50.2 deg, sky only.
+
+    * 2.5e8 samples, none below the horizon (sunsky.cpp:686 clamps theta to pi/2 - eps).
+    * The script's chi^2 against pdf_direction at 2.5e8 samples is not a usable bar: on
+      the uncropped sphere the 1/sin(theta) zenith singularity breaks the trapezoid cell
+      integrals (PDF sum 1.0195), and even with the zenith cap cut out the reference
+      algorithm itself is rejected at that count -- the oracle's own sampler scores
+      chi^2 = 13765 / 11663 dof (tools: tests/chi2.py on the CPU oracle), the GPU 13265.
+      The reference's bar (test06, 1e8 samples) is run in test_chi2_sampling.py.
+    * Here instead: the GPU sampler's histogram (1e8 samples) against the reference
+      algorithm's (the fp32 oracle, 2e7 samples) -- a two-sample chi^2 homogeneity test
+      on the script's 216-row grid, which needs no pdf integration."""
+    d = _sampling_dict(6.0, 0.5, math.radians(50.2))
+    em = ss.load_dict(d)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(123)
+    below, total = 0, 0
+    for _ in range(10):
+        u = torch.rand((2, 25_000_000), generator=g, device="cuda")
+        ds, _ = em.sample_direction(ss.Interaction3f(), u)
+        below += int((ds.d[2] < 0).sum())
+        total += u.shape[1]
+    assert total == 250_000_000 and below == 0
+
+    dom = SphericalDomain(0.00775)
+    sample, pdf = emitter_adapter(em)
+    t_gpu = ChiSquareTest(dom, sample, pdf, sample_count=100_000_000, res=216, ires=4, seed=5)
+    t_gpu.tabulate_histogram()
+    o = O.Oracle(d, "rgb", "jit", "f32")
+    o.override_w_sky(em.sky_sampling_w)
+
+    def sample_oracle(u):
+        r = o.sample_direction(np.ascontiguousarray(u.numpy().T))
+        return torch.from_numpy(np.ascontiguousarray(r["d"].T))
+
+    t_ref = ChiSquareTest(dom, sample_oracle, None, sample_count=20_000_000, res=216, ires=4, seed=9,
+                          device="cpu", chunk=1 << 22)
+    t_ref.tabulate_histogram()
+    chsq, dof, p = two_sample_chi2(t_gpu.histogram, t_ref.histogram)
+    print(f"two-sample chi^2 GPU vs reference sampler: {chsq:.1f} / {dof} dof, p = {p:.3f}")
+    assert p > 0.01, (chsq, dof, p)
+
+
+def test_sky_sun_sampling_weight_map():
+    """sampling_test.py:61-82 plots m_sky_sampling_w over turbidity x elevation; the staged
+    weight must match the oracle's quadrature everywhere on that map (host staging, CPU)."""
+    worst = 0.0
+    for t in np.linspace(1, 10, 7):
+        for eta in np.radians(np.linspace(0, 90, 7)):
+            d = _sampling_dict(float(t), 0.5, float(eta), 1.0, 1.0)
+            em = ss.SunskyEmitter(d, "rgb", device="host")
+            w = em.sky_sampling_w
+            ref = O.Oracle(d, "rgb", "jit", "f32").info()["w_sky"]
+            assert 0.0 <= w <= 1.0
+            worst = max(worst, abs(w - ref))
+    assert worst < 2e-5, worst

@@ -120,6 +120,16 @@ int main(int argc, char** argv) {
             CK(hipMemcpy(dd + 2 * n, hz.data(), n * 4, hipMemcpyHostToDevice));
         }
     }
+    // KB_COLD=k: rotate over k distinct input batches so inputs cannot stay in the
+    // 256 MiB Infinity Cache (rgb / spec modes).
+    const int cold = std::getenv("KB_COLD") ? std::max(1, std::atoi(std::getenv("KB_COLD"))) : 1;
+    std::vector<float*> cx(cold, wx), cy(cold, wy), cz(cold, wz);
+    for (int c = 1; c < cold; ++c) {
+        CK(hipMalloc(&cx[c], n * 4)); CK(hipMalloc(&cy[c], n * 4)); CK(hipMalloc(&cz[c], n * 4));
+        CK(hipMemcpy(cx[c], wx, n * 4, hipMemcpyDeviceToDevice));
+        CK(hipMemcpy(cy[c], wy, n * 4, hipMemcpyDeviceToDevice));
+        CK(hipMemcpy(cz[c], wz, n * 4, hipMemcpyDeviceToDevice));
+    }
     const float* nullf = nullptr;
     float* nullo = nullptr;
     size_t zero = 0;
@@ -131,6 +141,8 @@ int main(int argc, char** argv) {
         CK(hipModuleGetFunction(&f, mod, argv[a]));
         std::string name = argv[a];
         int vec = name.find("_v4") != std::string::npos ? 4 : (name.find("_v2") != std::string::npos ? 2 : 1);
+        if (name.find("_u2") != std::string::npos) vec = 8;
+        if (name.find("_u4") != std::string::npos) vec = 16;
         for (int mult : bpcu) {
             size_t items = n / vec;
             unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((items + 255) / 256, (size_t)cu * mult));
@@ -144,8 +156,11 @@ int main(int argc, char** argv) {
             hipEvent_t e0, e1;
             CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
             CK(hipEventRecord(e0, nullptr));
-            for (int it = 0; it < iters; ++it)
+            for (int it = 0; it < iters; ++it) {
+                if (cold > 1) { wx = cx[it % cold]; wy = cy[it % cold]; wz = cz[it % cold]; }
                 CK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
+            }
+            wx = cx[0]; wy = cy[0]; wz = cz[0];
             CK(hipEventRecord(e1, nullptr));
             CK(hipEventSynchronize(e1));
             float ms = 0;

@@ -185,6 +185,23 @@ int sunsky_sample_wavelengths(const sunsky_emitter *e, sunsky_vec3_in wi, const 
 /* sample_position(), sunsky.cpp:483-495: NotImplementedError in the reference */
 int sunsky_sample_position(const sunsky_emitter *e);
 
+/* ------------------------------------------------ forward-mode derivatives */
+typedef enum sunsky_param {         /* Differentiable traverse() parameters, sunsky.cpp:220-240 */
+    SUNSKY_PARAM_TURBIDITY = 0,     /* tangent: 1 value                               */
+    SUNSKY_PARAM_ALBEDO = 1,        /* tangent: 1 value or one per channel (3 / 11)   */
+    SUNSKY_PARAM_SUN_DIRECTION = 2  /* tangent: 3 values, world space (m_sun_dir)     */
+} sunsky_param;
+/* eval(si) and its forward-mode derivative along `tangent` of `param`: what
+ * dr::enable_grad(param); dr::set_grad(param, tangent); dr::forward_from(param);
+ * dr::grad(eval(si)) computes in the reference's AD variants (exercised by
+ * sunsky-testing/traversal_test.py:94-145).  Layout as sunsky_eval; d_out has the
+ * planes of out.  The tangent of the staged tables is computed on the host and
+ * uploaded before the launch (host-synchronous), the rays are processed on `stream`. */
+int sunsky_eval_jvp(const sunsky_emitter *e, int param, const float *tangent, int tangent_count,
+                    sunsky_vec3_in wi, const float *wavelengths, int n_wavelengths, size_t wl_stride,
+                    const uint8_t *active, size_t n, float *out, float *d_out, size_t out_stride,
+                    void *stream);
+
 /* --------------------------------------------- dataset I/O (sunsky_v.cpp:16-18) */
 /* array_from_file_d / _f (sunsky.h:516-561): file_dtype 0 = infer, 1 = fp32, 2 = fp64.
  * Writes min(count, capacity) fp64 values; shape gets up to 16 dims. */

@@ -110,6 +110,7 @@ const char* kKernelNames[K_COUNT] = {
 struct DeviceModule {
     hipModule_t module = nullptr;
     hipFunction_t fn[2][K_COUNT] = {};   // [precision][kernel]
+    hipFunction_t jvp_rgb = nullptr, jvp_spec = nullptr;   // eval_jvp (reference operation order)
     int cu_count = 256;
 };
 
@@ -129,6 +130,8 @@ DeviceModule* module_for_device(int dev) {
             std::string name = std::string(kKernelNames[k]) + (p == SUNSKY_PRECISION_FAST ? "_fast" : "_ref");
             hip_check(hipModuleGetFunction(&m->fn[p][k], m->module, name.c_str()), name.c_str());
         }
+    hip_check(hipModuleGetFunction(&m->jvp_rgb, m->module, "sunsky_eval_jvp_rgb"), "sunsky_eval_jvp_rgb");
+    hip_check(hipModuleGetFunction(&m->jvp_spec, m->module, "sunsky_eval_jvp_spec"), "sunsky_eval_jvp_spec");
     hip_check(hipDeviceGetAttribute(&m->cu_count, hipDeviceAttributeMultiprocessorCount, dev),
               "hipDeviceGetAttribute");
     DeviceModule* raw = m.release();
@@ -192,6 +195,7 @@ struct sunsky_emitter {
     int precision = SUNSKY_PRECISION_FAST;
     float* d_sun_table = nullptr;
     float* d_sun_ld = nullptr;
+    mutable float* d_jvp = nullptr;   // eval_jvp tangent tables (layout: sunsky_kernels.hip)
 
     void upload() {
         int cur = 0;
@@ -220,6 +224,7 @@ struct sunsky_emitter {
     ~sunsky_emitter() {
         if (d_sun_table) (void)hipFree(d_sun_table);
         if (d_sun_ld) (void)hipFree(d_sun_ld);
+        if (d_jvp) (void)hipFree(d_jvp);
     }
 };
 
@@ -557,6 +562,46 @@ int sunsky_sample_wavelengths(const sunsky_emitter* e, sunsky_vec3_in w, const f
         void* args[] = {&K, (void*)&w.x, (void*)&w.y, (void*)&w.z, &sample, &active, &n, &lam, &lstride, &weight, &wstride};
         const KernelId k = e->kargs.variant == kSpectral ? K_SAMPLE_WAVELENGTHS_SPEC : K_SAMPLE_WAVELENGTHS_RGB;
         launch(e->fn(k), grid_for(e->mod, k, n), (hipStream_t)stream, args);
+    });
+}
+
+int sunsky_eval_jvp(const sunsky_emitter* e, int param, const float* tangent, int tangent_count, sunsky_vec3_in wi,
+                    const float* lam, int nlam, size_t lstride, const uint8_t* active, size_t n, float* out,
+                    float* d_out, size_t ostride, void* stream) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (!tangent) return fail(SUNSKY_ERROR_INVALID_VALUE, "null tangent");
+    const bool spec = e->kargs.variant == kSpectral;
+    if (spec && (!lam || nlam < 1 || nlam > kMaxLambdaPerRay))
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "spectral eval needs 1..16 wavelength planes");
+    const size_t nout = spec ? (size_t)nlam : 3;
+    if (n && (!wi.x || !wi.y || !wi.z || !out || !d_out))
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "null ray / output pointer");
+    if (n && nout > 1 && ostride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "out_stride < n");
+    if (n && spec && nlam > 1 && lstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "wl_stride < n");
+    return guarded([&] {
+        EvalTangent tan = e->model->eval_tangent(param, tangent, tangent_count);   // validates param / count
+        if (n == 0) return;
+        if (!e->mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
+        std::vector<float> buf(128 + kSunRgbTableSize, 0.f);
+        std::memcpy(buf.data(), tan.dsky.data(), sizeof(float) * tan.dsky.size());
+        std::memcpy(buf.data() + kNbWavelengths * 10, tan.dsun_local, 3 * sizeof(float));
+        std::memcpy(buf.data() + 128, tan.dsun.data(), sizeof(float) * tan.dsun.size());
+        if (!e->d_jvp) hip_check(hipMalloc(&e->d_jvp, sizeof(float) * buf.size()), "hipMalloc");
+        // a previous eval_jvp of this emitter may still read the buffer
+        hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        hip_check(hipMemcpy(e->d_jvp, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice), "hipMemcpy");
+        SunskyKArgs K = e->kargs;
+        const float* jvp = e->d_jvp;
+        const float *x = wi.x, *y = wi.y, *z = wi.z;
+        float sign = -1.f;
+        if (!spec) {
+            void* args[] = {&K, &jvp, &x, &y, &z, &active, &n, &out, &d_out, &ostride, &sign};
+            launch(e->mod->jvp_rgb, grid_for(e->mod, K_EVAL_RGB_V1, n), (hipStream_t)stream, args);
+        } else {
+            int nl = nlam;
+            void* args[] = {&K, &jvp, &x, &y, &z, &lam, &lstride, &nl, &active, &n, &out, &d_out, &ostride, &sign};
+            launch(e->mod->jvp_spec, grid_for(e->mod, K_EVAL_SPEC_RAYS, n), (hipStream_t)stream, args);
+        }
     });
 }
 

@@ -913,6 +913,185 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
 }
 
 // ======================================================================
+// eval_jvp: forward-mode derivative of eval() with respect to one
+// differentiable parameter (turbidity / albedo / sun_direction, sunsky.cpp:
+// 220-240) -- what dr::forward_from(param) + dr::grad(eval(si)) give in the
+// reference.  The host stages the tangent of the tables (SunskyModel::
+// eval_tangent); this kernel carries value and tangent through the reference
+// operation order of eval (sunsky.cpp:303-352, 538-614, 631-650).
+// jvp buffer: [0, 110) d{A..I, rad} x 11 channels, [110, 113) d local sun
+// direction, [128, 128 + sun table size) d sun radiance table.
+// ======================================================================
+constexpr int kJvpSunOffset = 128;
+
+struct JvpLds { float dsky[kNbWavelengths * 10]; float dsun_local[4]; };
+
+// d unit_angle(a, b) along da (sunsky.cpp:311): gamma = 2 asin(h) or pi - 2 asin(h),
+// h = |b -/+ a| / 2.
+__device__ __forceinline__ float unit_angle_tangent(float3_ a, float3_ b, float3_ da) {
+    float d = dot3(a, b);
+    float3_ v = mk3(b.x - mulsignf_(a.x, d), b.y - mulsignf_(a.y, d), b.z - mulsignf_(a.z, d));
+    float3_ dv = mk3(-mulsignf_(da.x, d), -mulsignf_(da.y, d), -mulsignf_(da.z, d));
+    float h = 0.5f * sqrtf(dot3(v, v));
+    if (!(h > 0.f)) return 0.f;
+    float dtemp = 2.f * (dot3(v, dv) / (4.f * h)) / sqrtf(1.f - h * h);
+    return d >= 0.f ? dtemp : -dtemp;
+}
+
+// render_sky and its tangent (dk = d{A..I, rad}), unscaled
+__device__ __forceinline__ void sky_jvp(const SkyChannel& k, const float* dk, const DirTerms& t, float dgamma,
+                                        float sg, float* L, float* dL) {
+    const float cg = t.cg, dcg = -sg * dgamma;
+    const float e1 = expf(k.B * t.r);
+    const float c1 = 1.f + k.A * e1;
+    const float dc1 = dk[0] * e1 + k.A * e1 * t.r * dk[1];
+    const float e2 = expf(k.E * t.gamma);
+    const float b = 1.f + k.I * k.I - 2.f * k.I * cg;
+    const float pb = powf(b, 1.5f);
+    const float chi = t.u / pb;
+    const float db = 2.f * k.I * dk[8] - 2.f * dk[8] * cg - 2.f * k.I * dcg;
+    const float dchi = 2.f * cg * dcg / pb - 1.5f * chi * db / b;
+    const float c2 = k.C + k.D * e2 + k.F * t.cg2 + k.G * chi + k.H * t.sq;
+    const float dc2 = dk[2] + dk[3] * e2 + k.D * e2 * (dk[4] * t.gamma + k.E * dgamma) + dk[5] * t.cg2 +
+                      k.F * 2.f * cg * dcg + dk[6] * chi + k.G * dchi + dk[7] * t.sq;
+    *L = c1 * c2 * k.rad;
+    *dL = (dc1 * c2 + c1 * dc2) * k.rad + c1 * c2 * dk[9];
+}
+
+// cos_psi (sunsky.h:385-392) and its tangent
+__device__ __forceinline__ void cos_psi_jvp(const SunskyKArgs& K, const DirTerms& t, float sg, float dgamma,
+                                            float* cp, float* dcp) {
+    *cp = cos_psi(t.gamma, K.inv_sin2_half_ap);
+    *dcp = *cp > 0.f ? -K.inv_sin2_half_ap * sg * t.cg * dgamma / *cp : 0.f;
+}
+
+// Shared per-direction setup: reference-order DirTerms (cg = cos(gamma)), sin(gamma), d gamma.
+__device__ __forceinline__ DirTerms jvp_dir(const SunskyKArgs& K, const JvpLds& J, float3_ wo, bool m, float* sg,
+                                            float* dgamma) {
+    DirTerms t = dir_terms<false>(K, wo, m);
+    *sg = sinf(t.gamma);
+    *dgamma = unit_angle_tangent(mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), wo,
+                                 mk3(J.dsun_local[0], J.dsun_local[1], J.dsun_local[2]));
+    return t;
+}
+
+__device__ __forceinline__ void stage_jvp(const float* jvp, JvpLds* J, int nch) {
+    for (int i = threadIdx.x; i < nch * 10; i += blockDim.x) J->dsky[i] = jvp[i];
+    if (threadIdx.x < 3) J->dsun_local[threadIdx.x] = jvp[kNbWavelengths * 10 + threadIdx.x];
+    __syncthreads();
+}
+
+__device__ __forceinline__ void eval_jvp_rgb_body(const SunskyKArgs& K, const float* __restrict__ jvp,
+                                                  const float* __restrict__ wx, const float* __restrict__ wy,
+                                                  const float* __restrict__ wz, const uint8_t* __restrict__ active,
+                                                  size_t n, float* __restrict__ out, float* __restrict__ dout,
+                                                  size_t ostride, float sign) {
+    __shared__ JvpLds J;
+    stage_jvp(jvp, &J, 3);
+    const float* dsun_tab = jvp + kJvpSunOffset;
+    const float cie = (float)kCieYNormalization, conv = (float)kSpecToRgbSunConv;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        bool m = active ? active[i] != 0 : true;
+        float3_ wo = to_local(K, mk3(sign * wx[i], sign * wy[i], sign * wz[i]));
+        float sg, dg;
+        DirTerms t = jvp_dir(K, J, wo, m, &sg, &dg);
+        float v[3], dv[3];
+#pragma unroll 1
+        for (int c = 0; c < 3; ++c) {
+            sky_jvp(K.sky[c], J.dsky + c * 10, t, dg, sg, &v[c], &dv[c]);
+            v[c] *= K.sky_scale;
+            dv[c] *= K.sky_scale;
+        }
+        if (t.hit_sun) {
+            float xs, cp, dcp;
+            int pos = sun_segment(t.cos_theta, &xs);
+            cos_psi_jvp(K, t, sg, dg, &cp, &dcp);
+            const float sc = K.sun_scale * K.area_ratio * conv;
+#pragma unroll 1
+            for (int c = 0; c < 3; ++c) {
+                const float* S = K.sun_table + pos * (3 * kNbSunCtrlPts * kNbSunLdParams) + c * (kNbSunCtrlPts * kNbSunLdParams);
+                const float* dS = dsun_tab + pos * (3 * kNbSunCtrlPts * kNbSunLdParams) + c * (kNbSunCtrlPts * kNbSunLdParams);
+                float sv = 0.f, dsv = 0.f;
+                for (int k = 0; k < kNbSunCtrlPts; ++k)
+                    for (int j = 0; j < kNbSunLdParams; ++j) {
+                        const float xk = powif_(xs, k), cj = powif_(cp, j);
+                        sv += xk * cj * S[k * kNbSunLdParams + j];
+                        dsv += xk * cj * dS[k * kNbSunLdParams + j];
+                        if (j > 0) dsv += xk * (float)j * powif_(cp, j - 1) * S[k * kNbSunLdParams + j] * dcp;
+                    }
+                v[c] += sc * sv;
+                dv[c] += sc * dsv;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            out[(size_t)c * ostride + i] = t.active ? v[c] * cie : 0.f;
+            dout[(size_t)c * ostride + i] = t.active ? dv[c] * cie : 0.f;
+        }
+    }
+}
+
+__device__ __forceinline__ void eval_jvp_spec_body(const SunskyKArgs& K, const float* __restrict__ jvp,
+                                                   const float* __restrict__ wx, const float* __restrict__ wy,
+                                                   const float* __restrict__ wz, const float* __restrict__ lam,
+                                                   size_t lstride, int nlam, const uint8_t* __restrict__ active,
+                                                   size_t n, float* __restrict__ out, float* __restrict__ dout,
+                                                   size_t ostride, float sign) {
+    __shared__ JvpLds J;
+    stage_jvp(jvp, &J, kNbWavelengths);
+    const float* dsun_tab = jvp + kJvpSunOffset;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        bool m = active ? active[i] != 0 : true;
+        float3_ wo = to_local(K, mk3(sign * wx[i], sign * wy[i], sign * wz[i]));
+        float sg, dg;
+        DirTerms t = jvp_dir(K, J, wo, m, &sg, &dg);
+        float xs = 0.f, cp = 0.f, dcp = 0.f;
+        int pos = 0;
+        if (t.hit_sun) {
+            pos = sun_segment(t.cos_theta, &xs);
+            cos_psi_jvp(K, t, sg, dg, &cp, &dcp);
+        }
+        for (int q = 0; q < nlam; ++q) {
+            const float lambda = lam[(size_t)q * lstride + i];
+            float nw = (lambda - kWavelength0) / kWavelengthStep;
+            bool valid = (0.f <= nw) && (nw <= (float)(kNbWavelengths - 1));
+            float res = 0.f, dres = 0.f;
+            if (t.active && valid) {
+                int lo = (int)floorf(nw), hi = lo + 1;
+                float f = nw - (float)lo;
+                float la, dla, lb = 0.f, dlb = 0.f;
+                sky_jvp(K.sky[lo], J.dsky + lo * 10, t, dg, sg, &la, &dla);
+                if (hi < kNbWavelengths) sky_jvp(K.sky[hi], J.dsky + hi * 10, t, dg, sg, &lb, &dlb);
+                res = K.sky_scale * (f != 0.f ? lerpf_(la, lb, f) : la);
+                dres = K.sky_scale * (f != 0.f ? lerpf_(dla, dlb, f) : dla);
+                if (t.hit_sun) {
+                    float sa = render_sun_spec(K.sun_table, pos, lo, xs), dsa = render_sun_spec(dsun_tab, pos, lo, xs);
+                    float sun = sa, dsun = dsa;
+                    if (f != 0.f) {
+                        float sb = hi < kNbWavelengths ? render_sun_spec(K.sun_table, pos, hi, xs) : 0.f;
+                        float dsb = hi < kNbWavelengths ? render_sun_spec(dsun_tab, pos, hi, xs) : 0.f;
+                        sun = lerpf_(sa, sb, f);
+                        dsun = lerpf_(dsa, dsb, f);
+                    }
+                    float ld = sun_limb_darkening(K.sun_ld, lo, hi, f, cp), dld = 0.f;
+                    for (int j = 1; j < kNbSunLdParams; ++j) {
+                        float a = K.sun_ld[lo * kNbSunLdParams + j], coef = a;
+                        if (f != 0.f) coef = lerpf_(a, hi < kNbWavelengths ? K.sun_ld[hi * kNbSunLdParams + j] : 0.f, f);
+                        dld += (float)j * powif_(cp, j - 1) * coef * dcp;
+                    }
+                    res += K.sun_scale * sun * ld * K.area_ratio;
+                    dres += K.sun_scale * K.area_ratio * (dsun * ld + sun * dld);
+                }
+            }
+            out[(size_t)q * ostride + i] = res;
+            dout[(size_t)q * ostride + i] = dres;
+        }
+    }
+}
+
+// ======================================================================
 // extern "C" entry points (hipModuleGetFunction names)
 // ======================================================================
 #define SS_EVAL_RGB(NAME, VEC, FAST)                                                                          \
@@ -1001,3 +1180,14 @@ SS_SAMPLE_RAY(sunsky_sample_ray_rgb_fast, true, false)
 SS_SAMPLE_RAY(sunsky_sample_ray_rgb_ref, false, false)
 SS_SAMPLE_RAY(sunsky_sample_ray_spec_fast, true, true)
 SS_SAMPLE_RAY(sunsky_sample_ray_spec_ref, false, true)
+
+extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_jvp_rgb(
+    SunskyKArgs K, const float* jvp, const float* wx, const float* wy, const float* wz, const uint8_t* active,
+    size_t n, float* out, float* dout, size_t ostride, float sign) {
+    eval_jvp_rgb_body(K, jvp, wx, wy, wz, active, n, out, dout, ostride, sign);
+}
+extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_jvp_spec(
+    SunskyKArgs K, const float* jvp, const float* wx, const float* wy, const float* wz, const float* lam,
+    size_t lstride, int nlam, const uint8_t* active, size_t n, float* out, float* dout, size_t ostride, float sign) {
+    eval_jvp_spec_body(K, jvp, wx, wy, wz, lam, lstride, nlam, active, n, out, dout, ostride, sign);
+}

@@ -20,6 +20,16 @@ void compute_sun_coordinates(const DateTime& t, const Location& l, float out[3])
 // quad::gauss_legendre, quad.h:27-86 (fp64 nodes/weights)
 void gauss_legendre(int n, std::vector<double>* nodes, std::vector<double>* weights);
 
+// Forward-mode tangent of the staged eval tables with respect to one
+// differentiable parameter of traverse() (sunsky.cpp:220-240): what Dr.Jit's
+// dr::forward_from(param) propagates into the staging before eval runs.
+enum JvpParam { kJvpTurbidity = 0, kJvpAlbedo = 1, kJvpSunDirection = 2 };
+struct EvalTangent {
+    std::vector<float> dsky;   // nch x 10: d{A, B, C, D, E, F, G, H, I, rad} per channel
+    std::vector<float> dsun;   // d sun radiance table (turbidity), else all zero
+    float dsun_local[3] = {0, 0, 0};   // d local sun direction (sun_direction)
+};
+
 class SunskyModel {
 public:
     // SunskyEmitter(const Properties&), sunsky.cpp:162-218.  Throws std::invalid_argument /
@@ -48,6 +58,9 @@ public:
     const std::vector<float>& sky_radiance() const { return sky_rad_; }
     const float* gaussians_raw() const { return gauss_raw_; }
     std::string to_string() const;
+    // Tangent of the eval tables for param (JvpParam) along `tangent`
+    // (turbidity: 1 value; albedo: 1 or nch; sun_direction: 3, world space).
+    EvalTangent eval_tangent(int param, const float* tangent, int count) const;
     std::vector<std::string> warnings;
 
 private:

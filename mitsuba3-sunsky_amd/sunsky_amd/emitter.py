@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from . import _capi
-from ._capi import Vec3In, Vec3Out, check, lib
+from ._capi import PARAMS, Vec3In, Vec3Out, check, lib
 from .records import DirectionSample3f, Ray3f, ScalarBoundingBox3f
 
 _FLOAT_KEYS = ("turbidity", "sky_scale", "sun_scale", "sun_aperture", "latitude", "longitude",
@@ -291,6 +291,27 @@ class SunskyEmitter:
             out = torch.empty((3, n), dtype=torch.float32, device=self.device)
             check(fn(self._h, vin, None, 0, 0, _ptr(m), n, _ptr(out), n, self._stream()))
         return out
+
+    def eval_jvp(self, si, param, tangent, active=None):
+        """Forward-mode derivative of eval(si) along `tangent` of a differentiable
+        parameter ("turbidity", "albedo", "sun_direction"; sunsky.cpp:220-240) -- the
+        reference's dr.forward_from(param) / dr.grad(eval(si)).  -> (value, d_value)."""
+        wi, vin = self._vec_in(si.wi)
+        n = wi.shape[1]
+        m = self._mask(active, n)
+        tan = [float(x) for x in np.atleast_1d(np.asarray(tangent, dtype=np.float32))]
+        if param not in PARAMS:
+            raise ValueError(f"'{param}' is not a differentiable parameter ({', '.join(PARAMS)})")
+        wl, k = None, 3
+        if self.is_spectral:
+            wl = self._wavelengths(getattr(si, "wavelengths", None), n)
+            k = wl.shape[0]
+        out = torch.empty((k, n), dtype=torch.float32, device=self.device)
+        dout = torch.empty((k, n), dtype=torch.float32, device=self.device)
+        check(lib().sunsky_eval_jvp(self._h, PARAMS[param], _fa(tan), len(tan), vin, _ptr(wl),
+                                    k if self.is_spectral else 0, n, _ptr(m), n, _ptr(out), _ptr(dout), n,
+                                    self._stream()))
+        return out, dout
 
     def eval_spectral_broadcast(self, wi, wavelengths, active=None, out=None):
         """Spectral eval of one wavelength list for every direction -> (m, n)."""

@@ -1,0 +1,108 @@
+"""Forward-mode derivatives of eval() (sunsky_eval_jvp) against central finite
+differences of the fp64 oracle -- the reference differentiates turbidity,
+albedo and sun_direction (sunsky.cpp:220-240; sunsky-testing/traversal_test.py:
+94-145).  Bar: |jvp - fd| <= 2e-3 |fd| + 1e-4 max|fd| per lane (FD truncation
+and fp32 rounding), on the lanes where the quantity is differentiable."""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import oracle as O
+import sunsky_amd as ss
+from helpers import angles_dict, assert_parity, hemisphere_wo, sun_cone_wo
+
+ETA = math.radians(40)
+
+
+def scene(turb=3.4, albedo=0.3, sun=None):
+    d = angles_dict(turb, 0.6, math.pi / 2 - ETA, albedo, 1.0, 1.0)
+    if sun is not None:
+        d["sun_direction"] = [float(v) for v in sun]
+    return d
+
+
+def rays(o):
+    inf = o.info()
+    wo = np.concatenate([hemisphere_wo(1 << 14, seed=11),
+                         sun_cone_wo(1024, inf["sun_dir_local"], np.arccos(inf["cos_cutoff"]), seed=12, scale=0.9)])
+    return wo.astype(np.float32)
+
+
+def check(jvp, fd, mask):
+    j, f = jvp[mask].astype(np.float64), fd[mask]
+    bound = 2e-3 * np.abs(f) + 1e-4 * np.abs(f).max()
+    bad = np.abs(j - f) > bound
+    assert not bad.any(), f"{bad.sum()} lanes over bound, worst {np.max(np.abs(j - f) / bound):.2f}x"
+
+
+def test_jvp_argument_validation_host():
+    em = ss.SunskyEmitter(scene(), "rgb", device="host")
+    lib = ss.lib()
+    t = (ctypes.c_float * 3)(1, 0, 0)
+    vin = ss._capi.Vec3In(None, None, None)
+    # n = 0: the tangent is still staged and validated
+    assert lib.sunsky_eval_jvp(em._h, 0, t, 1, vin, None, 0, 0, None, 0, None, None, 0, None) == 0
+    assert lib.sunsky_eval_jvp(em._h, 0, t, 2, vin, None, 0, 0, None, 0, None, None, 0, None) != 0
+    assert b"turbidity tangent" in lib.sunsky_last_error()
+    assert lib.sunsky_eval_jvp(em._h, 1, t, 3, vin, None, 0, 0, None, 0, None, None, 0, None) == 0
+    assert lib.sunsky_eval_jvp(em._h, 7, t, 1, vin, None, 0, 0, None, 0, None, None, 0, None) != 0
+    hour = ss.SunskyEmitter({"type": "sunsky", "hour": 12.0}, "rgb", device="host")
+    assert lib.sunsky_eval_jvp(hour._h, 2, t, 3, vin, None, 0, 0, None, 0, None, None, 0, None) != 0
+    assert b"time/location" in lib.sunsky_last_error()
+    with pytest.raises(ValueError):
+        em.eval_jvp(ss.SurfaceInteraction3f(wi=torch.zeros(3, 1)), "sky_scale", 1.0)
+
+
+def _gpu(a):
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(a, np.float32).T)).cuda()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+@pytest.mark.parametrize("param", ["turbidity", "albedo", "sun_direction"])
+def test_eval_jvp_matches_finite_differences(variant, param):
+    d = scene()
+    em = ss.load_dict(d, variant=variant)
+    o32 = O.Oracle(d, variant, "jit", "f32")
+    wo = rays(o32)
+    wi = -wo
+    lam = np.random.default_rng(3).uniform(330, 710, (4, wo.shape[0])).astype(np.float32)
+    si = ss.SurfaceInteraction3f(wi=_gpu(wi), wavelengths=torch.from_numpy(lam).cuda() if variant == "spectral" else None)
+    inf = o32.info()
+    s = np.array(d["sun_direction"], np.float64)
+    if param == "turbidity":
+        tangent, h = [1.0], 1e-3
+        plus, minus = scene(turb=3.4 + h), scene(turb=3.4 - h)
+    elif param == "albedo":
+        tangent, h = [1.0], 1e-3
+        plus, minus = scene(albedo=0.3 + h), scene(albedo=0.3 - h)
+    else:
+        t = np.cross(s, [0.0, 0.0, 1.0])
+        t /= np.linalg.norm(t)
+        t = 0.6 * t + 0.8 * np.cross(s, t)            # a tangent mixing azimuth and elevation
+        tangent, h = list(t), 1e-4
+        plus, minus = scene(sun=(s + h * t) / np.linalg.norm(s + h * t)), scene(sun=(s - h * t) / np.linalg.norm(s - h * t))
+    val, dval = em.eval_jvp(si, param, tangent)
+    torch.cuda.synchronize()
+    val, dval = val.cpu().numpy().T, dval.cpu().numpy().T
+    lam_o = lam if variant == "spectral" else None
+    ev = lambda dd: O.Oracle(dd, variant, "jit", "f64").eval(wi, lam_o)   # noqa: E731
+    fd = (ev(plus) - ev(minus)) / (2 * h)
+    fd = fd.T if variant == "spectral" else fd
+    # value: the reference-order eval
+    ref32 = o32.eval(wi, lam_o)
+    ref64 = O.Oracle(d, variant, "jit", "f64").eval(wi, lam_o)
+    ref32, ref64 = (ref32.T, ref64.T) if variant == "spectral" else (ref32, ref64)
+    cosg = wo @ inf["sun_dir_local"]
+    sun = (cosg >= inf["cos_cutoff"]) & (wo[:, 2] >= 0)
+    assert_parity(val, ref32, ref64, sun)
+    mask = np.ones(wo.shape[0], bool)
+    if param == "sun_direction":
+        # the disc test flips under the perturbation and d gamma is singular at gamma = 0
+        mask &= cosg < math.cos(math.radians(1.0))
+    # finite differences straddle no discontinuity: keep lanes away from the horizon
+    mask &= wo[:, 2] > 1e-3
+    check(dval, fd, mask[:, None].repeat(dval.shape[1], 1))

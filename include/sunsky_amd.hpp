@@ -42,6 +42,12 @@ inline void check(int status) {
 enum class Variant { RGB = SUNSKY_VARIANT_RGB, Spectral = SUNSKY_VARIANT_SPECTRAL };
 enum class Semantics { JIT = SUNSKY_SEMANTICS_JIT, Scalar = SUNSKY_SEMANTICS_SCALAR };
 enum class Precision { Fast = SUNSKY_PRECISION_FAST, Reference = SUNSKY_PRECISION_REFERENCE };
+// Differentiable traverse() parameters (sunsky.cpp:220-240)
+enum class Param {
+    Turbidity = SUNSKY_PARAM_TURBIDITY,
+    Albedo = SUNSKY_PARAM_ALBEDO,
+    SunDirection = SUNSKY_PARAM_SUN_DIRECTION
+};
 
 // mitsuba::Properties subset consumed by SunskyEmitter::init_from_props (sunsky.cpp:889-948).
 class Properties {
@@ -174,6 +180,17 @@ public:
     [[noreturn]] void sample_position() const {
         check(sunsky_sample_position(e_));
         throw NotImplementedError("sample_position");
+    }
+    // eval(si) and its forward-mode derivative along `tangent` of `param` (the
+    // reference's dr::forward_from(param) + dr::grad(eval(si))); d_out mirrors out.
+    void eval_jvp(const SurfaceInteraction& si, Param param, const std::vector<float>& tangent, SpectrumOut out,
+                  SpectrumOut d_out, const uint8_t* active = nullptr, void* stream = nullptr) const {
+        const size_t stride = out.stride ? out.stride : si.n;
+        if ((d_out.stride ? d_out.stride : si.n) != stride)
+            throw Error(SUNSKY_ERROR_INVALID_VALUE, "out and d_out must share one plane stride");
+        check(sunsky_eval_jvp(e_, (int)param, tangent.data(), (int)tangent.size(), vin(si.wi), si.wavelengths.data,
+                              si.wavelengths.count, si.wavelengths.stride, active, si.n, out.data, d_out.data, stride,
+                              stream));
     }
     // Spectral eval of one wavelength list broadcast to every ray (test_sunsky.py:42-59 layout)
     void eval_spectral_broadcast(Vector3 wi, size_t n, const std::vector<float>& wavelengths, SpectrumOut out,

@@ -28,7 +28,7 @@ using namespace sunsky_amd;
 
 static void fill_props(Properties& p) {
     const double th = (90.0 - 45.0) * M_PI / 180.0;
-    p.set_float("turbidity", 4.0).set_float("albedo", 0.2);
+    p.set_float("turbidity", 4.3).set_float("albedo", 0.2);
     p.set_vector3("sun_direction", (float)std::sin(th), 0.f, (float)std::cos(th));
 }
 
@@ -79,10 +79,11 @@ static int gpu_mode(const std::string& dir) {
         wi[i] = -st * std::cos(ph); wi[n + i] = -st * std::sin(ph); wi[2 * n + i] = -ct;
         u[i] = U(rng); u[n + i] = U(rng);
     }
-    float *d_wi, *d_u, *d_rgb, *d_d, *d_pdf, *d_w, *d_pdf2;
+    float *d_wi, *d_u, *d_rgb, *d_d, *d_pdf, *d_w, *d_pdf2, *d_jv, *d_djv;
     HIPCK(hipMalloc(&d_wi, 3 * n * 4)); HIPCK(hipMalloc(&d_u, 2 * n * 4)); HIPCK(hipMalloc(&d_rgb, 3 * n * 4));
     HIPCK(hipMalloc(&d_d, 3 * n * 4)); HIPCK(hipMalloc(&d_pdf, n * 4)); HIPCK(hipMalloc(&d_w, 3 * n * 4));
     HIPCK(hipMalloc(&d_pdf2, n * 4));
+    HIPCK(hipMalloc(&d_jv, 3 * n * 4)); HIPCK(hipMalloc(&d_djv, 3 * n * 4));
     HIPCK(hipMemcpy(d_wi, wi.data(), 3 * n * 4, hipMemcpyHostToDevice));
     HIPCK(hipMemcpy(d_u, u.data(), 2 * n * 4, hipMemcpyHostToDevice));
 
@@ -104,9 +105,11 @@ static int gpu_mode(const std::string& dir) {
     DirectionSampleIn dsi;
     dsi.d = {d_d, d_d + n, d_d + 2 * n};
     em.pdf_direction(n, dsi, d_pdf2);
+    em.eval_jvp(si, Param::Turbidity, {1.f}, {d_jv, n}, {d_djv, n});   // d eval / d turbidity
     HIPCK(hipDeviceSynchronize());
 
-    std::vector<float> rgb(3 * n), dd(3 * n), pdf(n), w(3 * n), pdf2(n);
+    std::vector<float> rgb(3 * n), dd(3 * n), pdf(n), w(3 * n), pdf2(n), djv(3 * n);
+    HIPCK(hipMemcpy(djv.data(), d_djv, 3 * n * 4, hipMemcpyDeviceToHost));
     HIPCK(hipMemcpy(rgb.data(), d_rgb, 3 * n * 4, hipMemcpyDeviceToHost));
     HIPCK(hipMemcpy(dd.data(), d_d, 3 * n * 4, hipMemcpyDeviceToHost));
     HIPCK(hipMemcpy(pdf.data(), d_pdf, n * 4, hipMemcpyDeviceToHost));
@@ -114,8 +117,8 @@ static int gpu_mode(const std::string& dir) {
     HIPCK(hipMemcpy(pdf2.data(), d_pdf2, n * 4, hipMemcpyDeviceToHost));
     bool ok = write_file(dir + "/wi.f32", wi) && write_file(dir + "/u.f32", u) && write_file(dir + "/rgb.f32", rgb) &&
               write_file(dir + "/d.f32", dd) && write_file(dir + "/pdf.f32", pdf) && write_file(dir + "/w.f32", w) &&
-              write_file(dir + "/pdf2.f32", pdf2);
-    for (float* ptr : {d_wi, d_u, d_rgb, d_d, d_pdf, d_w, d_pdf2}) (void)hipFree(ptr);
+              write_file(dir + "/pdf2.f32", pdf2) && write_file(dir + "/drgb_dturbidity.f32", djv);
+    for (float* ptr : {d_wi, d_u, d_rgb, d_d, d_pdf, d_w, d_pdf2, d_jv, d_djv}) (void)hipFree(ptr);
     if (!ok) { std::puts("FAIL writing outputs"); return 1; }
     std::printf("gpu ok w_sky=%.9g\n", em.info().sky_sampling_w);
     return 0;

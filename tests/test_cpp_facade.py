@@ -14,7 +14,7 @@ from helpers import assert_parity, max_rel
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "tests", "cpp", "build", "facade_check")
-SUN45 = {"type": "sunsky", "turbidity": 4.0, "albedo": 0.2,
+SUN45 = {"type": "sunsky", "turbidity": 4.3, "albedo": 0.2,
          "sun_direction": [float(np.sin(np.pi / 4)), 0.0, float(np.cos(np.pi / 4))]}
 
 
@@ -62,3 +62,10 @@ def test_facade_gpu_mode(exe, tmp_path):
     o32.override_w_sky(w_gpu)
     ref = o32.sample_direction(u)
     assert np.quantile(np.abs(d - ref["d"]).max(axis=1), 0.999) < 2e-6
+    # eval_jvp through the facade: d eval / d turbidity vs fp64 central differences
+    djv = load("drgb_dturbidity.f32", 3)
+    h = 1e-3
+    fd = (O.Oracle(dict(SUN45, turbidity=4.3 + h), "rgb", "jit", "f64").eval(wi) -
+          O.Oracle(dict(SUN45, turbidity=4.3 - h), "rgb", "jit", "f64").eval(wi)) / (2 * h)
+    keep = wo[:, 2] > 1e-3
+    assert np.all(np.abs(djv[keep] - fd[keep]) <= 2e-3 * np.abs(fd[keep]) + 1e-4 * np.abs(fd[keep]).max())

@@ -201,6 +201,21 @@ int sunsky_eval_jvp(const sunsky_emitter *e, int param, const float *tangent, in
                     sunsky_vec3_in wi, const float *wavelengths, int n_wavelengths, size_t wl_stride,
                     const uint8_t *active, size_t n, float *out, float *d_out, size_t out_stride,
                     void *stream);
+/* Reverse mode: grad[p] += sum over rays and output planes of d_out * d eval / d p,
+ * i.e. the parameter gradients dr.backward(dr.sum(d_out * eval(si))) accumulates in the
+ * reference.  `grad` is a DEVICE array of SUNSKY_GRAD_COUNT floats:
+ *   [SUNSKY_GRAD_TURBIDITY]          turbidity
+ *   [SUNSKY_GRAD_ALBEDO + c]         albedo of channel c (c < 3 RGB, < 11 spectral;
+ *                                    a uniform albedo's gradient is their sum)
+ *   [SUNSKY_GRAD_SUN_DIRECTION + k]  sun_direction, world axis k (0 in time/location mode)
+ * Accumulation is deterministic (fixed-order workgroup and block reductions). */
+#define SUNSKY_GRAD_COUNT 16
+#define SUNSKY_GRAD_TURBIDITY 0
+#define SUNSKY_GRAD_ALBEDO 1
+#define SUNSKY_GRAD_SUN_DIRECTION 12
+int sunsky_eval_vjp(const sunsky_emitter *e, sunsky_vec3_in wi, const float *wavelengths, int n_wavelengths,
+                    size_t wl_stride, const uint8_t *active, size_t n, const float *d_out, size_t out_stride,
+                    float *grad, void *stream);
 
 /* --------------------------------------------- dataset I/O (sunsky_v.cpp:16-18) */
 /* array_from_file_d / _f (sunsky.h:516-561): file_dtype 0 = infer, 1 = fp32, 2 = fp64.

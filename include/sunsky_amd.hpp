@@ -192,6 +192,13 @@ public:
                               si.wavelengths.count, si.wavelengths.stride, active, si.n, out.data, d_out.data, stride,
                               stream));
     }
+    // Reverse mode: grad (device, SUNSKY_GRAD_COUNT floats) += sum(d_out * d eval(si) / d param);
+    // layout SUNSKY_GRAD_TURBIDITY / _ALBEDO + c / _SUN_DIRECTION + k.
+    void eval_vjp(const SurfaceInteraction& si, const float* d_out, size_t d_out_stride, float* grad,
+                  const uint8_t* active = nullptr, void* stream = nullptr) const {
+        check(sunsky_eval_vjp(e_, vin(si.wi), si.wavelengths.data, si.wavelengths.count, si.wavelengths.stride,
+                              active, si.n, d_out, d_out_stride ? d_out_stride : si.n, grad, stream));
+    }
     // Spectral eval of one wavelength list broadcast to every ray (test_sunsky.py:42-59 layout)
     void eval_spectral_broadcast(Vector3 wi, size_t n, const std::vector<float>& wavelengths, SpectrumOut out,
                                  const uint8_t* active = nullptr, void* stream = nullptr) const {

@@ -111,6 +111,7 @@ struct DeviceModule {
     hipModule_t module = nullptr;
     hipFunction_t fn[2][K_COUNT] = {};   // [precision][kernel]
     hipFunction_t jvp_rgb = nullptr, jvp_spec = nullptr;   // eval_jvp (reference operation order)
+    hipFunction_t vjp_rgb = nullptr, vjp_spec = nullptr, grad_reduce = nullptr;   // eval_vjp
     int cu_count = 256;
 };
 
@@ -132,6 +133,9 @@ DeviceModule* module_for_device(int dev) {
         }
     hip_check(hipModuleGetFunction(&m->jvp_rgb, m->module, "sunsky_eval_jvp_rgb"), "sunsky_eval_jvp_rgb");
     hip_check(hipModuleGetFunction(&m->jvp_spec, m->module, "sunsky_eval_jvp_spec"), "sunsky_eval_jvp_spec");
+    hip_check(hipModuleGetFunction(&m->vjp_rgb, m->module, "sunsky_eval_vjp_rgb"), "sunsky_eval_vjp_rgb");
+    hip_check(hipModuleGetFunction(&m->vjp_spec, m->module, "sunsky_eval_vjp_spec"), "sunsky_eval_vjp_spec");
+    hip_check(hipModuleGetFunction(&m->grad_reduce, m->module, "sunsky_grad_reduce"), "sunsky_grad_reduce");
     hip_check(hipDeviceGetAttribute(&m->cu_count, hipDeviceAttributeMultiprocessorCount, dev),
               "hipDeviceGetAttribute");
     DeviceModule* raw = m.release();
@@ -196,6 +200,9 @@ struct sunsky_emitter {
     float* d_sun_table = nullptr;
     float* d_sun_ld = nullptr;
     mutable float* d_jvp = nullptr;   // eval_jvp tangent tables (layout: sunsky_kernels.hip)
+    mutable float* d_vjp = nullptr;   // eval_vjp basis-tangent tables
+    mutable float* d_partials = nullptr;   // eval_vjp per-workgroup gradient partials
+    mutable size_t partials_cap = 0;
 
     void upload() {
         int cur = 0;
@@ -225,6 +232,8 @@ struct sunsky_emitter {
         if (d_sun_table) (void)hipFree(d_sun_table);
         if (d_sun_ld) (void)hipFree(d_sun_ld);
         if (d_jvp) (void)hipFree(d_jvp);
+        if (d_vjp) (void)hipFree(d_vjp);
+        if (d_partials) (void)hipFree(d_partials);
     }
 };
 
@@ -602,6 +611,74 @@ int sunsky_eval_jvp(const sunsky_emitter* e, int param, const float* tangent, in
             void* args[] = {&K, &jvp, &x, &y, &z, &lam, &lstride, &nl, &active, &n, &out, &d_out, &ostride, &sign};
             launch(e->mod->jvp_spec, grid_for(e->mod, K_EVAL_SPEC_RAYS, n), (hipStream_t)stream, args);
         }
+    });
+}
+
+int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam, int nlam, size_t lstride,
+                    const uint8_t* active, size_t n, const float* d_out, size_t ostride, float* grad, void* stream) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (!grad) return fail(SUNSKY_ERROR_INVALID_VALUE, "null gradient buffer");
+    const bool spec = e->kargs.variant == kSpectral;
+    if (n == 0) return SUNSKY_OK;
+    if (spec && (!lam || nlam < 1 || nlam > kMaxLambdaPerRay))
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "spectral eval needs 1..16 wavelength planes");
+    const size_t nout = spec ? (size_t)nlam : 3;
+    if (!wi.x || !wi.y || !wi.z || !d_out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null ray / cotangent pointer");
+    if (nout > 1 && ostride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "out_stride < n");
+    if (spec && nlam > 1 && lstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "wl_stride < n");
+    return guarded([&] {
+        if (!e->mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
+        // basis tangents: turbidity, albedo (all channels at once: channel c's tables depend on
+        // albedo[c] only, so the all-ones tangent is the diagonal), sun_direction x / y / z
+        const SunskyModel& M = *e->model;
+        const int nch = M.nch();
+        const size_t blk = (size_t)kNbWavelengths * 10;
+        std::vector<float> buf(576 + kSunRgbTableSize, 0.f);
+        const float one = 1.f;
+        EvalTangent tT = M.eval_tangent(kJvpTurbidity, &one, 1);
+        std::memcpy(buf.data(), tT.dsky.data(), sizeof(float) * tT.dsky.size());
+        std::memcpy(buf.data() + 576, tT.dsun.data(), sizeof(float) * tT.dsun.size());
+        std::vector<float> ones(nch, 1.f);
+        EvalTangent tA = M.eval_tangent(kJvpAlbedo, ones.data(), nch);
+        std::memcpy(buf.data() + blk, tA.dsky.data(), sizeof(float) * tA.dsky.size());
+        if (!M.active_record())
+            for (int k = 0; k < 3; ++k) {
+                float axis[3] = {0.f, 0.f, 0.f};
+                axis[k] = 1.f;
+                EvalTangent tS = M.eval_tangent(kJvpSunDirection, axis, 3);
+                std::memcpy(buf.data() + (2 + k) * blk, tS.dsky.data(), sizeof(float) * tS.dsky.size());
+                std::memcpy(buf.data() + 5 * blk + 3 * k, tS.dsun_local, 3 * sizeof(float));
+            }
+        const KernelId kid = spec ? K_EVAL_SPEC_RAYS : K_EVAL_RGB_V1;
+        const unsigned grid = grid_for(e->mod, kid, n);
+        if (!e->d_vjp) hip_check(hipMalloc(&e->d_vjp, sizeof(float) * buf.size()), "hipMalloc");
+        // a previous eval_vjp of this emitter may still read the tables / partials
+        hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        if (e->partials_cap < grid) {
+            if (e->d_partials) hip_check(hipFree(e->d_partials), "hipFree");
+            e->d_partials = nullptr;
+            hip_check(hipMalloc(&e->d_partials, sizeof(float) * 16 * grid), "hipMalloc");
+            e->partials_cap = grid;
+        }
+        hip_check(hipMemcpy(e->d_vjp, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice), "hipMemcpy");
+        SunskyKArgs K = e->kargs;
+        const float* vjp = e->d_vjp;
+        float* partials = e->d_partials;
+        const float *x = wi.x, *y = wi.y, *z = wi.z;
+        float sign = -1.f;
+        hipStream_t st = (hipStream_t)stream;
+        if (!spec) {
+            void* args[] = {&K, &vjp, &x, &y, &z, &active, &n, &d_out, &ostride, &sign, &partials};
+            launch(e->mod->vjp_rgb, grid, st, args);
+        } else {
+            int nl = nlam;
+            void* args[] = {&K, &vjp, &x, &y, &z, &lam, &lstride, &nl, &active, &n, &d_out, &ostride, &sign, &partials};
+            launch(e->mod->vjp_spec, grid, st, args);
+        }
+        unsigned nb = grid;
+        void* rargs[] = {&partials, &nb, &grad};
+        hip_check(hipModuleLaunchKernel(e->mod->grad_reduce, 1, 1, 1, 64, 1, 1, 0, st, rargs, nullptr),
+                  "hipModuleLaunchKernel");
     });
 }
 

@@ -1092,6 +1092,200 @@ __device__ __forceinline__ void eval_jvp_spec_body(const SunskyKArgs& K, const f
 }
 
 // ======================================================================
+// eval_vjp: reverse mode.  grad[p] += sum_rays sum_channels d_out * d eval / d p
+// for p = turbidity (0), albedo per channel (1 + c), sun_direction x/y/z (12..14),
+// the gradient dr.backward(dot(d_out, eval(si))) accumulates in the reference.
+// Each ray evaluates the derivative along the 5 basis tangents (T, albedo
+// diagonal, 3 sun axes) with the JVP kernels' device code; the sums are reduced
+// per workgroup in a fixed order (wave shuffles, then LDS) into per-block
+// partials, which sunsky_grad_reduce adds to grad in block order --
+// deterministic, no float atomics.
+// vjp buffer: [0, 550) dsky for T / albedo-diagonal / sun x / sun y / sun z
+// (5 x 110), [550, 559) d local sun direction of the 3 sun axes, [576, ...) d sun table (T).
+// ======================================================================
+constexpr int kGradCount = 16;           // 0: T, 1..11: albedo channel, 12..14: sun_direction, 15: pad
+constexpr int kVjpSunOffset = 576;
+
+struct VjpLds {
+    float dsky[5][kNbWavelengths * 10];
+    float dlocal[3][3];
+    float red[SS_BLOCK / 64][kGradCount];
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    return v;   // lane 0 holds the wave's sum
+}
+
+// Per-workgroup reduction of the per-lane gradient accumulators -> partials[block][16]
+__device__ __forceinline__ void block_reduce_grad(VjpLds& L, const float g[kGradCount], float* partials) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int p = 0; p < kGradCount; ++p) {
+        float w = wave_sum(g[p]);
+        if (lane == 0) L.red[wave][p] = w;
+    }
+    __syncthreads();
+    if (threadIdx.x < kGradCount) {
+        float acc = 0.f;
+        for (int w = 0; w < SS_BLOCK / 64; ++w) acc += L.red[w][threadIdx.x];
+        partials[(size_t)blockIdx.x * kGradCount + threadIdx.x] = acc;
+    }
+}
+
+__device__ __forceinline__ void stage_vjp(const float* vjp, VjpLds* L) {
+    for (int i = threadIdx.x; i < 5 * kNbWavelengths * 10; i += blockDim.x) (&L->dsky[0][0])[i] = vjp[i];
+    if (threadIdx.x < 9) (&L->dlocal[0][0])[threadIdx.x] = vjp[5 * kNbWavelengths * 10 + threadIdx.x];
+    __syncthreads();
+}
+
+__device__ __forceinline__ void eval_vjp_rgb_body(const SunskyKArgs& K, const float* __restrict__ vjp,
+                                                  const float* __restrict__ wx, const float* __restrict__ wy,
+                                                  const float* __restrict__ wz, const uint8_t* __restrict__ active,
+                                                  size_t n, const float* __restrict__ dout, size_t ostride,
+                                                  float sign, float* __restrict__ partials) {
+    __shared__ VjpLds L;
+    stage_vjp(vjp, &L);
+    const float* dsun_tab = vjp + kVjpSunOffset;
+    const float cie = (float)kCieYNormalization, conv = (float)kSpecToRgbSunConv;
+    const float3_ sn = mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]);
+    float g[kGradCount];
+#pragma unroll
+    for (int p = 0; p < kGradCount; ++p) g[p] = 0.f;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        bool m = active ? active[i] != 0 : true;
+        float3_ wo = to_local(K, mk3(sign * wx[i], sign * wy[i], sign * wz[i]));
+        DirTerms t = dir_terms<false>(K, wo, m);
+        if (!t.active) continue;
+        const float sg = sinf(t.gamma);
+        float dgs[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dgs[k] = unit_angle_tangent(sn, wo, mk3(L.dlocal[k][0], L.dlocal[k][1], L.dlocal[k][2]));
+        int pos = 0;
+        float xs = 0.f, cp = 0.f, dcps[3] = {0.f, 0.f, 0.f};
+        if (t.hit_sun) {
+            pos = sun_segment(t.cos_theta, &xs);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cos_psi_jvp(K, t, sg, dgs[k], &cp, &dcps[k]);
+        }
+        const float sc = K.sun_scale * K.area_ratio * conv;
+#pragma unroll 1
+        for (int c = 0; c < 3; ++c) {
+            const float cot = dout[(size_t)c * ostride + i] * cie;
+            float v, d;
+            sky_jvp(K.sky[c], L.dsky[0] + c * 10, t, 0.f, sg, &v, &d);
+            g[0] += cot * K.sky_scale * d;
+            sky_jvp(K.sky[c], L.dsky[1] + c * 10, t, 0.f, sg, &v, &d);
+            g[1 + c] += cot * K.sky_scale * d;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                sky_jvp(K.sky[c], L.dsky[2 + k] + c * 10, t, dgs[k], sg, &v, &d);
+                g[12 + k] += cot * K.sky_scale * d;
+            }
+            if (t.hit_sun) {
+                const float* S = K.sun_table + pos * (3 * kNbSunCtrlPts * kNbSunLdParams) + c * (kNbSunCtrlPts * kNbSunLdParams);
+                const float* dS = dsun_tab + pos * (3 * kNbSunCtrlPts * kNbSunLdParams) + c * (kNbSunCtrlPts * kNbSunLdParams);
+                float dT = 0.f, dC = 0.f;   // d/dT, d/d cos_psi
+                for (int kk = 0; kk < kNbSunCtrlPts; ++kk)
+                    for (int j = 0; j < kNbSunLdParams; ++j) {
+                        const float xk = powif_(xs, kk);
+                        dT += xk * powif_(cp, j) * dS[kk * kNbSunLdParams + j];
+                        if (j > 0) dC += xk * (float)j * powif_(cp, j - 1) * S[kk * kNbSunLdParams + j];
+                    }
+                g[0] += cot * sc * dT;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) g[12 + k] += cot * sc * dC * dcps[k];
+            }
+        }
+    }
+    block_reduce_grad(L, g, partials);
+}
+
+__device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const float* __restrict__ vjp,
+                                                   const float* __restrict__ wx, const float* __restrict__ wy,
+                                                   const float* __restrict__ wz, const float* __restrict__ lam,
+                                                   size_t lstride, int nlam, const uint8_t* __restrict__ active,
+                                                   size_t n, const float* __restrict__ dout, size_t ostride,
+                                                   float sign, float* __restrict__ partials) {
+    __shared__ VjpLds L;
+    stage_vjp(vjp, &L);
+    const float* dsun_tab = vjp + kVjpSunOffset;
+    const float3_ sn = mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]);
+    float g[kGradCount];
+#pragma unroll
+    for (int p = 0; p < kGradCount; ++p) g[p] = 0.f;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        bool m = active ? active[i] != 0 : true;
+        float3_ wo = to_local(K, mk3(sign * wx[i], sign * wy[i], sign * wz[i]));
+        DirTerms t = dir_terms<false>(K, wo, m);
+        if (!t.active) continue;
+        const float sg = sinf(t.gamma);
+        float dgs[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dgs[k] = unit_angle_tangent(sn, wo, mk3(L.dlocal[k][0], L.dlocal[k][1], L.dlocal[k][2]));
+        int pos = 0;
+        float xs = 0.f, cp = 0.f, dcps[3] = {0.f, 0.f, 0.f};
+        if (t.hit_sun) {
+            pos = sun_segment(t.cos_theta, &xs);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) cos_psi_jvp(K, t, sg, dgs[k], &cp, &dcps[k]);
+        }
+        for (int q = 0; q < nlam; ++q) {
+            const float cot = dout[(size_t)q * ostride + i];
+            const float lambda = lam[(size_t)q * lstride + i];
+            float nw = (lambda - kWavelength0) / kWavelengthStep;
+            if (!((0.f <= nw) && (nw <= (float)(kNbWavelengths - 1)))) continue;
+            int lo = (int)floorf(nw), hi = lo + 1;
+            float f = nw - (float)lo;
+            const bool has_hi = f != 0.f && hi < kNbWavelengths;
+            const float wlo = f != 0.f ? 1.f - f : 1.f, whi = f;   // lerp weights (f = 0: low channel only)
+            float v, da, db = 0.f;
+            // turbidity, albedo (diagonal), sun axes: each lerped over the two channels
+            sky_jvp(K.sky[lo], L.dsky[0] + lo * 10, t, 0.f, sg, &v, &da);
+            if (has_hi) sky_jvp(K.sky[hi], L.dsky[0] + hi * 10, t, 0.f, sg, &v, &db);
+            g[0] += cot * K.sky_scale * (wlo * da + whi * db);
+            sky_jvp(K.sky[lo], L.dsky[1] + lo * 10, t, 0.f, sg, &v, &da);
+            g[1 + lo] += cot * K.sky_scale * wlo * da;
+            if (has_hi) {
+                sky_jvp(K.sky[hi], L.dsky[1] + hi * 10, t, 0.f, sg, &v, &db);
+                g[1 + hi] += cot * K.sky_scale * whi * db;
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                db = 0.f;
+                sky_jvp(K.sky[lo], L.dsky[2 + k] + lo * 10, t, dgs[k], sg, &v, &da);
+                if (has_hi) sky_jvp(K.sky[hi], L.dsky[2 + k] + hi * 10, t, dgs[k], sg, &v, &db);
+                g[12 + k] += cot * K.sky_scale * (wlo * da + whi * db);
+            }
+            if (t.hit_sun) {
+                float sa = render_sun_spec(K.sun_table, pos, lo, xs), dsa = render_sun_spec(dsun_tab, pos, lo, xs);
+                float sun = sa, dsun = dsa;
+                if (f != 0.f) {
+                    float sb = hi < kNbWavelengths ? render_sun_spec(K.sun_table, pos, hi, xs) : 0.f;
+                    float dsb = hi < kNbWavelengths ? render_sun_spec(dsun_tab, pos, hi, xs) : 0.f;
+                    sun = lerpf_(sa, sb, f);
+                    dsun = lerpf_(dsa, dsb, f);
+                }
+                float ld = sun_limb_darkening(K.sun_ld, lo, hi, f, cp), dldc = 0.f;
+                for (int j = 1; j < kNbSunLdParams; ++j) {
+                    float a = K.sun_ld[lo * kNbSunLdParams + j], coef = a;
+                    if (f != 0.f) coef = lerpf_(a, hi < kNbWavelengths ? K.sun_ld[hi * kNbSunLdParams + j] : 0.f, f);
+                    dldc += (float)j * powif_(cp, j - 1) * coef;
+                }
+                const float sc = K.sun_scale * K.area_ratio;
+                g[0] += cot * sc * dsun * ld;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) g[12 + k] += cot * sc * sun * dldc * dcps[k];
+            }
+        }
+    }
+    block_reduce_grad(L, g, partials);
+}
+
+// ======================================================================
 // extern "C" entry points (hipModuleGetFunction names)
 // ======================================================================
 #define SS_EVAL_RGB(NAME, VEC, FAST)                                                                          \
@@ -1190,4 +1384,26 @@ extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_jvp_spec(
     SunskyKArgs K, const float* jvp, const float* wx, const float* wy, const float* wz, const float* lam,
     size_t lstride, int nlam, const uint8_t* active, size_t n, float* out, float* dout, size_t ostride, float sign) {
     eval_jvp_spec_body(K, jvp, wx, wy, wz, lam, lstride, nlam, active, n, out, dout, ostride, sign);
+}
+
+extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_vjp_rgb(
+    SunskyKArgs K, const float* vjp, const float* wx, const float* wy, const float* wz, const uint8_t* active,
+    size_t n, const float* dout, size_t ostride, float sign, float* partials) {
+    eval_vjp_rgb_body(K, vjp, wx, wy, wz, active, n, dout, ostride, sign, partials);
+}
+extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_vjp_spec(
+    SunskyKArgs K, const float* vjp, const float* wx, const float* wy, const float* wz, const float* lam,
+    size_t lstride, int nlam, const uint8_t* active, size_t n, const float* dout, size_t ostride, float sign,
+    float* partials) {
+    eval_vjp_spec_body(K, vjp, wx, wy, wz, lam, lstride, nlam, active, n, dout, ostride, sign, partials);
+}
+// grad[p] += sum over blocks (in block order) of partials[block][p]; one wave.
+extern "C" __global__ __launch_bounds__(64) void sunsky_grad_reduce(const float* partials, unsigned nblocks,
+                                                                     float* grad) {
+    const int p = threadIdx.x;
+    if (p < kGradCount) {
+        float acc = 0.f;
+        for (unsigned b = 0; b < nblocks; ++b) acc += partials[(size_t)b * kGradCount + p];
+        grad[p] += acc;
+    }
 }

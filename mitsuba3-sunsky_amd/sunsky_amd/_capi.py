@@ -23,6 +23,7 @@ TABLES = {"sky_params": 0, "sky_radiance": 1, "sun_radiance": 2, "sun_ld": 3, "g
           "gaussian_cdf": 5, "spectral_pdf": 6, "spectral_cdf": 7, "albedo": 8}
 FLAG_INFINITE, FLAG_SPATIALLY_VARYING = 0x04, 0x10
 PARAMS = {"turbidity": 0, "albedo": 1, "sun_direction": 2}   # sunsky_param (differentiable, sunsky.cpp:220-240)
+GRAD_COUNT, GRAD_TURBIDITY, GRAD_ALBEDO, GRAD_SUN_DIRECTION = 16, 0, 1, 12   # eval_vjp gradient layout
 
 c_float_p = C.POINTER(C.c_float)
 vp = C.c_void_p
@@ -81,6 +82,7 @@ _SIGS = {
     "sunsky_sample_position": (C.c_int, [vp]),
     "sunsky_eval_jvp": (C.c_int, [vp, C.c_int, c_float_p, C.c_int, Vec3In, vp, C.c_int, C.c_size_t, vp, C.c_size_t,
                                   vp, vp, C.c_size_t, vp]),
+    "sunsky_eval_vjp": (C.c_int, [vp, Vec3In, vp, C.c_int, C.c_size_t, vp, C.c_size_t, vp, C.c_size_t, vp, vp]),
     "sunsky_array_from_file": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_double), C.c_size_t,
                                          C.POINTER(C.c_size_t), C.POINTER(C.c_uint64), C.POINTER(C.c_int)]),
     "sunsky_array_to_file": (C.c_int, [C.c_char_p, c_float_p, C.c_size_t, C.POINTER(C.c_uint64), C.c_int]),

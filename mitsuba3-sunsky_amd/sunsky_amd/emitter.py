@@ -313,6 +313,30 @@ class SunskyEmitter:
                                     self._stream()))
         return out, dout
 
+    def eval_vjp(self, si, d_out, active=None, grad=None):
+        """Reverse mode: accumulate sum(d_out * d eval(si) / d param) into `grad` (a (16,)
+        device tensor; zeros if None) and return it together with a dict view
+        {"turbidity", "albedo" (per channel), "sun_direction" (world, 3)}."""
+        wi, vin = self._vec_in(si.wi)
+        n = wi.shape[1]
+        m = self._mask(active, n)
+        wl, k = None, 3
+        if self.is_spectral:
+            wl = self._wavelengths(getattr(si, "wavelengths", None), n)
+            k = wl.shape[0]
+        d_out = self._f32(d_out)
+        if tuple(d_out.shape) != (k, n):
+            raise ValueError(f"d_out must have shape ({k}, {n})")
+        if grad is None:
+            grad = torch.zeros(_capi.GRAD_COUNT, dtype=torch.float32, device=self.device)
+        check(lib().sunsky_eval_vjp(self._h, vin, _ptr(wl), k if self.is_spectral else 0, n, _ptr(m), n,
+                                    _ptr(d_out), n, _ptr(grad), self._stream()))
+        nch = 11 if self.is_spectral else 3
+        view = {"turbidity": grad[_capi.GRAD_TURBIDITY],
+                "albedo": grad[_capi.GRAD_ALBEDO:_capi.GRAD_ALBEDO + nch],
+                "sun_direction": grad[_capi.GRAD_SUN_DIRECTION:_capi.GRAD_SUN_DIRECTION + 3]}
+        return grad, view
+
     def eval_spectral_broadcast(self, wi, wavelengths, active=None, out=None):
         """Spectral eval of one wavelength list for every direction -> (m, n)."""
         wi, vin = self._vec_in(wi)

@@ -262,6 +262,22 @@ def main():
                                        "note": "headline kernel, 4 distinct input batches round-robin so "
                                                "inputs cannot stay in the 256 MiB Infinity Cache"}
         del cold_in, cold_v
+        # caller: 8192 x 4096 lat-long RGB bake of the sky (write-only, 12 B per pixel)
+        bw, bh = 8192, 4096
+        bake_out = torch.empty((3, bh, bw), dtype=torch.float32, device=dev)
+        for _ in range(2):
+            ems[0].bake_latlong(bw, bh, out=bake_out)
+        tm = KernelTimer()
+        reps = max(3, args.steps // 4)
+        tm.begin()
+        for _ in range(reps):
+            ems[0].bake_latlong(bw, bh, out=bake_out)
+        tm.end(reps)
+        ms = tm.mean_ms()
+        sec["latlong_bake_8192x4096"] = {"kernel_ms": ms, "pixels_per_s": bw * bh / (ms * 1e-3),
+                                         "achieved_GBps": 12 * bw * bh / (ms * 1e-3) / 1e9,
+                                         "note": "sunsky_bake_latlong: directions generated on device, RGB writes only"}
+        del bake_out
         # C3: spectral eval, 11 model wavelengths broadcast
         spec = ss.SunskyEmitter(dict(sun_dict(3.0), albedo=0.3), "spectral", precision=args.precision, device=dev)
         lams = [float(x) for x in range(320, 721, 40)]

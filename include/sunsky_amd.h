@@ -185,6 +185,17 @@ int sunsky_sample_wavelengths(const sunsky_emitter *e, sunsky_vec3_in wi, const 
 /* sample_position(), sunsky.cpp:483-495: NotImplementedError in the reference */
 int sunsky_sample_position(const sunsky_emitter *e);
 
+/* Lat-long bake of the sky (a caller of eval, as sunsky-testing/sky_data_test.py:58-79
+ * builds an environment map from eval over helpers.py get_spherical_rays): pixel (x, y)
+ * of a width x height image holds eval(si.wi = -sphdir(theta_y, phi_x)) with
+ * theta_y = linspace(theta0, theta1, height)[y], phi_x = linspace(phi0, phi1, width)[x]
+ * (z-up, local frame of to_world applied).  Planes [c][height * width], row-major:
+ * 3 RGB planes, or one per host wavelength (spectral).  Directions are generated on the
+ * device: the bake only writes HBM. */
+int sunsky_bake_latlong(const sunsky_emitter *e, int width, int height, float theta0, float theta1,
+                        float phi0, float phi1, const float *wavelengths_host, int n_wavelengths,
+                        float *out, size_t out_stride, void *stream);
+
 /* ------------------------------------------------ forward-mode derivatives */
 typedef enum sunsky_param {         /* Differentiable traverse() parameters, sunsky.cpp:220-240 */
     SUNSKY_PARAM_TURBIDITY = 0,     /* tangent: 1 value                               */

@@ -199,6 +199,14 @@ public:
         check(sunsky_eval_vjp(e_, vin(si.wi), si.wavelengths.data, si.wavelengths.count, si.wavelengths.stride,
                               active, si.n, d_out, d_out_stride ? d_out_stride : si.n, grad, stream));
     }
+    // Lat-long environment map of the sky (sunsky_bake_latlong): planes [c][height * width]
+    void bake_latlong(int width, int height, float theta0, float theta1, float phi0, float phi1, SpectrumOut out,
+                      const std::vector<float>& wavelengths = {}, void* stream = nullptr) const {
+        const size_t n = (size_t)width * (size_t)height;
+        check(sunsky_bake_latlong(e_, width, height, theta0, theta1, phi0, phi1,
+                                  wavelengths.empty() ? nullptr : wavelengths.data(), (int)wavelengths.size(),
+                                  out.data, out.stride ? out.stride : n, stream));
+    }
     // Spectral eval of one wavelength list broadcast to every ray (test_sunsky.py:42-59 layout)
     void eval_spectral_broadcast(Vector3 wi, size_t n, const std::vector<float>& wavelengths, SpectrumOut out,
                                  const uint8_t* active = nullptr, void* stream = nullptr) const {

@@ -99,13 +99,14 @@ std::string code_object_path() {
 enum KernelId {
     K_EVAL_RGB_V4, K_EVAL_RGB_V1, K_EVAL_SPEC_BCAST_V4, K_EVAL_SPEC_BCAST_V1, K_EVAL_SPEC_NODES_V4,
     K_EVAL_SPEC_RAYS, K_SAMPLE_DIRECTION_RGB, K_SAMPLE_DIRECTION_SPEC, K_PDF_DIRECTION, K_SAMPLE_WAVELENGTHS_RGB,
-    K_SAMPLE_WAVELENGTHS_SPEC, K_SAMPLE_RAY_RGB, K_SAMPLE_RAY_SPEC, K_COUNT
+    K_SAMPLE_WAVELENGTHS_SPEC, K_SAMPLE_RAY_RGB, K_SAMPLE_RAY_SPEC, K_BAKE_RGB, K_BAKE_SPEC, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
     "sunsky_eval_spec_nodes_v4", "sunsky_eval_spec_rays", "sunsky_sample_direction_rgb",
     "sunsky_sample_direction_spec", "sunsky_pdf_direction", "sunsky_sample_wavelengths_rgb",
-    "sunsky_sample_wavelengths_spec", "sunsky_sample_ray_rgb", "sunsky_sample_ray_spec"};
+    "sunsky_sample_wavelengths_spec", "sunsky_sample_ray_rgb", "sunsky_sample_ray_spec",
+    "sunsky_bake_latlong_rgb", "sunsky_bake_latlong_spec"};
 
 struct DeviceModule {
     hipModule_t module = nullptr;
@@ -161,6 +162,7 @@ int blocks_per_cu(KernelId k) {
         case K_EVAL_RGB_V4: case K_EVAL_RGB_V1: return 64;
         case K_EVAL_SPEC_BCAST_V4: case K_EVAL_SPEC_BCAST_V1: case K_EVAL_SPEC_NODES_V4: return 64;
         case K_SAMPLE_DIRECTION_RGB: case K_SAMPLE_DIRECTION_SPEC: case K_PDF_DIRECTION: return 64;
+        case K_BAKE_RGB: case K_BAKE_SPEC: return 64;
         default: return 16;
     }
 }
@@ -183,6 +185,26 @@ struct LambdaSet {   // mirrors the kernel-side struct
     int lo[kMaxBroadcastLambda];
     float f[kMaxBroadcastLambda];
 };
+
+struct LatLong {     // mirrors the kernel-side struct
+    int w, h;
+    float theta0, dtheta, phi0, dphi;
+};
+
+// normalized_wavelengths / floor2int / lerp factor of eval, sunsky.cpp:326-332
+LambdaSet make_lambda_set(const float* lam, int m) {
+    LambdaSet L;
+    std::memset(&L, 0, sizeof(L));
+    L.m = m;
+    for (int k = 0; k < m; ++k) {
+        float nw = (lam[k] - kWavelength0) / kWavelengthStep;
+        bool valid = (0.f <= nw) && (nw <= (float)(kNbWavelengths - 1));
+        int lo = valid ? (int)std::floor(nw) : 0;
+        L.lo[k] = lo;
+        L.f[k] = valid ? nw - (float)lo : -1.f;
+    }
+    return L;
+}
 
 }  // namespace
 
@@ -466,17 +488,7 @@ int sunsky_eval_spectral_broadcast(const sunsky_emitter* e, sunsky_vec3_in w, co
     if (n == 0) return SUNSKY_OK;
     if (!w.x || !w.y || !w.z || !out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null ray / output pointer");
     if (m > 1 && ostride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "out_stride < n");
-    LambdaSet L;
-    std::memset(&L, 0, sizeof(L));
-    L.m = m;
-    for (int k = 0; k < m; ++k) {
-        // normalized_wavelengths / floor2int / lerp factor, sunsky.cpp:326-332
-        float nw = (lam_host[k] - kWavelength0) / kWavelengthStep;
-        bool valid = (0.f <= nw) && (nw <= (float)(kNbWavelengths - 1));
-        int lo = valid ? (int)std::floor(nw) : 0;
-        L.lo[k] = lo;
-        L.f[k] = valid ? nw - (float)lo : -1.f;
-    }
+    LambdaSet L = make_lambda_set(lam_host, m);
     // The 11 model wavelengths 320:40:720 in order: compile-time channel kernel.
     bool nodes = m == kNbWavelengths;
     for (int k = 0; nodes && k < m; ++k) nodes = L.lo[k] == k && L.f[k] == 0.f;
@@ -679,6 +691,34 @@ int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam
         void* rargs[] = {&partials, &nb, &grad};
         hip_check(hipModuleLaunchKernel(e->mod->grad_reduce, 1, 1, 1, 64, 1, 1, 0, st, rargs, nullptr),
                   "hipModuleLaunchKernel");
+    });
+}
+
+int sunsky_bake_latlong(const sunsky_emitter* e, int width, int height, float theta0, float theta1, float phi0,
+                        float phi1, const float* lam_host, int m, float* out, size_t ostride, void* stream) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (width < 1 || height < 1) return fail(SUNSKY_ERROR_INVALID_VALUE, "image size must be >= 1 x 1");
+    const bool spec = e->kargs.variant == kSpectral;
+    if (spec && (!lam_host || m < 1 || m > kMaxBroadcastLambda))
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "1..32 wavelengths required for a spectral bake");
+    if (!spec && lam_host && m) return fail(SUNSKY_ERROR_INVALID_VALUE, "RGB bake takes no wavelengths");
+    const size_t n = (size_t)width * (size_t)height;
+    if (!out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null output pointer");
+    if (ostride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "out_stride < width * height");
+    // dr::linspace(start, end, count): step = (end - start) / (count - 1) in fp32
+    LatLong G = {width, height, theta0, height > 1 ? (theta1 - theta0) / (float)(height - 1) : 0.f,
+                 phi0, width > 1 ? (phi1 - phi0) / (float)(width - 1) : 0.f};
+    return guarded([&] {
+        SunskyKArgs K = e->kargs;
+        hipStream_t s = (hipStream_t)stream;
+        if (!spec) {
+            void* args[] = {&K, &G, &out, &ostride};
+            launch(e->fn(K_BAKE_RGB), grid_for(e->mod, K_BAKE_RGB, (n + 3) / 4), s, args);
+        } else {
+            LambdaSet L = make_lambda_set(lam_host, m);
+            void* args[] = {&K, &G, &L, &out, &ostride};
+            launch(e->fn(K_BAKE_SPEC), grid_for(e->mod, K_BAKE_SPEC, n), s, args);
+        }
     });
 }
 

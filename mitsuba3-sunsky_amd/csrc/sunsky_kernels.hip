@@ -913,6 +913,82 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
 }
 
 // ======================================================================
+// Lat-long bake (a caller of eval: sky -> environment map, as the reference's
+// sunsky-testing/sky_data_test.py:58-79 builds an envmap from eval() over
+// helpers.py get_spherical_rays): pixel (x, y) of a W x H image looks along
+// d = sphdir(theta_y, phi_x), theta_y = linspace(theta0, theta1, H)[y],
+// phi_x = linspace(phi0, phi1, W)[x] (dr::linspace: fma(i, step, start)), and
+// holds eval(si.wi = -d).  Directions are generated in-kernel: the bake only
+// writes HBM (12 B per RGB pixel).  Planes [c][H * W], row-major.
+// ======================================================================
+struct LatLong { int w, h; float theta0, dtheta, phi0, dphi; };
+
+__device__ __forceinline__ float3_ latlong_dir(const LatLong& G, size_t i) {
+    const int x = (int)(i % (size_t)G.w), y = (int)(i / (size_t)G.w);
+    const float theta = fmaf((float)y, G.dtheta, G.theta0), phi = fmaf((float)x, G.dphi, G.phi0);
+    float st, ct, sp, cp;
+    sincosf(theta, &st, &ct);
+    sincosf(phi, &sp, &cp);
+    return mk3(cp * st, sp * st, ct);
+}
+
+template <bool FAST>
+__device__ __forceinline__ void bake_rgb_body(const SunskyKArgs& K, LatLong G, float* __restrict__ out,
+                                              size_t ostride) {
+    const size_t n = (size_t)G.w * G.h, ngroups = (n + 3) / 4;
+    const bool vec_ok = ((uintptr_t)out & 15u) == 0 && (ostride & 3u) == 0;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < ngroups; v += stride) {
+        const size_t i0 = v * 4;
+        float r[4] = {0, 0, 0, 0}, g[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (i0 + j >= n) break;
+            float3_ d = latlong_dir(G, i0 + j);
+            float o[3];
+            eval_rgb_local<FAST>(K, K.sun_table, to_local(K, d), true, o);
+            r[j] = o[0]; g[j] = o[1]; b[j] = o[2];
+        }
+        if (vec_ok && i0 + 4 <= n) {
+            store_vec<4>(out, i0, r);
+            store_vec<4>(out + ostride, i0, g);
+            store_vec<4>(out + 2 * ostride, i0, b);
+        } else {
+            for (int j = 0; j < 4 && i0 + j < n; ++j) {
+                out[i0 + j] = r[j];
+                out[ostride + i0 + j] = g[j];
+                out[2 * ostride + i0 + j] = b[j];
+            }
+        }
+    }
+}
+
+template <bool FAST>
+__device__ __forceinline__ void bake_spec_body(const SunskyKArgs& K, LatLong G, const LambdaSet& L,
+                                               float* __restrict__ out, size_t ostride) {
+    __shared__ ChanLds<FAST> S;
+    const auto* chans = stage_chans<FAST>(K, &S);
+    __syncthreads();
+    const size_t n = (size_t)G.w * G.h;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        DirTerms t = dir_terms<FAST>(K, to_local(K, latlong_dir(G, i)), true);
+        add_sun_terms<FAST>(K, t);
+        for (int k = 0; k < L.m; ++k) {
+            const int lo = L.lo[k];
+            const float f = L.f[k];
+            float o = 0.f;
+            if (f >= 0.f && t.active) {
+                o = sky_eval<FAST>(chans[lo], t, K.sky_scale);
+                if (f != 0.f) o = lerpf_(o, lo + 1 < kNbWavelengths ? sky_eval<FAST>(chans[lo + 1], t, K.sky_scale) : 0.f, f);
+                if (t.hit_sun) o += sun_spec_term<FAST>(K, K.sun_table, K.sun_ld, t, lo, f);
+            }
+            __builtin_nontemporal_store(o, out + (size_t)k * ostride + i);
+        }
+    }
+}
+
+// ======================================================================
 // eval_jvp: forward-mode derivative of eval() with respect to one
 // differentiable parameter (turbidity / albedo / sun_direction, sunsky.cpp:
 // 220-240) -- what dr::forward_from(param) + dr::grad(eval(si)) give in the
@@ -1407,3 +1483,15 @@ extern "C" __global__ __launch_bounds__(64) void sunsky_grad_reduce(const float*
         grad[p] += acc;
     }
 }
+
+#define SS_BAKE(NAME_RGB, NAME_SPEC, FAST)                                                                    \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME_RGB(SunskyKArgs K, LatLong G, float* out,      \
+                                                                    size_t ostride) {                          \
+        bake_rgb_body<FAST>(K, G, out, ostride);                                                               \
+    }                                                                                                          \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME_SPEC(SunskyKArgs K, LatLong G, LambdaSet L,    \
+                                                                     float* out, size_t ostride) {             \
+        bake_spec_body<FAST>(K, G, L, out, ostride);                                                           \
+    }
+SS_BAKE(sunsky_bake_latlong_rgb_fast, sunsky_bake_latlong_spec_fast, true)
+SS_BAKE(sunsky_bake_latlong_rgb_ref, sunsky_bake_latlong_spec_ref, false)

@@ -6,6 +6,7 @@ Every batch method takes and returns torch tensors on the emitter's GPU in SoA
 layout ((3, n) vectors, (k, n) spectra) and runs on the current torch stream.
 """
 import ctypes as C
+import math
 
 import numpy as np
 import torch
@@ -336,6 +337,24 @@ class SunskyEmitter:
                 "albedo": grad[_capi.GRAD_ALBEDO:_capi.GRAD_ALBEDO + nch],
                 "sun_direction": grad[_capi.GRAD_SUN_DIRECTION:_capi.GRAD_SUN_DIRECTION + 3]}
         return grad, view
+
+    def bake_latlong(self, width, height, theta=(0.0, math.pi), phi=(0.0, 2 * math.pi), wavelengths=None,
+                     out=None):
+        """Lat-long environment map of the emitter (sunsky_bake_latlong): (C, height, width),
+        pixel (x, y) = eval(wi = -sphdir(linspace(*theta, height)[y], linspace(*phi, width)[x]))
+        -- sunsky-testing/sky_data_test.py:58-79 with helpers.py get_spherical_rays."""
+        if self.is_spectral:
+            if wavelengths is None:
+                raise ValueError("a spectral bake needs a wavelength list")
+            lam = [float(x) for x in np.atleast_1d(np.asarray(wavelengths, dtype=np.float32))]
+            k, lam_p, m = len(lam), _fa(lam), len(lam)
+        else:
+            k, lam_p, m = 3, None, 0
+        if out is None:
+            out = torch.empty((k, height, width), dtype=torch.float32, device=self.device)
+        check(lib().sunsky_bake_latlong(self._h, width, height, float(theta[0]), float(theta[1]), float(phi[0]),
+                                        float(phi[1]), lam_p, m, _ptr(out), height * width, self._stream()))
+        return out
 
     def eval_spectral_broadcast(self, wi, wavelengths, active=None, out=None):
         """Spectral eval of one wavelength list for every direction -> (m, n)."""

@@ -113,6 +113,7 @@ struct DeviceModule {
     hipFunction_t fn[2][K_COUNT] = {};   // [precision][kernel]
     hipFunction_t jvp_rgb = nullptr, jvp_spec = nullptr;   // eval_jvp (reference operation order)
     hipFunction_t vjp_rgb = nullptr, vjp_spec = nullptr, grad_reduce = nullptr;   // eval_vjp
+    hipFunction_t latlong_tables = nullptr;                                     // bake_latlong
     int cu_count = 256;
 };
 
@@ -137,6 +138,7 @@ DeviceModule* module_for_device(int dev) {
     hip_check(hipModuleGetFunction(&m->vjp_rgb, m->module, "sunsky_eval_vjp_rgb"), "sunsky_eval_vjp_rgb");
     hip_check(hipModuleGetFunction(&m->vjp_spec, m->module, "sunsky_eval_vjp_spec"), "sunsky_eval_vjp_spec");
     hip_check(hipModuleGetFunction(&m->grad_reduce, m->module, "sunsky_grad_reduce"), "sunsky_grad_reduce");
+    hip_check(hipModuleGetFunction(&m->latlong_tables, m->module, "sunsky_latlong_tables"), "sunsky_latlong_tables");
     hip_check(hipDeviceGetAttribute(&m->cu_count, hipDeviceAttributeMultiprocessorCount, dev),
               "hipDeviceGetAttribute");
     DeviceModule* raw = m.release();
@@ -189,6 +191,7 @@ struct LambdaSet {   // mirrors the kernel-side struct
 struct LatLong {     // mirrors the kernel-side struct
     int w, h;
     float theta0, dtheta, phi0, dphi;
+    const float* tab;
 };
 
 // normalized_wavelengths / floor2int / lerp factor of eval, sunsky.cpp:326-332
@@ -225,6 +228,8 @@ struct sunsky_emitter {
     mutable float* d_vjp = nullptr;   // eval_vjp basis-tangent tables
     mutable float* d_partials = nullptr;   // eval_vjp per-workgroup gradient partials
     mutable size_t partials_cap = 0;
+    mutable float* d_bake = nullptr;       // bake_latlong angle tables
+    mutable size_t bake_cap = 0;
 
     void upload() {
         int cur = 0;
@@ -256,6 +261,7 @@ struct sunsky_emitter {
         if (d_jvp) (void)hipFree(d_jvp);
         if (d_vjp) (void)hipFree(d_vjp);
         if (d_partials) (void)hipFree(d_partials);
+        if (d_bake) (void)hipFree(d_bake);
     }
 };
 
@@ -698,6 +704,7 @@ int sunsky_bake_latlong(const sunsky_emitter* e, int width, int height, float th
                         float phi1, const float* lam_host, int m, float* out, size_t ostride, void* stream) {
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     if (width < 1 || height < 1) return fail(SUNSKY_ERROR_INVALID_VALUE, "image size must be >= 1 x 1");
+    if ((int64_t)width * height >= (int64_t)1 << 31) return fail(SUNSKY_ERROR_INVALID_VALUE, "image larger than 2^31 pixels");
     const bool spec = e->kargs.variant == kSpectral;
     if (spec && (!lam_host || m < 1 || m > kMaxBroadcastLambda))
         return fail(SUNSKY_ERROR_INVALID_VALUE, "1..32 wavelengths required for a spectral bake");
@@ -707,13 +714,30 @@ int sunsky_bake_latlong(const sunsky_emitter* e, int width, int height, float th
     if (ostride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "out_stride < width * height");
     // dr::linspace(start, end, count): step = (end - start) / (count - 1) in fp32
     LatLong G = {width, height, theta0, height > 1 ? (theta1 - theta0) / (float)(height - 1) : 0.f,
-                 phi0, width > 1 ? (phi1 - phi0) / (float)(width - 1) : 0.f};
+                 phi0, width > 1 ? (phi1 - phi0) / (float)(width - 1) : 0.f, nullptr};
     return guarded([&] {
+        if (!e->mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
         SunskyKArgs K = e->kargs;
         hipStream_t s = (hipStream_t)stream;
+        const size_t need = 2 * (size_t)width + 2 * (size_t)height;
+        if (e->bake_cap < need) {
+            // the tables of a previous bake may still be in use
+            hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+            if (e->d_bake) hip_check(hipFree(e->d_bake), "hipFree");
+            e->d_bake = nullptr;
+            hip_check(hipMalloc(&e->d_bake, sizeof(float) * need), "hipMalloc");
+            e->bake_cap = need;
+        }
+        float* tab = e->d_bake;
+        G.tab = tab;
+        {
+            void* targs[] = {&G, &tab};
+            const unsigned tg = (unsigned)((std::max(width, height) + kBlock - 1) / kBlock);
+            launch(e->mod->latlong_tables, tg, s, targs);
+        }
         if (!spec) {
             void* args[] = {&K, &G, &out, &ostride};
-            launch(e->fn(K_BAKE_RGB), grid_for(e->mod, K_BAKE_RGB, (n + 3) / 4), s, args);
+            launch(e->fn(K_BAKE_RGB), grid_for(e->mod, K_BAKE_RGB, (size_t)((width + 3) / 4) * height), s, args);
         } else {
             LambdaSet L = make_lambda_set(lam_host, m);
             void* args[] = {&K, &G, &L, &out, &ostride};

@@ -921,40 +921,65 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
 // holds eval(si.wi = -d).  Directions are generated in-kernel: the bake only
 // writes HBM (12 B per RGB pixel).  Planes [c][H * W], row-major.
 // ======================================================================
-struct LatLong { int w, h; float theta0, dtheta, phi0, dphi; };
+// The sines and cosines of the W column and H row angles are tabulated once per
+// bake by sunsky_latlong_tables (tab = [cos phi (W), sin phi (W), sin theta (H),
+// cos theta (H)]); each pixel then reads 4 L2-resident table entries instead of
+// two sincosf.
+struct LatLong { int w, h; float theta0, dtheta, phi0, dphi; const float* tab; };
 
 __device__ __forceinline__ float3_ latlong_dir(const LatLong& G, size_t i) {
-    const int x = (int)(i % (size_t)G.w), y = (int)(i / (size_t)G.w);
-    const float theta = fmaf((float)y, G.dtheta, G.theta0), phi = fmaf((float)x, G.dphi, G.phi0);
-    float st, ct, sp, cp;
-    sincosf(theta, &st, &ct);
-    sincosf(phi, &sp, &cp);
+    const unsigned y = (unsigned)i / (unsigned)G.w, x = (unsigned)i - y * (unsigned)G.w;   // W * H < 2^31
+    const float cp = G.tab[x], sp = G.tab[G.w + x], st = G.tab[2 * G.w + y], ct = G.tab[2 * G.w + G.h + y];
     return mk3(cp * st, sp * st, ct);
 }
 
+extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_latlong_tables(LatLong G, float* tab) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < G.w) {
+        float sp, cp;
+        sincosf(fmaf((float)i, G.dphi, G.phi0), &sp, &cp);
+        tab[i] = cp;
+        tab[G.w + i] = sp;
+    }
+    if (i < G.h) {
+        float st, ct;
+        sincosf(fmaf((float)i, G.dtheta, G.theta0), &st, &ct);
+        tab[2 * G.w + i] = st;
+        tab[2 * G.w + G.h + i] = ct;
+    }
+}
+
+// One lane = 4 consecutive pixels of one row: (row, column group) from one 32-bit
+// division per group; 16-byte stores when the row width is a multiple of 4.
 template <bool FAST>
 __device__ __forceinline__ void bake_rgb_body(const SunskyKArgs& K, LatLong G, float* __restrict__ out,
                                               size_t ostride) {
-    const size_t n = (size_t)G.w * G.h, ngroups = (n + 3) / 4;
-    const bool vec_ok = ((uintptr_t)out & 15u) == 0 && (ostride & 3u) == 0;
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < ngroups; v += stride) {
-        const size_t i0 = v * 4;
+    const unsigned gpr = ((unsigned)G.w + 3u) / 4u, ngroups = gpr * (unsigned)G.h;
+    const bool vec_ok = ((uintptr_t)out & 15u) == 0 && (ostride & 3u) == 0 && (G.w & 3) == 0;
+    const unsigned stride = gridDim.x * blockDim.x;
+    for (unsigned v = blockIdx.x * blockDim.x + threadIdx.x; v < ngroups; v += stride) {
+        const unsigned y = v / gpr, x0 = (v - y * gpr) * 4u;
+        const float st = G.tab[2 * G.w + y], ct = G.tab[2 * G.w + G.h + y];
+        const size_t i0 = (size_t)y * (unsigned)G.w + x0;
         float r[4] = {0, 0, 0, 0}, g[4] = {0, 0, 0, 0}, b[4] = {0, 0, 0, 0};
+        // rows below the horizon are 0 (eval's cos_theta >= 0 mask) without evaluating
+        // them when no to_world rotation maps them back up
+        const bool below = K.identity_xform && ct < 0.f;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (i0 + j >= n) break;
-            float3_ d = latlong_dir(G, i0 + j);
+            if (below) break;
+            const unsigned x = x0 + j < (unsigned)G.w ? x0 + j : (unsigned)G.w - 1;
+            float3_ d = mk3(G.tab[x] * st, G.tab[G.w + x] * st, ct);
             float o[3];
             eval_rgb_local<FAST>(K, K.sun_table, to_local(K, d), true, o);
             r[j] = o[0]; g[j] = o[1]; b[j] = o[2];
         }
-        if (vec_ok && i0 + 4 <= n) {
+        if (vec_ok) {
             store_vec<4>(out, i0, r);
             store_vec<4>(out + ostride, i0, g);
             store_vec<4>(out + 2 * ostride, i0, b);
         } else {
-            for (int j = 0; j < 4 && i0 + j < n; ++j) {
+            for (unsigned j = 0; j < 4 && x0 + j < (unsigned)G.w; ++j) {
                 out[i0 + j] = r[j];
                 out[ostride + i0 + j] = g[j];
                 out[2 * ostride + i0 + j] = b[j];

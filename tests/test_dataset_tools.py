@@ -49,3 +49,18 @@ def test_pack_tgmm_entry_layout():
     # weights of each (turbidity, elevation) mixture are positive, sigmas positive,
     # mean zenith angles within [0, pi/2] (mk_sampling_dataset.py's pi/2 - elevation)
     assert np.all(t[..., 4] > 0) and np.all(t[..., 2:4] > 0)
+
+
+HW_DIR = os.path.join(REF, "include/mitsuba/render/sunsky")
+
+
+@pytest.mark.skipif(not os.path.isdir(HW_DIR), reason="Hosek-Wilkie data headers not present (GPU box)")
+def test_datasets_regenerated_from_hosek_wilkie_headers_are_bit_exact(tmp_path):
+    """tools/mk_hw_datasets.py restates sunsky.h:600-932; its output must be the shipped files
+    byte for byte, and the pack's entries must hold the same numbers."""
+    from mk_hw_datasets import generate
+    names = generate(HW_DIR, str(tmp_path))
+    assert len(names) == 6
+    for name in names:
+        assert (tmp_path / name).read_bytes() == open(os.path.join(REF, "resources/sunsky/datasets", name), "rb").read()
+        np.testing.assert_array_equal(ss.array_from_file(tmp_path / name), read_pack_entry(name[:-4]))

@@ -163,10 +163,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # One rank per GPU over RCCL ("nccl").  More ranks than GPUs (a multi-rank rehearsal
+    # on a 1-GPU box) share the GPUs and synchronise over gloo with CPU tensors.
+    ndev = max(1, torch.cuda.device_count())
+    rehearsal = world > ndev
+    backend = "gloo" if rehearsal else os.environ.get("SUNSKY_BENCH_BACKEND", "nccl")
+    torch.cuda.set_device(local % ndev)
+    dev = torch.device("cuda", local % ndev)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     n = args.n
     wi = -hemisphere_dirs(n, seed=1234 + rank, device=dev)     # si.wi = -wo
@@ -205,7 +214,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kernel_ms = timer.mean_ms()
@@ -225,7 +234,8 @@ def main():
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "RGB eval(): 16,777,216 uniform upper-hemisphere dirs per GPU x turbidity {2,6,10}",
                        "dirs_per_gpu": n, "turbidity": list(TURBIDITIES), "sun_elevation_deg": 45,
-                       "albedo": 0.1, "precision": args.precision, "parallelism": f"shard{world}"},
+                       "albedo": 0.1, "precision": args.precision, "parallelism": f"shard{world}",
+                       **({"rehearsal": f"{world} ranks on {ndev} GPU(s), gloo"} if rehearsal else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "traffic": traffic, "traffic_source": traffic_src,
@@ -354,13 +364,13 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        full = gather_radiance(outs[0], n * world)
+        full = gather_radiance(outs[0].to(coll_dev), n * world)
         torch.cuda.synchronize()
         gt = time.perf_counter() - t0
         if rank == 0:
             nbytes = outs[0].numel() * 4 * (world - 1)
             result["gather"] = {"seconds": gt, "bytes_to_root": nbytes, "GBps": nbytes / gt / 1e9,
-                                "bitwise_own_shard": bool(torch.equal(full[:, :n], outs[0]))}
+                                "bitwise_own_shard": bool(torch.equal(full[:, :n].to(dev), outs[0]))}
         del full
 
     if rank == 0:

@@ -305,6 +305,30 @@ def main():
                                    "achieved_GBps": BYTES_SPEC_PER_DIR * n / (ms * 1e-3) / 1e9,
                                    "unit": "(dir x lambda) evals/s"}
         del spec_out
+        # Mitsuba's spectral variants: 4 wavelengths per ray (Spectrum<Float, 4>), per-ray lambda
+        lam4 = 360.0 + 360.0 * torch.rand((4, n), generator=torch.Generator(device=dev).manual_seed(5 + rank),
+                                          device=dev)
+        rays_out = torch.empty((4, n), dtype=torch.float32, device=dev)
+
+        def rays_step():
+            rc = lib.sunsky_eval(spec._h, vin, lam4.data_ptr(), 4, n, None, n, rays_out.data_ptr(), n, stream)
+            if rc:
+                raise RuntimeError(lib.sunsky_last_error().decode())
+
+        for _ in range(2):
+            rays_step()
+        tm = KernelTimer()
+        reps = max(3, args.steps // 4)
+        tm.begin()
+        for _ in range(reps):
+            rays_step()
+        tm.end(reps)
+        ms = tm.mean_ms()
+        sec["spectral_eval_per_ray_4lambda"] = {"evals_per_s": 4 * n / (ms * 1e-3), "kernel_ms": ms,
+                                                "achieved_GBps": (12 + 16 + 16) * n / (ms * 1e-3) / 1e9,
+                                                "note": "16M rays x 4 random wavelengths in [360, 720] nm "
+                                                        "(reads wi + lambda, writes 4 radiances)"}
+        del lam4, rays_out
         # C4: sample_direction + pdf_direction, 64M samples (per GPU)
         ns = 4 * n
         smp = ss.SunskyEmitter(dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), "rgb", precision=args.precision,

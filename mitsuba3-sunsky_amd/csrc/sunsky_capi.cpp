@@ -98,12 +98,12 @@ std::string code_object_path() {
 // carries only its own tables and registers.
 enum KernelId {
     K_EVAL_RGB_V4, K_EVAL_RGB_V1, K_EVAL_SPEC_BCAST_V4, K_EVAL_SPEC_BCAST_V1, K_EVAL_SPEC_NODES_V4,
-    K_EVAL_SPEC_RAYS, K_SAMPLE_DIRECTION_RGB, K_SAMPLE_DIRECTION_SPEC, K_PDF_DIRECTION, K_SAMPLE_WAVELENGTHS_RGB,
+    K_EVAL_SPEC_RAYS_V4, K_EVAL_SPEC_RAYS_V1, K_SAMPLE_DIRECTION_RGB, K_SAMPLE_DIRECTION_SPEC, K_PDF_DIRECTION, K_SAMPLE_WAVELENGTHS_RGB,
     K_SAMPLE_WAVELENGTHS_SPEC, K_SAMPLE_RAY_RGB, K_SAMPLE_RAY_SPEC, K_BAKE_RGB, K_BAKE_SPEC, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
-    "sunsky_eval_spec_nodes_v4", "sunsky_eval_spec_rays", "sunsky_sample_direction_rgb",
+    "sunsky_eval_spec_nodes_v4", "sunsky_eval_spec_rays_v4", "sunsky_eval_spec_rays_v1", "sunsky_sample_direction_rgb",
     "sunsky_sample_direction_spec", "sunsky_pdf_direction", "sunsky_sample_wavelengths_rgb",
     "sunsky_sample_wavelengths_spec", "sunsky_sample_ray_rgb", "sunsky_sample_ray_spec",
     "sunsky_bake_latlong_rgb", "sunsky_bake_latlong_spec"};
@@ -165,6 +165,7 @@ int blocks_per_cu(KernelId k) {
         case K_EVAL_SPEC_BCAST_V4: case K_EVAL_SPEC_BCAST_V1: case K_EVAL_SPEC_NODES_V4: return 64;
         case K_SAMPLE_DIRECTION_RGB: case K_SAMPLE_DIRECTION_SPEC: case K_PDF_DIRECTION: return 64;
         case K_BAKE_RGB: case K_BAKE_SPEC: return 64;
+        case K_EVAL_SPEC_RAYS_V4: case K_EVAL_SPEC_RAYS_V1: return 64;
         default: return 16;
     }
 }
@@ -467,10 +468,25 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
                 launch(e->fn(K_EVAL_RGB_V1), grid_for(e->mod, K_EVAL_RGB_V1, rem), s, args);
             }
         } else {
-            const float *x = w.x, *y = w.y, *z = w.z;
+            // VEC = 4 over rays when every plane is 16-byte aligned; VEC = 1 tail
+            bool vec = n >= 4 && aligned16(w.x) && aligned16(w.y) && aligned16(w.z) && aligned16(out) &&
+                       aligned16(lam) && (ostride % 4) == 0 && (nlam == 1 || (lstride % 4) == 0) &&
+                       (!active || ((uintptr_t)active & 3u) == 0);
+            size_t n4 = vec ? (n & ~(size_t)3) : 0;
             int nl = nlam;
-            void* args[] = {&K, &x, &y, &z, &lam, &lstride, &nl, &active, &n, &out, &ostride, &sign};
-            launch(e->fn(K_EVAL_SPEC_RAYS), grid_for(e->mod, K_EVAL_SPEC_RAYS, n), s, args);
+            if (n4) {
+                const float *x = w.x, *y = w.y, *z = w.z;
+                void* args[] = {&K, &x, &y, &z, &lam, &lstride, &nl, &active, &n4, &out, &ostride, &sign};
+                launch(e->fn(K_EVAL_SPEC_RAYS_V4), grid_for(e->mod, K_EVAL_SPEC_RAYS_V4, n4 / 4), s, args);
+            }
+            if (n4 < n) {
+                const float *x = w.x + n4, *y = w.y + n4, *z = w.z + n4, *l = lam + n4;
+                const uint8_t* a = active ? active + n4 : nullptr;
+                float* o = out + n4;
+                size_t rem = n - n4;
+                void* args[] = {&K, &x, &y, &z, &l, &lstride, &nl, &a, &rem, &o, &ostride, &sign};
+                launch(e->fn(K_EVAL_SPEC_RAYS_V1), grid_for(e->mod, K_EVAL_SPEC_RAYS_V1, rem), s, args);
+            }
         }
     });
 }
@@ -627,7 +643,7 @@ int sunsky_eval_jvp(const sunsky_emitter* e, int param, const float* tangent, in
         } else {
             int nl = nlam;
             void* args[] = {&K, &jvp, &x, &y, &z, &lam, &lstride, &nl, &active, &n, &out, &d_out, &ostride, &sign};
-            launch(e->mod->jvp_spec, grid_for(e->mod, K_EVAL_SPEC_RAYS, n), (hipStream_t)stream, args);
+            launch(e->mod->jvp_spec, grid_for(e->mod, K_EVAL_SPEC_RAYS_V1, n), (hipStream_t)stream, args);
         }
     });
 }
@@ -667,7 +683,7 @@ int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam
                 std::memcpy(buf.data() + (2 + k) * blk, tS.dsky.data(), sizeof(float) * tS.dsky.size());
                 std::memcpy(buf.data() + 5 * blk + 3 * k, tS.dsun_local, 3 * sizeof(float));
             }
-        const KernelId kid = spec ? K_EVAL_SPEC_RAYS : K_EVAL_RGB_V1;
+        const KernelId kid = spec ? K_EVAL_SPEC_RAYS_V1 : K_EVAL_RGB_V1;
         const unsigned grid = grid_for(e->mod, kid, n);
         if (!e->d_vjp) hip_check(hipMalloc(&e->d_vjp, sizeof(float) * buf.size()), "hipMalloc");
         // a previous eval_vjp of this emitter may still read the tables / partials

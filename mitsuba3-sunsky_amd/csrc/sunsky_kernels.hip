@@ -486,7 +486,7 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
 // eval(): spectral with per-ray wavelengths (Mitsuba Spectrum<Float, k>):
 // lambda plane k at lam + k * lstride, out plane k at out + k * ostride.
 // ======================================================================
-template <bool FAST>
+template <int VEC, bool FAST>
 __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                                     const float* __restrict__ wy, const float* __restrict__ wz,
                                                     const float* __restrict__ lam, size_t lstride, int nlam,
@@ -495,14 +495,40 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
     __shared__ ChanLds<FAST> S;
     const auto* chans = stage_chans<FAST>(K, &S);
     __syncthreads();
+    const size_t nvec = n / VEC;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        bool m = active ? active[i] != 0 : true;
-        DirTerms t = dir_terms<FAST>(K, to_local(K, mk3(sign * wx[i], sign * wy[i], sign * wz[i])), m);
-        add_sun_terms<FAST>(K, t);
-        for (int k = 0; k < nlam; ++k)
-            __builtin_nontemporal_store(eval_spec_one<FAST>(K, chans, K.sun_table, K.sun_ld, t, lam[(size_t)k * lstride + i]),
-                                        out + (size_t)k * ostride + i);
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+        const size_t i = v * VEC;
+        float x[VEC], y[VEC], z[VEC];
+        bool m[VEC];
+        load_dirs<VEC>(wx, wy, wz, active, i, x, y, z, m);
+        // wavelengths in chunks of 4 planes (Mitsuba's Spectrum<Float, 4> is one chunk):
+        // every load of a chunk is issued before its first use
+        float l4[4][VEC];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < nlam) load_vec<VEC>(lam + (size_t)k * lstride, i, l4[k]);
+        DirTerms t[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            t[j] = dir_terms<FAST>(K, to_local(K, mk3(sign * x[j], sign * y[j], sign * z[j])), m[j]);
+            add_sun_terms<FAST>(K, t[j]);
+        }
+        for (int k0 = 0; k0 < nlam; k0 += 4) {
+            if (k0 > 0) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k0 + k < nlam) load_vec<VEC>(lam + (size_t)(k0 + k) * lstride, i, l4[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k0 + k >= nlam) break;
+                float o[VEC];
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) o[j] = eval_spec_one<FAST>(K, chans, K.sun_table, K.sun_ld, t[j], l4[k][j]);
+                store_vec<VEC>(out + (size_t)(k0 + k) * ostride, i, o);
+            }
+        }
     }
 }
 
@@ -1421,14 +1447,16 @@ SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v1_ref, 1, false)
 SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v4_fast, 4, true)
 SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v4_ref, 4, false)
 
-#define SS_EVAL_SPEC_RAYS(NAME, FAST)                                                                         \
+#define SS_EVAL_SPEC_RAYS(NAME, VEC, FAST)                                                                    \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
         SunskyKArgs K, const float* wx, const float* wy, const float* wz, const float* lam, size_t lstride,    \
         int nlam, const uint8_t* active, size_t n, float* out, size_t ostride, float sign) {                   \
-        eval_spec_rays_body<FAST>(K, wx, wy, wz, lam, lstride, nlam, active, n, out, ostride, sign);           \
+        eval_spec_rays_body<VEC, FAST>(K, wx, wy, wz, lam, lstride, nlam, active, n, out, ostride, sign);      \
     }
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_fast, true)
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_ref, false)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_fast, 4, true)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_fast, 1, true)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_ref, 4, false)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_ref, 1, false)
 
 #define SS_SAMPLE_DIRECTION(NAME, FAST, SPEC)                                                                 \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \

@@ -98,13 +98,14 @@ std::string code_object_path() {
 // carries only its own tables and registers.
 enum KernelId {
     K_EVAL_RGB_V4, K_EVAL_RGB_V1, K_EVAL_SPEC_BCAST_V4, K_EVAL_SPEC_BCAST_V1, K_EVAL_SPEC_NODES_V4,
-    K_EVAL_SPEC_RAYS_V4, K_EVAL_SPEC_RAYS_V1, K_SAMPLE_DIRECTION_RGB, K_SAMPLE_DIRECTION_SPEC, K_PDF_DIRECTION, K_SAMPLE_WAVELENGTHS_RGB,
+    K_EVAL_SPEC_RAYS_V4, K_EVAL_SPEC_RAYS_V1, K_SAMPLE_DIRECTION_RGB, K_SAMPLE_DIRECTION_SPEC, K_PDF_DIRECTION_V4, K_PDF_DIRECTION_V1, K_SAMPLE_WAVELENGTHS_RGB,
     K_SAMPLE_WAVELENGTHS_SPEC, K_SAMPLE_RAY_RGB, K_SAMPLE_RAY_SPEC, K_BAKE_RGB, K_BAKE_SPEC, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
     "sunsky_eval_spec_nodes_v4", "sunsky_eval_spec_rays_v4", "sunsky_eval_spec_rays_v1", "sunsky_sample_direction_rgb",
-    "sunsky_sample_direction_spec", "sunsky_pdf_direction", "sunsky_sample_wavelengths_rgb",
+    "sunsky_sample_direction_spec", "sunsky_pdf_direction_v4", "sunsky_pdf_direction_v1",
+    "sunsky_sample_wavelengths_rgb",
     "sunsky_sample_wavelengths_spec", "sunsky_sample_ray_rgb", "sunsky_sample_ray_spec",
     "sunsky_bake_latlong_rgb", "sunsky_bake_latlong_spec"};
 
@@ -163,7 +164,8 @@ int blocks_per_cu(KernelId k) {
     switch (k) {
         case K_EVAL_RGB_V4: case K_EVAL_RGB_V1: return 64;
         case K_EVAL_SPEC_BCAST_V4: case K_EVAL_SPEC_BCAST_V1: case K_EVAL_SPEC_NODES_V4: return 64;
-        case K_SAMPLE_DIRECTION_RGB: case K_SAMPLE_DIRECTION_SPEC: case K_PDF_DIRECTION: return 64;
+        case K_SAMPLE_DIRECTION_RGB: case K_SAMPLE_DIRECTION_SPEC: case K_PDF_DIRECTION_V4: case K_PDF_DIRECTION_V1:
+            return 64;
         case K_BAKE_RGB: case K_BAKE_SPEC: return 64;
         case K_EVAL_SPEC_RAYS_V4: case K_EVAL_SPEC_RAYS_V1: return 64;
         default: return 16;
@@ -570,8 +572,22 @@ int sunsky_pdf_direction(const sunsky_emitter* e, sunsky_vec3_in d, const uint8_
     if (!d.x || !d.y || !d.z || !pdf) return fail(SUNSKY_ERROR_INVALID_VALUE, "null direction / output pointer");
     return guarded([&] {
         SunskyKArgs K = e->kargs;
-        void* args[] = {&K, (void*)&d.x, (void*)&d.y, (void*)&d.z, &active, &n, &pdf};
-        launch(e->fn(K_PDF_DIRECTION), grid_for(e->mod, K_PDF_DIRECTION, n), (hipStream_t)stream, args);
+        hipStream_t s = (hipStream_t)stream;
+        bool vec = n >= 4 && aligned16(d.x) && aligned16(d.y) && aligned16(d.z) && aligned16(pdf) &&
+                   (!active || ((uintptr_t)active & 3u) == 0);
+        size_t n4 = vec ? (n & ~(size_t)3) : 0;
+        if (n4) {
+            void* args[] = {&K, (void*)&d.x, (void*)&d.y, (void*)&d.z, &active, &n4, &pdf};
+            launch(e->fn(K_PDF_DIRECTION_V4), grid_for(e->mod, K_PDF_DIRECTION_V4, n4 / 4), s, args);
+        }
+        if (n4 < n) {
+            const float *x = d.x + n4, *y = d.y + n4, *z = d.z + n4;
+            const uint8_t* a = active ? active + n4 : nullptr;
+            float* p = pdf + n4;
+            size_t rem = n - n4;
+            void* args[] = {&K, &x, &y, &z, &a, &rem, &p};
+            launch(e->fn(K_PDF_DIRECTION_V1), grid_for(e->mod, K_PDF_DIRECTION_V1, rem), s, args);
+        }
     });
 }
 

@@ -539,10 +539,13 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
 // terms: tg = {mu_phi, mu_theta, c / sigma_phi, c / sigma_theta} with
 // c = sqrt(log2(e) / 2), tc = weight / (volume * 2 pi), so that a gaussian
 // costs exp2(-(sx^2 + sy^2)) and one fma.
+// tg/tc/tref hold only the K.tgmm_count gaussians with a non-zero coefficient
+// (SunskyKArgs::tgmm_idx), so tgmm_pdf loops over those.
 struct TgmmLds {
-    Gaussian gauss[kNbMixture];
+    Gaussian gauss[kNbMixture];                  // full mixture: sample_sky
     float4 tg[kNbMixture];
     float tc[kNbMixture];
+    Gaussian tref[kNbMixture];                   // compacted, reference-order tgmm_pdf
     float cdf[kNbMixture], pmf[kNbMixture];
 };
 
@@ -551,11 +554,12 @@ __device__ __forceinline__ void stage_tgmm(const SunskyKArgs& K, TgmmLds* s) {
     lds_copy(s->cdf, K.gauss_cdf, kNbMixture);
     lds_copy(s->pmf, K.gauss_pmf, kNbMixture);
     const int i = threadIdx.x;
-    if (i < kNbMixture) {
+    if (i < K.tgmm_count) {
         const float c = 0.84932180028801904272f;   // sqrt(log2(e) / 2)
-        const Gaussian& g = K.gauss[i];
+        const Gaussian& g = K.gauss[K.tgmm_idx[i]];
         s->tg[i] = make_float4(g.mu_phi, g.mu_theta, g.inv_sigma_phi * c, g.inv_sigma_theta * c);
         s->tc[i] = g.coef * kInvTwoPi;
+        s->tref[i] = g;
     }
 }
 
@@ -676,15 +680,15 @@ __device__ __forceinline__ float tgmm_pdf(const SunskyKArgs& K, const TgmmLds& T
     // the ray loop into ~100 VGPRs.
     if constexpr (FAST) {
 #pragma unroll 4
-        for (int i = 0; i < kNbMixture; ++i) {
+        for (int i = 0; i < K.tgmm_count; ++i) {
             const float4 a = T.tg[i];
             float sx = (phi - a.x) * a.z, sy = (theta - a.y) * a.w;
             pdf = fmaf(T.tc[i], fast_exp2(-fmaf(sy, sy, sx * sx)), pdf);
         }
     } else {
 #pragma unroll 4
-        for (int i = 0; i < kNbMixture; ++i) {
-            const Gaussian& g = T.gauss[i];
+        for (int i = 0; i < K.tgmm_count; ++i) {
+            const Gaussian& g = T.tref[i];
             float sx = (phi - g.mu_phi) * g.inv_sigma_phi, sy = (theta - g.mu_theta) * g.inv_sigma_theta;
             float q = fmaf(sy, sy, sx * sx);
             pdf = fmaf(g.coef, kInvTwoPi * expf(-0.5f * q), pdf);
@@ -825,8 +829,9 @@ __device__ __forceinline__ void sample_direction_body(
     }
 }
 
-// pdf_direction, sunsky.cpp:443-451
-template <bool FAST>
+// pdf_direction, sunsky.cpp:443-451.  VEC directions per lane: each gaussian's
+// LDS-broadcast parameters are read once for VEC directions; 16-byte loads/stores.
+template <int VEC, bool FAST>
 __device__ __forceinline__ void pdf_direction_body(const SunskyKArgs& K, const float* __restrict__ dx,
                                                    const float* __restrict__ dy, const float* __restrict__ dz,
                                                    const uint8_t* __restrict__ active, size_t n,
@@ -834,14 +839,61 @@ __device__ __forceinline__ void pdf_direction_body(const SunskyKArgs& K, const f
     __shared__ TgmmLds T;
     stage_tgmm(K, &T);
     __syncthreads();
+    const float3_ sn = mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]);
+    const size_t nvec = n / VEC;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        bool act = active ? active[i] != 0 : true;
-        float3_ l = to_local(K, mk3(dx[i], dy[i], dz[i]));
-        float skyp, sunp;
-        compute_pdfs<FAST>(K, T, l, true, true, &skyp, &sunp);
-        float pd = lerpf_(sunp, skyp, K.w_sky);
-        __builtin_nontemporal_store(act ? pd : 0.f, pdf + i);
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+        const size_t i = v * VEC;
+        float x[VEC], y[VEC], z[VEC];
+        bool m[VEC];
+        load_dirs<VEC>(dx, dy, dz, active, i, x, y, z, m);
+        // compute_pdfs (sunsky.cpp:711-723) per direction, tgmm_pdf (:732-763) vectorised
+        float phi[VEC], theta[VEC], sin_theta[VEC], sunp[VEC], acc[VEC];
+        bool ok[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            float3_ d = to_local(K, mk3(x[j], y[j], z[j]));
+            float st = safe_sqrtf_(fmaf(d.x, d.x, d.y * d.y));
+            bool a = (d.z >= 0.f) && (st != 0.f);
+            sin_theta[j] = fmaxf(st, kEpsilon);
+            float ph = atan2f(d.y, d.x) - (K.sun_phi - 0.5f * kPi);
+            ph = ph < 0.f ? ph + kTwoPi : ph;
+            phi[j] = ph > kTwoPi ? ph - kTwoPi : ph;
+            theta[j] = unit_angle_z(d);
+            ok[j] = a && (theta[j] >= 0.f) && (theta[j] <= 0.5f * kPi);
+            sunp[j] = dot3(sn, d) >= K.cos_cutoff ? K.sun_pdf : 0.f;
+            acc[j] = 0.f;
+        }
+        if constexpr (FAST) {
+#pragma unroll 2
+            for (int g = 0; g < K.tgmm_count; ++g) {
+                const float4 a = T.tg[g];
+                const float c = T.tc[g];
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) {
+                    float sx = (phi[j] - a.x) * a.z, sy = (theta[j] - a.y) * a.w;
+                    acc[j] = fmaf(c, fast_exp2(-fmaf(sy, sy, sx * sx)), acc[j]);
+                }
+            }
+        } else {
+#pragma unroll 2
+            for (int g = 0; g < K.tgmm_count; ++g) {
+                const Gaussian& G = T.tref[g];
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) {
+                    float sx = (phi[j] - G.mu_phi) * G.inv_sigma_phi, sy = (theta[j] - G.mu_theta) * G.inv_sigma_theta;
+                    float q = fmaf(sy, sy, sx * sx);
+                    acc[j] = fmaf(G.coef, kInvTwoPi * expf(-0.5f * q), acc[j]);
+                }
+            }
+        }
+        float pd[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            float skyp = fdiv<FAST>(ok[j] ? acc[j] : 0.f, sin_theta[j]);
+            pd[j] = m[j] ? lerpf_(sunp[j], skyp, K.w_sky) : 0.f;
+        }
+        store_vec<VEC>(pdf, i, pd);
     }
 }
 
@@ -1471,14 +1523,16 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_ref, false, false)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_fast, true, true)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_ref, false, true)
 
-#define SS_PDF_DIRECTION(NAME, FAST)                                                                          \
+#define SS_PDF_DIRECTION(NAME, VEC, FAST)                                                                     \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
         SunskyKArgs K, const float* dx, const float* dy, const float* dz, const uint8_t* active, size_t n,     \
         float* pdf) {                                                                                          \
-        pdf_direction_body<FAST>(K, dx, dy, dz, active, n, pdf);                                               \
+        pdf_direction_body<VEC, FAST>(K, dx, dy, dz, active, n, pdf);                                          \
     }
-SS_PDF_DIRECTION(sunsky_pdf_direction_fast, true)
-SS_PDF_DIRECTION(sunsky_pdf_direction_ref, false)
+SS_PDF_DIRECTION(sunsky_pdf_direction_v4_fast, 4, true)
+SS_PDF_DIRECTION(sunsky_pdf_direction_v1_fast, 1, true)
+SS_PDF_DIRECTION(sunsky_pdf_direction_v4_ref, 4, false)
+SS_PDF_DIRECTION(sunsky_pdf_direction_v1_ref, 1, false)
 
 #define SS_SAMPLE_WAVELENGTHS(NAME, FAST, SPEC)                                                               \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \

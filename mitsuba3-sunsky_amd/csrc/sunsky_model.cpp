@@ -472,6 +472,9 @@ void SunskyModel::stage() {
             G.coef = r[4] / volume;
             k_.gauss_pmf[g] = r[4];
         }
+        k_.tgmm_count = 0;
+        for (int g = 0; g < kNbMixture; ++g)
+            if (k_.gauss[g].coef != 0.f) k_.tgmm_idx[k_.tgmm_count++] = (uint8_t)g;
         // DiscreteDistribution(mis_weights): JIT prefix_sum in fp32 (distr_1d.h:218-231),
         // scalar accumulation in fp64 + first/last nonzero bounds (:233-265)
         bool any_pos = false;

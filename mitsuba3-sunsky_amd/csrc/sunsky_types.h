@@ -105,6 +105,10 @@ struct SunskyKArgs {
     float gauss_pmf[kNbMixture];
     float gauss_sum, gauss_norm;
     int   gauss_first, gauss_last; // scalar-variant search bounds (distr_1d.h:233-265)
+    // tgmm_pdf terms with a non-zero coefficient, in mixture order: a gaussian whose
+    // corner weight is 0 (integer turbidity / table-node elevation) adds exactly +0
+    int   tgmm_count;
+    uint8_t tgmm_idx[kNbMixture];
     // -------- wavelength sampling (ContinuousDistribution over [360, 720])
     int   spec_size;               // 10 (JIT) / 2 (scalar) / 0 (RGB)
     float spec_pdf[10], spec_cdf[9];

@@ -130,3 +130,24 @@ def test_reference_bin_directory_equals_bundled_pack():
         assert a.sky_sampling_w == b.sky_sampling_w
     arr = ss.array_from_file(os.path.join(REF_DATASETS, "sky_rgb_rad.bin"))
     assert arr.shape == (10, 2, 6, 3)
+
+
+def test_device_entry_points_refuse_host_only_emitter():
+    """bake / eval_jvp / eval_vjp on an emitter staged without a device fail with a message."""
+    import ctypes
+    lib = ss.lib()
+    em = ss.SunskyEmitter({"type": "sunsky", "sun_direction": [0.3, 0.2, 0.9]}, "rgb", device="host")
+    buf = (ctypes.c_float * 64)()
+    assert lib.sunsky_bake_latlong(em._h, 8, 4, 0.0, 3.14, 0.0, 6.28, None, 0, buf, 32, None) != 0
+    assert b"host-only" in lib.sunsky_last_error()
+    vin = ss._capi.Vec3In(ctypes.addressof(buf), ctypes.addressof(buf), ctypes.addressof(buf))
+    assert lib.sunsky_eval_vjp(em._h, vin, None, 0, 0, None, 4, buf, 4, buf, None) != 0
+    assert b"host-only" in lib.sunsky_last_error()
+    t = (ctypes.c_float * 1)(1.0)
+    assert lib.sunsky_eval_jvp(em._h, 0, t, 1, vin, None, 0, 0, None, 4, buf, buf, 4, None) != 0
+    assert b"host-only" in lib.sunsky_last_error()
+    # argument validation happens before any device work
+    assert lib.sunsky_bake_latlong(em._h, 0, 4, 0.0, 3.14, 0.0, 6.28, None, 0, buf, 32, None) != 0
+    assert b"image size" in lib.sunsky_last_error()
+    assert lib.sunsky_eval_vjp(em._h, vin, None, 0, 0, None, 4, buf, 4, None, None) != 0
+    assert b"gradient" in lib.sunsky_last_error()

@@ -374,3 +374,78 @@ def test_config1_scalar_rgb_grid_at_solar_noon():
     wo = wo.astype(np.float32)
     out = host(em.eval(ss.SurfaceInteraction3f(wi=soa(-wo)))).T
     assert_parity(out, o32.eval(-wo), o64.eval(-wo), sun_mask(o32, wo))
+
+
+# ------------------------------------------------- sampling: transforms, time mode, ray weights
+def _rot_x(a):
+    c, s = np.cos(a), np.sin(a)
+    return np.array([[1, 0, 0, 0], [0, c, -s, 0], [0, s, c, 0], [0, 0, 0, 1]], dtype=np.float32)
+
+
+@pytest.mark.parametrize("mode", ["to_world", "hour"])
+def test_sampling_parity_rotated_and_time_mode(mode):
+    """sample_direction / pdf_direction with a non-identity to_world (the local frame of
+    sunsky.cpp:258-263) and in time/location mode (compute_sun_coordinates)."""
+    if mode == "to_world":
+        d = dict(angles_dict(5.0, 0.3, np.deg2rad(40), 0.2, 1.0, 1.0), to_world=_rot_x(0.4))
+    else:
+        d = hour_dict(4.5, 9.5, 0.2, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, "rgb")
+    o32 = O.Oracle(d, "rgb", "jit", "f32")
+    o32.override_w_sky(em.sky_sampling_w)
+    rng = np.random.default_rng(17)
+    n = 1 << 14
+    u = rng.random((n, 2), dtype=np.float32)
+    ds, w = em.sample_direction(ss.Interaction3f(), soa(u))
+    gd, gp = host(ds.d).T, host(ds.pdf)
+    ref = o32.sample_direction(u)
+    derr = np.abs(gd - ref["d"]).max(axis=1)
+    assert np.quantile(derr, 0.999) < 2e-6 and derr.max() < 1e-4
+    pd = host(em.pdf_direction(ss.Interaction3f(), ds))
+    assert max_rel(pd, o32.pdf_direction(gd)) < 1e-5
+    assert np.all(np.isfinite(host(w)))
+
+
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+def test_sample_ray_weights_parity(variant):
+    """sample_ray weights (eval / pdf with the bounding-sphere area, sunsky.cpp:354-397) at the
+    GPU's own rays: eval of the oracle over pdf_direction x 1/(pi r^2)."""
+    d = angles_dict(4.0, 0.3, np.deg2rad(40), 0.3, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, variant)
+    em.set_scene([-1, -2, -3], [3, 2, 1])
+    info = em.info()
+    o32 = O.Oracle(dict(d, bsphere_center=info["bsphere_center"], bsphere_radius=info["bsphere_radius"]),
+                   variant, "jit", "f32")
+    o64 = O.Oracle(dict(d, bsphere_center=info["bsphere_center"], bsphere_radius=info["bsphere_radius"]),
+                   variant, "jit", "f64")
+    o32.override_w_sky(em.sky_sampling_w)
+    rng = np.random.default_rng(6)
+    n = 1 << 14
+    ws = rng.random(n, dtype=np.float32)
+    s2, s3 = rng.random((n, 2), dtype=np.float32), rng.random((n, 2), dtype=np.float32)
+    ray, w = em.sample_ray(None, torch.from_numpy(ws).cuda(), soa(s2), soa(s3))
+    rd, gw = host(ray.d).T, host(w).T
+    ref = o32.sample_ray(ws, s2, s3)
+    # same rays and, at the GPU's rays, the same weights up to pdf / radiance conditioning
+    assert np.quantile(np.abs(rd - ref["d"]).max(axis=1), 0.999) < 2e-6
+    if variant == "spectral":
+        # weight = eval / (lambda pdf x direction pdf) (sample_wavelengths, sunsky.cpp:463-480): compare
+        # with the oracle's own sample_ray weights on rays that agree to rounding
+        lam = host(ray.wavelengths).T
+        # (the sampled wavelengths themselves differ by up to ~1e-3 nm: ContinuousDistribution's
+        # t = (y0 - sqrt(y0^2 + 2 s (y1 - y0))) / (y0 - y1) cancels when y0 ~ y1)
+        same = np.abs(rd - ref["d"]).max(axis=1) <= 2e-7
+        assert same.mean() > 0.9
+        rel = (np.abs(gw[same] - ref["weight"][same]) / np.maximum(np.abs(ref["weight"][same]), 1e-6)).max(axis=1)
+        assert np.median(rel) < 1e-5 and np.quantile(rel, 0.999) < 1e-3, (np.median(rel), np.quantile(rel, 0.999))
+        return
+    lam = None
+    r = float(info["bsphere_radius"])
+    pdf = o32.pdf_direction(-rd).astype(np.float64) / (np.pi * r * r)
+    e32 = o32.eval(rd, lam.T if lam is not None else None)
+    e64 = o64.eval(rd, lam.T if lam is not None else None)
+    e32, e64 = (e32.T, e64.T) if variant == "spectral" else (e32, e64)
+    inside = (-rd @ info["sun_dir_local"]) >= info["cos_cutoff"]
+    same_formula = (s3[:, 0] < em.sky_sampling_w) | inside   # sun picks skip the cone test (sunsky.cpp:720)
+    g, a, b = gw[same_formula], (e32 / pdf[:, None])[same_formula], (e64 / pdf[:, None])[same_formula]
+    assert_parity(g, a.astype(np.float32), b, inside[same_formula], rtol=2e-5)

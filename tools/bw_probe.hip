@@ -41,6 +41,10 @@ __global__ __launch_bounds__(256) void rw2(const float* x, const float* y, const
     }
 }
 
+// cold: rotate over 4 input batches (805 MB > the 256 MiB Infinity Cache)
+static const float *g_cx[4], *g_cy[4], *g_cz[4];
+static int g_cold = 1;
+
 template <typename F>
 int run(const char* name, F kern, int vec, int K, const float* x, const float* y, const float* z, float* out,
         size_t n, int cu) {
@@ -49,9 +53,12 @@ int run(const char* name, F kern, int vec, int K, const float* x, const float* y
         for (int w = 0; w < 3; ++w) kern<<<grid, 256>>>(x, y, z, out, n);
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-        const int it = 30;
+        const int it = 32;
         CK(hipEventRecord(e0));
-        for (int i = 0; i < it; ++i) kern<<<grid, 256>>>(x, y, z, out, n);
+        for (int i = 0; i < it; ++i) {
+            if (g_cold > 1) { x = g_cx[i % g_cold]; y = g_cy[i % g_cold]; z = g_cz[i % g_cold]; }
+            kern<<<grid, 256>>>(x, y, z, out, n);
+        }
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms;
@@ -70,6 +77,16 @@ int main() {
     CK(hipMalloc(&x, n * 4)); CK(hipMalloc(&y, n * 4)); CK(hipMalloc(&z, n * 4)); CK(hipMalloc(&out, n * 4 * 11));
     CK(hipMemset(x, 0, n * 4)); CK(hipMemset(y, 0, n * 4)); CK(hipMemset(z, 0, n * 4));
     run("rw4_nt", rw4<3, true>, 4, 3, x, y, z, out, n, cu);
+    // the same with 4 rotating input batches (cold inputs)
+    g_cold = 4;
+    for (int c = 0; c < 4; ++c) {
+        float *a, *b, *d;
+        CK(hipMalloc(&a, n * 4)); CK(hipMalloc(&b, n * 4)); CK(hipMalloc(&d, n * 4));
+        CK(hipMemset(a, 0, n * 4)); CK(hipMemset(b, 0, n * 4)); CK(hipMemset(d, 0, n * 4));
+        g_cx[c] = a; g_cy[c] = b; g_cz[c] = d;
+    }
+    run("rw4_nt_cold", rw4<3, true>, 4, 3, x, y, z, out, n, cu);
+    g_cold = 1;
     run("rw4_nt", rw4<11, true>, 4, 11, x, y, z, out, n, cu);
     run("rw4_plain", rw4<11, false>, 4, 11, x, y, z, out, n, cu);
     run("rw2_nt", rw2<11, true>, 2, 11, x, y, z, out, n, cu);

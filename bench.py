@@ -158,6 +158,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather of the radiance to rank 0")
     ap.add_argument("--no-pmc", action="store_true", help="do not read the committed PMC traffic summary")
+    ap.add_argument("--c5", action="store_true",
+                    help="also run configs[4]: spectral 11-lambda eval of --c5-dirs per GPU + gather to rank 0")
+    ap.add_argument("--c5-dirs", type=int, default=1 << 26, help="directions per GPU for --c5 (default 64M)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -396,6 +399,51 @@ def main():
             result["gather"] = {"seconds": gt, "bytes_to_root": nbytes, "GBps": nbytes / gt / 1e9,
                                 "bitwise_own_shard": bool(torch.equal(full[:, :n].to(dev), outs[0]))}
         del full
+
+    # ------------------------------------------- configs[4]: spectral shard + gather
+    if args.c5:
+        from sunsky_amd.sharding import gather_radiance
+        n5 = args.c5_dirs
+        del outs
+        wi5 = -hemisphere_dirs(n5, seed=4321 + rank, device=dev)
+        spec5 = ss.SunskyEmitter(dict(sun_dict(3.0), albedo=0.3), "spectral", precision=args.precision, device=dev)
+        lams = [float(x) for x in range(320, 721, 40)]
+        out5 = torch.empty((11, n5), dtype=torch.float32, device=dev)
+        for _ in range(2):
+            spec5.eval_spectral_broadcast(wi5, lams, out=out5)
+        reps = max(3, args.steps // 10)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            spec5.eval_spectral_broadcast(wi5, lams, out=out5)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        te = (time.perf_counter() - t0) / reps
+        tg, own_ok = 0.0, True
+        if world > 1:
+            t = torch.tensor([te], device=coll_dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            te = float(t.item())
+            dist.barrier()
+            t0 = time.perf_counter()
+            full = gather_radiance(out5.to(coll_dev), n5 * world)
+            torch.cuda.synchronize()
+            tg = time.perf_counter() - t0
+            if rank == 0:
+                own_ok = bool(torch.equal(full[:, :n5].to(dev), out5))
+            del full
+        if rank == 0:
+            nbytes = 11 * n5 * 4 * (world - 1)
+            result["c5_spectral_shard_gather"] = {
+                "dirs_per_gpu": n5, "lambdas": 11, "eval_s": te,
+                "evals_per_s_whole_job": 11 * n5 * world / te,
+                "gather_s": tg, "gather_bytes_to_root": nbytes, "gather_GBps": nbytes / tg / 1e9 if tg else None,
+                "end_to_end_s": te + tg, "bitwise_own_shard": own_ok,
+                "note": "configs[4]: per-GPU spectral eval (weak scaling) then gather of the radiance to rank 0"}
+        del wi5, out5
 
     if rank == 0:
         if not args.no_cpu:

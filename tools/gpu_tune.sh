@@ -11,5 +11,5 @@ O=$R/gpurun_out/tune.log
 : > $O
 for cold in 1 4; do
   echo "== KB_COLD=$cold" >> $O
-  KB_COLD=$cold timeout -k 10 200 $KB $T rgb 16777216 32 16,32,64 sunsky_eval_rgb_v4_fast tune_rgb_u2 tune_rgb_u4 sunsky_eval_rgb_v4_fast >> $O 2>&1 || exit 1
+  KB_COLD=$cold timeout -k 10 200 $KB $T rgb 16777216 32 4,8,16,32,64 sunsky_eval_rgb_v4_fast tune_rgb_pf_v4 sunsky_eval_rgb_v4_fast >> $O 2>&1 || exit 1
 done

@@ -70,3 +70,39 @@ __device__ __forceinline__ void eval_rgb_body_u(const SunskyKArgs& K, const floa
     }
 TUNE_RGB_U(tune_rgb_u2, 2)
 TUNE_RGB_U(tune_rgb_u4, 4)
+
+// Software-pipelined grid-stride loop: the next group's loads are issued before
+// the current group's compute.
+template <bool FAST>
+__device__ __forceinline__ void eval_rgb_body_pf(const SunskyKArgs& K, const float* __restrict__ wx,
+                                                 const float* __restrict__ wy, const float* __restrict__ wz,
+                                                 size_t n, float* __restrict__ out, size_t ostride, float sign) {
+    const size_t nvec = n / 4;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float nx[4], ny[4], nz[4];
+    bool nm[4];
+    if (v < nvec) load_dirs<4>(wx, wy, wz, nullptr, v * 4, nx, ny, nz, nm);
+    for (; v < nvec; v += stride) {
+        float x[4], y[4], z[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { x[j] = nx[j]; y[j] = ny[j]; z[j] = nz[j]; }
+        if (v + stride < nvec) load_dirs<4>(wx, wy, wz, nullptr, (v + stride) * 4, nx, ny, nz, nm);
+        float r[4], g[4], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float o[3];
+            eval_rgb_local<FAST>(K, K.sun_table, to_local(K, mk3(sign * x[j], sign * y[j], sign * z[j])), true, o);
+            r[j] = o[0]; g[j] = o[1]; b[j] = o[2];
+        }
+        store_vec<4>(out, v * 4, r);
+        store_vec<4>(out + ostride, v * 4, g);
+        store_vec<4>(out + 2 * ostride, v * 4, b);
+    }
+}
+extern "C" __global__ __launch_bounds__(SS_BLOCK) void tune_rgb_pf_v4(
+    SunskyKArgs K, const float* wx, const float* wy, const float* wz, const uint8_t* active, size_t n,
+    float* out, size_t ostride, float sign) {
+    (void)active;
+    eval_rgb_body_pf<true>(K, wx, wy, wz, n, out, ostride, sign);
+}

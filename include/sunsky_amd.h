@@ -236,6 +236,18 @@ int sunsky_array_from_file(const char *path, int file_dtype, double *out, size_t
 /* array_to_file (sunsky.h:573-597) */
 int sunsky_array_to_file(const char *path, const float *data, size_t count, const uint64_t *shape,
                          int ndims);
+/* mi.hosek_sun_rad (sunsky_v.cpp:19): arhosekskymodel_solar_radiance_internal2
+ * (ArHosekSkyModel.c:686-784), the Hosek-Wilkie solar radiance in fp64 for a
+ * turbidity, a wavelength (nm), the sun elevation and the angle gamma from the sun
+ * centre (radians).  dataset_path: NULL for the bundled pack. */
+int sunsky_hosek_sun_rad(const char *dataset_path, double turbidity, double wavelength, double elevation,
+                         double gamma, double *out);
+
+/* Plugin identification of MI_EXPORT_PLUGIN (class.h:220-225; sunsky.cpp:1037):
+ * plugin_name() = "sunsky". */
+const char *plugin_name(void);
+const char *plugin_descr(void);
+
 /* Path of the bundled dataset pack the library resolves by default. */
 int sunsky_default_dataset_path(char *buf, size_t capacity);
 

@@ -26,6 +26,11 @@
 using namespace sunsky;
 
 // ---------------------------------------------------------------- errors
+namespace sunsky {
+double hosek_solar_radiance(const std::string& datasets, double turbidity, double wavelength, double elevation,
+                            double gamma);
+}
+
 namespace {
 thread_local std::string g_error;
 
@@ -806,6 +811,18 @@ int sunsky_array_to_file(const char* path, const float* data, size_t count, cons
     if (!write_array_file(path, data, count, sh.empty() ? nullptr : sh.data(), (int)sh.size(), &err))
         return fail(SUNSKY_ERROR_FILE, err);
     return SUNSKY_OK;
+}
+
+const char* plugin_name(void) { return "sunsky"; }
+const char* plugin_descr(void) { return "Sun and Sky dome background emitter (MI355X)"; }
+
+int sunsky_hosek_sun_rad(const char* dataset_path, double turbidity, double wavelength, double elevation,
+                         double gamma, double* out) {
+    if (!out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null output pointer");
+    return guarded([&] {
+        std::string ds = dataset_path && *dataset_path ? std::string(dataset_path) : default_pack_path();
+        *out = hosek_solar_radiance(ds, turbidity, wavelength, elevation, gamma);
+    });
 }
 
 int sunsky_default_dataset_path(char* buf, size_t cap) {

@@ -471,6 +471,14 @@ def array_to_file(path, data, shape=None):
                                      len(sh)))
 
 
+def hosek_sun_rad(turbidity, wavelength, elevation, gamma, dataset_path=None):
+    """mi.hosek_sun_rad (sunsky_v.cpp:19): Hosek-Wilkie solar radiance, fp64 (ArHosekSkyModel.c:686-784)."""
+    out = C.c_double()
+    check(lib().sunsky_hosek_sun_rad(dataset_path.encode() if dataset_path else None, float(turbidity),
+                                     float(wavelength), float(elevation), float(gamma), C.byref(out)))
+    return out.value
+
+
 def default_dataset_path():
     buf = C.create_string_buffer(4096)
     check(lib().sunsky_default_dataset_path(buf, 4096))

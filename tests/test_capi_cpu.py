@@ -151,3 +151,14 @@ def test_device_entry_points_refuse_host_only_emitter():
     assert b"image size" in lib.sunsky_last_error()
     assert lib.sunsky_eval_vjp(em._h, vin, None, 0, 0, None, 4, buf, 4, None, None) != 0
     assert b"gradient" in lib.sunsky_last_error()
+
+
+def test_hosek_sun_rad_reproduces_spd_fixtures(golden_dir):
+    """mi.hosek_sun_rad's product counterpart reproduces the reference's 80 .spd fixtures
+    (generated by mi.hosek_sun_rad, test_sunsky.py:154-196) bit for bit in fp32."""
+    sp = np.load(os.path.join(golden_dir, "sun_spectra.npz"))
+    for t, eta, g, rad in zip(sp["turbidity"], sp["eta"], sp["gamma"], sp["radiance"]):
+        got = np.array([ss.hosek_sun_rad(t, w, eta, g) for w in sp["wavelengths"]])
+        np.testing.assert_array_equal(got.astype(np.float32), rad)
+    assert ss.hosek_sun_rad(3.0, 800.0, 0.5, 0.0) == 0.0          # outside [320, 720] nm
+    assert ss.lib().plugin_name() == b"sunsky"

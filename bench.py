@@ -380,6 +380,34 @@ def main():
                               "note": "sample_direction (reads u; writes d, pdf, RGB weight) + pdf_direction "
                                       "(reads d; writes pdf)"}
         del u, d, pdf_s, wgt, pdf_q
+        # caller (§8f row 4): direct sun+sky light at 16M diffuse points x 4 spp, emitter + BSDF
+        # sampling with MIS fused in one kernel (sunsky_direct_diffuse); reads 12 B normal, writes 12 B RGB
+        npts, spp = n, 4
+        nrm = torch.randn((3, npts), generator=g, device=dev)
+        nrm[2].abs_().add_(0.2)
+        nrm /= nrm.norm(dim=0, keepdim=True)
+        nrm = nrm.contiguous()
+        dd = torch.empty((3, npts), dtype=torch.float32, device=dev)
+        n_in = ss._capi.Vec3In(nrm[0].data_ptr(), nrm[1].data_ptr(), nrm[2].data_ptr())
+
+        def direct_step():
+            rc = lib.sunsky_direct_diffuse(smp._h, n_in, None, None, 0, 0, 7, spp, npts, dd.data_ptr(), npts, stream)
+            if rc:
+                raise RuntimeError(lib.sunsky_last_error().decode())
+
+        direct_step()
+        t_d = KernelTimer()
+        t_d.begin()
+        for _ in range(reps):
+            direct_step()
+        t_d.end(reps)
+        ms_d = t_d.mean_ms()
+        sec["direct_diffuse_16M_x4spp"] = {"samples_per_s": npts * spp / (ms_d * 1e-3), "ms": ms_d,
+                                           "points": npts, "spp": spp,
+                                           "note": "per sample: sample_direction + eval (emitter sampling), cosine "
+                                                   "BSDF sample + pdf_direction + eval (escaped ray), power-heuristic "
+                                                   "MIS; C4 sun/sky, random normals; one fused kernel"}
+        del nrm, dd
         if rank == 0:
             result["secondary"] = sec
 

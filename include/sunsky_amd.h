@@ -196,6 +196,19 @@ int sunsky_bake_latlong(const sunsky_emitter *e, int width, int height, float th
                         float phi0, float phi1, const float *wavelengths_host, int n_wavelengths,
                         float *out, size_t out_stride, void *stream);
 
+/* A caller of sample_direction / pdf_direction / eval: the sun-and-sky light an
+ * unoccluded smooth-diffuse point receives, gathered as the path integrator does at
+ * one vertex (src/integrators/path.cpp:176-250; src/bsdfs/diffuse.cpp:100-180):
+ * emitter sampling + cosine-hemisphere BSDF sampling combined with the power
+ * heuristic, spp samples per point from PCG32Sampler-seeded streams
+ * (src/render/sampler.cpp:125-144: sample_tea_32(seed, point index)).
+ * normal: unit world-space normals; reflectance: gray per point (NULL = 1).
+ * out planes: 3 (RGB) or n_wavelengths <= 4 (spectral, per-point wavelengths).
+ * n < 2^32. */
+int sunsky_direct_diffuse(const sunsky_emitter *e, sunsky_vec3_in normal, const float *reflectance,
+                          const float *wavelengths, int n_wavelengths, size_t wl_stride, uint32_t seed,
+                          uint32_t spp, size_t n, float *out, size_t out_stride, void *stream);
+
 /* ------------------------------------------------ forward-mode derivatives */
 typedef enum sunsky_param {         /* Differentiable traverse() parameters, sunsky.cpp:220-240 */
     SUNSKY_PARAM_TURBIDITY = 0,     /* tangent: 1 value                               */

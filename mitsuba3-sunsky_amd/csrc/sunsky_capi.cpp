@@ -104,7 +104,8 @@ std::string code_object_path() {
 enum KernelId {
     K_EVAL_RGB_V4, K_EVAL_RGB_V1, K_EVAL_SPEC_BCAST_V4, K_EVAL_SPEC_BCAST_V1, K_EVAL_SPEC_NODES_V4,
     K_EVAL_SPEC_RAYS_V4, K_EVAL_SPEC_RAYS_V1, K_SAMPLE_DIRECTION_RGB, K_SAMPLE_DIRECTION_SPEC, K_PDF_DIRECTION_V4, K_PDF_DIRECTION_V1, K_SAMPLE_WAVELENGTHS_RGB,
-    K_SAMPLE_WAVELENGTHS_SPEC, K_SAMPLE_RAY_RGB, K_SAMPLE_RAY_SPEC, K_BAKE_RGB, K_BAKE_SPEC, K_COUNT
+    K_SAMPLE_WAVELENGTHS_SPEC, K_SAMPLE_RAY_RGB, K_SAMPLE_RAY_SPEC, K_BAKE_RGB, K_BAKE_SPEC,
+    K_DIRECT_DIFFUSE_RGB, K_DIRECT_DIFFUSE_SPEC, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
@@ -112,7 +113,7 @@ const char* kKernelNames[K_COUNT] = {
     "sunsky_sample_direction_spec", "sunsky_pdf_direction_v4", "sunsky_pdf_direction_v1",
     "sunsky_sample_wavelengths_rgb",
     "sunsky_sample_wavelengths_spec", "sunsky_sample_ray_rgb", "sunsky_sample_ray_spec",
-    "sunsky_bake_latlong_rgb", "sunsky_bake_latlong_spec"};
+    "sunsky_bake_latlong_rgb", "sunsky_bake_latlong_spec", "sunsky_direct_diffuse_rgb", "sunsky_direct_diffuse_spec"};
 
 struct DeviceModule {
     hipModule_t module = nullptr;
@@ -172,6 +173,7 @@ int blocks_per_cu(KernelId k) {
         case K_SAMPLE_DIRECTION_RGB: case K_SAMPLE_DIRECTION_SPEC: case K_PDF_DIRECTION_V4: case K_PDF_DIRECTION_V1:
             return 64;
         case K_BAKE_RGB: case K_BAKE_SPEC: return 64;
+        case K_DIRECT_DIFFUSE_RGB: case K_DIRECT_DIFFUSE_SPEC: return 64;
         case K_EVAL_SPEC_RAYS_V4: case K_EVAL_SPEC_RAYS_V1: return 64;
         default: return 16;
     }
@@ -780,6 +782,30 @@ int sunsky_bake_latlong(const sunsky_emitter* e, int width, int height, float th
             void* args[] = {&K, &G, &L, &out, &ostride};
             launch(e->fn(K_BAKE_SPEC), grid_for(e->mod, K_BAKE_SPEC, n), s, args);
         }
+    });
+}
+
+int sunsky_direct_diffuse(const sunsky_emitter* e, sunsky_vec3_in nrm, const float* rho, const float* lam, int nlam,
+                          size_t lstride, uint32_t seed, uint32_t spp, size_t n, float* out, size_t ostride,
+                          void* stream) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (n == 0) return SUNSKY_OK;
+    const bool spec = e->kargs.variant == kSpectral;
+    if (!nrm.x || !nrm.y || !nrm.z || !out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null normal / output pointer");
+    if (spp < 1) return fail(SUNSKY_ERROR_INVALID_VALUE, "spp must be >= 1");
+    if (n > 0xffffffffull) return fail(SUNSKY_ERROR_INVALID_VALUE, "more than 2^32 points (the sampler's lane index is 32-bit)");
+    if (spec && (!lam || nlam < 1 || nlam > 4))
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "spectral direct lighting needs 1..4 wavelength planes");
+    if (!spec && (lam || nlam)) return fail(SUNSKY_ERROR_INVALID_VALUE, "RGB direct lighting takes no wavelengths");
+    if (ostride < n || (spec && lstride < n)) return fail(SUNSKY_ERROR_INVALID_VALUE, "stride < n");
+    return guarded([&] {
+        if (!e->mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
+        SunskyKArgs K = e->kargs;
+        int nl = spec ? nlam : 0;
+        void* args[] = {&K, (void*)&nrm.x, (void*)&nrm.y, (void*)&nrm.z, &rho, &lam, &lstride, &nl, &seed, &spp, &n,
+                        &out, &ostride};
+        const KernelId k = spec ? K_DIRECT_DIFFUSE_SPEC : K_DIRECT_DIFFUSE_RGB;
+        launch(e->fn(k), grid_for(e->mod, k, n), (hipStream_t)stream, args);
     });
 }
 

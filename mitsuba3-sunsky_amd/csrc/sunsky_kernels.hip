@@ -1003,6 +1003,126 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
 // bake by sunsky_latlong_tables (tab = [cos phi (W), sin phi (W), sin theta (H),
 // cos theta (H)]); each pixel then reads 4 L2-resident table entries instead of
 // two sincosf.
+// ------------------------------------------------ caller: direct light at diffuse points
+// mis_weight (power heuristic, src/integrators/path.cpp:315-321)
+template <bool FAST>
+__device__ __forceinline__ float mis_power(float a, float b) {
+    a *= a;
+    b *= b;
+    const float w = fdiv<FAST>(a, a + b);
+    return isfinite(w) ? w : 0.f;
+}
+
+// The sky-and-sun lighting of an unoccluded diffuse point, as the path
+// integrator gathers it in one vertex (src/integrators/path.cpp:176-250 with
+// the smooth diffuse BSDF of src/bsdfs/diffuse.cpp:100-180, the sun/sky the
+// scene's only emitter, nothing occluding):
+//   emitter sampling: (ds, w) = sample_direction(u_em); f = rho/pi max(0, n.d);
+//     result += f * w * mis(ds.pdf, pdf_bsdf(d))           (when ds.pdf != 0)
+//   BSDF sampling: wo = Frame(n).to_world(square_to_cosine_hemisphere(u_bsdf)),
+//     pdf_bsdf = cos/pi, weight = rho; the ray escapes, so
+//     result += rho * eval(-wo) * mis(pdf_bsdf, pdf_direction(wo))
+// averaged over spp samples drawn from PCG32Sampler-seeded streams
+// (next_2d for u_em, then next_2d for u_bsdf).  Out: 3 planes (RGB) or one per
+// per-point wavelength (spectral, si.wavelengths).  Everything between the
+// normal and the accumulated radiance stays in VGPRs: per point the kernel
+// reads 12 B (+ rho, + wavelengths) and writes 4 B per channel, whatever spp.
+template <bool FAST, bool SPEC>
+__device__ __forceinline__ void direct_diffuse_body(
+    const SunskyKArgs& K, const float* __restrict__ nx, const float* __restrict__ ny, const float* __restrict__ nz,
+    const float* __restrict__ rho, const float* __restrict__ lam, size_t lstride, int nlam, uint32_t seed,
+    uint32_t spp, size_t n, float* __restrict__ out, size_t ostride) {
+    __shared__ SamplerLds<FAST, SPEC> S;
+    stage_sampler_lds<FAST, SPEC>(K, &S);
+    constexpr int C = SPEC ? 4 : 3;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float3_ nrm = mk3(nx[i], ny[i], nz[i]);
+        float3_ fs, ft;
+        coordinate_system(nrm, &fs, &ft);
+        uint32_t v0 = seed, v1 = (uint32_t)i;
+        sample_tea_32(&v0, &v1);
+        Pcg32 rng;
+        rng.seed(v0, v1);
+        float wl[C];
+        if constexpr (SPEC) {
+#pragma unroll
+            for (int k = 0; k < C; ++k) wl[k] = k < nlam ? lam[(size_t)k * lstride + i] : 0.f;
+        }
+        float acc[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) acc[c] = 0.f;
+        for (uint32_t smp = 0; smp < spp; ++smp) {
+            const float u0 = rng.next_float(), u1 = rng.next_float();
+            const float u2 = rng.next_float(), u3 = rng.next_float();
+            // ---- emitter sampling: sample_direction (sunsky.cpp:399-441)
+            const bool pick_sky = u0 < K.w_sky;
+            float3_ sd = pick_sky ? sample_sky<FAST>(K, S.tgmm, u0 / K.w_sky, u1)
+                                  : sample_sun<FAST>(K, (u0 - K.w_sky) / (1.f - K.w_sky), u1);
+            bool act = sd.z >= 0.f;
+            const float3_ d = to_world(K, sd);
+            float skyp, sunp;
+            compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+            const float pd = lerpf_(sunp, skyp, K.w_sky);
+            const float cos_em = dot3(nrm, d);
+            if (pd != 0.f && cos_em > 0.f) {
+                const float bpdf = kInvPi * cos_em;     // diffuse eval / pdf: rho / pi cos, cos / pi
+                const float scale = bpdf * mis_power<FAST>(pd, bpdf);
+                const float3_ wo = to_local(K, d);
+                if constexpr (!SPEC) {
+                    float e[3];
+                    eval_rgb_local<FAST>(K, S.sun, wo, act, e);
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        const float w = e[c] / pd;
+                        acc[c] = fmaf(scale, isfinite(w) ? w : 0.f, acc[c]);
+                    }
+                } else {
+                    DirTerms t = dir_terms<FAST>(K, wo, act);
+                    add_sun_terms<FAST>(K, t);
+#pragma unroll
+                    for (int c = 0; c < C; ++c)
+                        if (c < nlam) {
+                            const float w = eval_spec_one<FAST>(K, S.chans.c, S.sun, S.ld, t, wl[c]) / pd;
+                            acc[c] = fmaf(scale, isfinite(w) ? w : 0.f, acc[c]);
+                        }
+                }
+            }
+            // ---- BSDF sampling: square_to_cosine_hemisphere (warp.h:412-420), then the miss
+            float px, py;
+            disk_concentric(u2, u3, &px, &py);
+            const float lz = safe_sqrtf_(1.f - fmaf(px, px, py * py));
+            const float bpdf = kInvPi * lz;
+            if (bpdf > 0.f) {
+                const float3_ dw = frame_to_world(fs, ft, nrm, mk3(px, py, lz));
+                const float3_ wo = to_local(K, dw);
+                // pdf_direction (sunsky.cpp:443-451) of the escaped ray
+                float bskyp, bsunp;
+                compute_pdfs<FAST>(K, S.tgmm, wo, true, true, &bskyp, &bsunp);
+                const float mis = mis_power<FAST>(bpdf, lerpf_(bsunp, bskyp, K.w_sky));
+                const bool up = wo.z >= 0.f;
+                if constexpr (!SPEC) {
+                    float e[3];
+                    eval_rgb_local<FAST>(K, S.sun, wo, up, e);
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) acc[c] = fmaf(e[c], mis, acc[c]);
+                } else {
+                    DirTerms t = dir_terms<FAST>(K, wo, up);
+                    add_sun_terms<FAST>(K, t);
+#pragma unroll
+                    for (int c = 0; c < C; ++c)
+                        if (c < nlam) acc[c] = fmaf(eval_spec_one<FAST>(K, S.chans.c, S.sun, S.ld, t, wl[c]), mis, acc[c]);
+                }
+            }
+        }
+        const float r = (rho ? rho[i] : 1.f) / (float)spp;
+        const int nc = SPEC ? nlam : 3;
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            if (c < nc) __builtin_nontemporal_store(acc[c] * r, out + (size_t)c * ostride + i);
+    }
+}
+
 struct LatLong { int w, h; float theta0, dtheta, phi0, dphi; const float* tab; };
 
 __device__ __forceinline__ float3_ latlong_dir(const LatLong& G, size_t i) {
@@ -1557,6 +1677,17 @@ SS_SAMPLE_RAY(sunsky_sample_ray_rgb_fast, true, false)
 SS_SAMPLE_RAY(sunsky_sample_ray_rgb_ref, false, false)
 SS_SAMPLE_RAY(sunsky_sample_ray_spec_fast, true, true)
 SS_SAMPLE_RAY(sunsky_sample_ray_spec_ref, false, true)
+
+#define SS_DIRECT_DIFFUSE(NAME, FAST, SPEC)                                                                   \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                              \
+        SunskyKArgs K, const float* nx, const float* ny, const float* nz, const float* rho, const float* lam, \
+        size_t lstride, int nlam, uint32_t seed, uint32_t spp, size_t n, float* out, size_t ostride) {          \
+        direct_diffuse_body<FAST, SPEC>(K, nx, ny, nz, rho, lam, lstride, nlam, seed, spp, n, out, ostride);   \
+    }
+SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_rgb_fast, true, false)
+SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_rgb_ref, false, false)
+SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_spec_fast, true, true)
+SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_spec_ref, false, true)
 
 extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_jvp_rgb(
     SunskyKArgs K, const float* jvp, const float* wx, const float* wy, const float* wz, const uint8_t* active,

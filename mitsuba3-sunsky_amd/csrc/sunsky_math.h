@@ -135,6 +135,49 @@ SS_NO_UNROLL
     return res;
 }
 
+// sample_tea_32 (include/mitsuba/core/random.h:77-90), 4 rounds
+SS_HD inline void sample_tea_32(uint32_t* v0, uint32_t* v1) {
+    uint32_t a = *v0, b = *v1, sum = 0;
+    for (int i = 0; i < 4; ++i) {
+        sum += 0x9e3779b9u;
+        a += ((b << 4) + 0xa341316cu) ^ (b + sum) ^ ((b >> 5) + 0xc8013ea4u);
+        b += ((a << 4) + 0xad90777du) ^ (a + sum) ^ ((a >> 5) + 0x7e95761eu);
+    }
+    *v0 = a;
+    *v1 = b;
+}
+
+// PCG32 (M. O'Neill's pcg32_srandom_r / pcg32_random_r: XSH-RR output of a 64-bit
+// LCG), the generator of Dr.Jit's PCG32 used by the independent sampler
+// (src/samplers/independent.cpp:88-97).  Dr.Jit is not vendored:
+// this is the published algorithm, seeded as PCG32Sampler::seed does
+// (src/render/sampler.cpp:125-144): (v0, v1) = sample_tea_32(seed, lane index),
+// rng.seed(initstate = v0, initseq = v1).
+struct Pcg32 {
+    uint64_t state, inc;
+    SS_HD void seed(uint64_t initstate, uint64_t initseq) {
+        state = 0;
+        inc = (initseq << 1) | 1u;
+        next_uint32();
+        state += initstate;
+        next_uint32();
+    }
+    SS_HD uint32_t next_uint32() {
+        const uint64_t old = state;
+        state = old * 0x5851f42d4c957f2dull + inc;
+        const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
+        const uint32_t rot = (uint32_t)(old >> 59);
+        return (xs >> rot) | (xs << ((0u - rot) & 31u));
+    }
+    // next_float32: the 23 high bits as the mantissa of [1, 2), minus 1
+    SS_HD float next_float() {
+        const uint32_t bits = (next_uint32() >> 9) | 0x3f800000u;
+        float f;
+        __builtin_memcpy(&f, &bits, sizeof f);
+        return f - 1.f;
+    }
+};
+
 // warp::square_to_uniform_disk_concentric, warp.h:54-90
 SS_HD inline void disk_concentric(float sx, float sy, float* ox, float* oy) {
     float x = fmaf(2.f, sx, -1.f), y = fmaf(2.f, sy, -1.f);

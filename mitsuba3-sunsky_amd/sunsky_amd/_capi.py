@@ -84,6 +84,8 @@ _SIGS = {
                                   vp, vp, C.c_size_t, vp]),
     "sunsky_bake_latlong": (C.c_int, [vp, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, C.c_float, c_float_p,
                                       C.c_int, vp, C.c_size_t, vp]),
+    "sunsky_direct_diffuse": (C.c_int, [vp, Vec3In, vp, vp, C.c_int, C.c_size_t, C.c_uint32, C.c_uint32,
+                                        C.c_size_t, vp, C.c_size_t, vp]),
     "sunsky_hosek_sun_rad": (C.c_int, [C.c_char_p, C.c_double, C.c_double, C.c_double, C.c_double,
                                        C.POINTER(C.c_double)]),
     "plugin_name": (C.c_char_p, []),

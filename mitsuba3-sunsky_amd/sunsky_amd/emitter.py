@@ -356,6 +356,30 @@ class SunskyEmitter:
                                         float(phi[1]), lam_p, m, _ptr(out), height * width, self._stream()))
         return out
 
+    def direct_diffuse(self, normals, seed=0, spp=1, wavelengths=None, reflectance=None, out=None):
+        """Sun-and-sky light at unoccluded smooth-diffuse points (sunsky_direct_diffuse): the
+        path integrator's emitter sampling + BSDF sampling with MIS at one vertex
+        (path.cpp:176-250, diffuse.cpp:100-180), spp PCG32 samples per point.
+        normals (3, n); wavelengths (k <= 4, n) for spectral -> (C, n)."""
+        normals, nin = self._vec_in(normals)
+        n = normals.shape[1]
+        if self.is_spectral:
+            if wavelengths is None:
+                raise ValueError("spectral direct lighting needs per-point wavelengths")
+            wl = self._f32(wavelengths, rows=1)
+            if wl.dim() == 1:
+                wl = wl.view(1, -1)
+            k, lam_p, lstride = wl.shape[0], _ptr(wl), wl.stride(0)
+        else:
+            wl, k, lam_p, lstride = None, 3, None, 0
+        rho = self._f32(reflectance)
+        if out is None:
+            out = torch.empty((k, n), dtype=torch.float32, device=self.device)
+        check(lib().sunsky_direct_diffuse(self._h, nin, _ptr(rho), lam_p, k if self.is_spectral else 0, lstride,
+                                          int(seed) & 0xFFFFFFFF, int(spp), n, _ptr(out), out.stride(0),
+                                          self._stream()))
+        return out
+
     def eval_spectral_broadcast(self, wi, wavelengths, active=None, out=None):
         """Spectral eval of one wavelength list for every direction -> (m, n)."""
         wi, vin = self._vec_in(wi)

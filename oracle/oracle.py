@@ -292,3 +292,119 @@ def set_threads(n):
 
 def get_threads():
     return lib().oracle_get_threads()
+
+
+# ---------------------------------------------------------------- caller: direct light at diffuse points
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def sample_tea_32(v0, v1, rounds=4):
+    """sample_tea_32, include/mitsuba/core/random.h:77-90 (uint32 arrays)."""
+    v0 = np.asarray(v0, dtype=np.uint32).copy()
+    v1 = np.asarray(v1, dtype=np.uint32).copy()
+    s = np.uint32(0)
+    with np.errstate(over="ignore"):
+        for _ in range(rounds):
+            s = np.uint32(s + np.uint32(0x9E3779B9))
+            v0 += ((v1 << np.uint32(4)) + np.uint32(0xA341316C)) ^ (v1 + s) ^ ((v1 >> np.uint32(5)) + np.uint32(0xC8013EA4))
+            v1 += ((v0 << np.uint32(4)) + np.uint32(0xAD90777D)) ^ (v0 + s) ^ ((v0 >> np.uint32(5)) + np.uint32(0x7E95761E))
+    return v0, v1
+
+
+class Pcg32:
+    """PCG32 (O'Neill's pcg32_srandom_r / pcg32_random_r), vectorised over lanes, seeded as
+    PCG32Sampler::seed (src/render/sampler.cpp:125-144): rng.seed(*sample_tea_32(seed, lane)).
+    next_float follows Dr.Jit's next_float32 (23 high bits as a [1, 2) mantissa, minus 1)."""
+
+    MULT = np.uint64(0x5851F42D4C957F2D)
+
+    def __init__(self, seed, n):
+        v0, v1 = sample_tea_32(np.full(n, seed, dtype=np.uint32), np.arange(n, dtype=np.uint32))
+        self.state = np.zeros(n, dtype=np.uint64)
+        self.inc = (v1.astype(np.uint64) << np.uint64(1)) | np.uint64(1)
+        self.next_uint32()
+        self.state += v0.astype(np.uint64)
+        self.next_uint32()
+
+    def next_uint32(self):
+        old = self.state
+        with np.errstate(over="ignore"):
+            self.state = old * self.MULT + self.inc
+        xs = (((old >> np.uint64(18)) ^ old) >> np.uint64(27)).astype(np.uint32)
+        rot = (old >> np.uint64(59)).astype(np.uint32)
+        return (xs >> rot) | (xs << ((np.uint32(0) - rot) & np.uint32(31)))
+
+    def next_float(self):
+        bits = (self.next_uint32() >> np.uint32(9)) | np.uint32(0x3F800000)
+        return bits.view(np.float32) - np.float32(1.0)
+
+
+def _coordinate_system(n):
+    """coordinate_system, include/mitsuba/core/vector.h:116-137 (fp32)."""
+    n = n.astype(np.float32)
+    nx, ny, nz = n[:, 0], n[:, 1], n[:, 2]
+    sgn = np.copysign(np.float32(1), nz).astype(np.float32)      # mulsign uses the sign bit
+    a = (np.float32(-1) / (sgn + nz)).astype(np.float32)
+    b = (nx * ny * a).astype(np.float32)
+    s = np.stack([sgn * (nx * nx * a) + np.float32(1), sgn * b, -sgn * nx], axis=1).astype(np.float32)
+    t = np.stack([b, ny * (ny * a) + sgn, -ny], axis=1).astype(np.float32)
+    return s, t
+
+
+def _disk_concentric(sx, sy):
+    """square_to_uniform_disk_concentric, include/mitsuba/core/warp.h:54-90 (fp32)."""
+    x = (np.float32(2) * sx - np.float32(1)).astype(np.float32)
+    y = (np.float32(2) * sy - np.float32(1)).astype(np.float32)
+    is_zero = (x == 0) & (y == 0)
+    q13 = np.abs(x) < np.abs(y)
+    r = np.where(q13, y, x)
+    rp = np.where(q13, x, y)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        phi = (np.float32(0.25 * np.pi) * rp / r).astype(np.float32)
+    phi = np.where(q13, np.float32(0.5 * np.pi) - phi, phi)
+    phi = np.where(is_zero, np.float32(0), phi).astype(np.float32)
+    return (r * np.cos(phi)).astype(np.float32), (r * np.sin(phi)).astype(np.float32)
+
+
+def _mis_power(a, b):
+    """mis_weight, src/integrators/path.cpp:315-321."""
+    a = a * a
+    b = b * b
+    with np.errstate(divide="ignore", invalid="ignore"):
+        w = a / (a + b)
+    return np.where(np.isfinite(w), w, 0.0)
+
+
+def direct_diffuse(em, normals, seed, spp, wavelengths=None, rho=None):
+    """Sun-and-sky light at unoccluded smooth-diffuse points, gathered as the path
+    integrator does at one vertex (src/integrators/path.cpp:176-250; diffuse BSDF
+    src/bsdfs/diffuse.cpp:100-180): emitter sampling + cosine BSDF sampling with the
+    power heuristic, spp samples per point (u_em = next_2d, u_bsdf = next_2d).
+    em: an Oracle.  normals (n, 3); wavelengths (k, n) for spectral.  Returns (C, n) fp64."""
+    normals = np.asarray(normals, dtype=np.float32)
+    n = normals.shape[0]
+    rng = Pcg32(seed, n)
+    s, t = _coordinate_system(normals)
+    c = wavelengths.shape[0] if em.spectral else 3
+    acc = np.zeros((c, n), dtype=np.float64)
+    lam = None if not em.spectral else np.asarray(wavelengths, dtype=np.float32)
+    for _ in range(spp):
+        u0, u1, u2, u3 = rng.next_float(), rng.next_float(), rng.next_float(), rng.next_float()
+        # emitter sampling (path.cpp:208-250)
+        r = em.sample_direction(np.stack([u0, u1], axis=1), wavelengths=lam)
+        d, pd, w = r["d"], r["pdf"], r["weight"]
+        cos_em = (normals.astype(np.float64) * d).sum(axis=1)
+        ok = (pd != 0) & (cos_em > 0)
+        bpdf = np.where(ok, cos_em / np.pi, 0.0)
+        scale = np.where(ok, bpdf * _mis_power(pd, bpdf), 0.0)
+        acc += scale[None, :] * w.T
+        # BSDF sampling + the escaped ray (path.cpp:176-196)
+        px, py = _disk_concentric(u2, u3)
+        lz = np.sqrt(np.maximum(0.0, 1.0 - (px.astype(np.float64) ** 2 + py.astype(np.float64) ** 2)))
+        dw = (s * px[:, None] + t * py[:, None] + normals * lz[:, None]).astype(np.float32)
+        bp = lz / np.pi
+        mis = np.where(bp > 0, _mis_power(bp, em.pdf_direction(dw)), 0.0)
+        e = em.eval(-dw, lam) if em.spectral else em.eval(-dw).T
+        acc += mis[None, :] * e
+    r = np.ones(n) if rho is None else np.asarray(rho, dtype=np.float64)
+    return acc * (r / spp)[None, :]

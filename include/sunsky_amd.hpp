@@ -207,6 +207,16 @@ public:
                                   wavelengths.empty() ? nullptr : wavelengths.data(), (int)wavelengths.size(),
                                   out.data, out.stride ? out.stride : n, stream));
     }
+    // Direct sun + sky light at unoccluded diffuse points (sunsky_direct_diffuse): one vertex of
+    // PathIntegrator::sample (path.cpp:176-250) with diffuse.cpp's BSDF, spp samples per point.
+    // Spectral: wavelengths = the points' si.wavelengths (<= 4 planes).
+    void direct_diffuse(Vector3 normal, size_t n, uint32_t seed, uint32_t spp, SpectrumOut out,
+                        const float* reflectance = nullptr, Wavelengths wavelengths = {},
+                        void* stream = nullptr) const {
+        check(sunsky_direct_diffuse(e_, vin(normal), reflectance, wavelengths.data, wavelengths.count,
+                                    wavelengths.stride ? wavelengths.stride : n, seed, spp, n, out.data,
+                                    out.stride ? out.stride : n, stream));
+    }
     // Spectral eval of one wavelength list broadcast to every ray (test_sunsky.py:42-59 layout)
     void eval_spectral_broadcast(Vector3 wi, size_t n, const std::vector<float>& wavelengths, SpectrumOut out,
                                  const uint8_t* active = nullptr, void* stream = nullptr) const {
@@ -271,5 +281,13 @@ private:
     static sunsky_vec3_out vout(const Vector3Out& v) { return sunsky_vec3_out{v.x, v.y, v.z}; }
     sunsky_emitter* e_ = nullptr;
 };
+
+// mi.hosek_sun_rad (sunsky_v.cpp:19): Hosek-Wilkie solar radiance, fp64; dataset nullptr = bundled pack
+inline double hosek_sun_rad(double turbidity, double wavelength, double elevation, double gamma,
+                            const char* dataset = nullptr) {
+    double out = 0.0;
+    check(sunsky_hosek_sun_rad(dataset, turbidity, wavelength, elevation, gamma, &out));
+    return out;
+}
 
 }  // namespace sunsky_amd

@@ -57,6 +57,7 @@ static int host_mode() {
     } catch (const NotImplementedError& e) {
         std::printf("not implemented: %s\n", e.what());
     }
+    std::printf("hosek_sun_rad=%.17g\n", hosek_sun_rad(3.5, 555.0, 0.7, 0.001));
     std::puts("host ok");
     return 0;
 }
@@ -106,7 +107,19 @@ static int gpu_mode(const std::string& dir) {
     dsi.d = {d_d, d_d + n, d_d + 2 * n};
     em.pdf_direction(n, dsi, d_pdf2);
     em.eval_jvp(si, Param::Turbidity, {1.f}, {d_jv, n}, {d_djv, n});   // d eval / d turbidity
+    // direct light at upward diffuse points, 2 spp, seed 3
+    float *d_nrm, *d_dd;
+    HIPCK(hipMalloc(&d_nrm, 3 * n * 4)); HIPCK(hipMalloc(&d_dd, 3 * n * 4));
+    {
+        std::vector<float> nrm(3 * n, 0.f);
+        std::fill(nrm.begin() + 2 * n, nrm.end(), 1.f);
+        HIPCK(hipMemcpy(d_nrm, nrm.data(), 3 * n * 4, hipMemcpyHostToDevice));
+    }
+    em.direct_diffuse({d_nrm, d_nrm + n, d_nrm + 2 * n}, n, 3, 2, {d_dd, n});
     HIPCK(hipDeviceSynchronize());
+    std::vector<float> direct(3 * n);
+    HIPCK(hipMemcpy(direct.data(), d_dd, 3 * n * 4, hipMemcpyDeviceToHost));
+    (void)hipFree(d_nrm); (void)hipFree(d_dd);
 
     std::vector<float> rgb(3 * n), dd(3 * n), pdf(n), w(3 * n), pdf2(n), djv(3 * n);
     HIPCK(hipMemcpy(djv.data(), d_djv, 3 * n * 4, hipMemcpyDeviceToHost));
@@ -117,7 +130,8 @@ static int gpu_mode(const std::string& dir) {
     HIPCK(hipMemcpy(pdf2.data(), d_pdf2, n * 4, hipMemcpyDeviceToHost));
     bool ok = write_file(dir + "/wi.f32", wi) && write_file(dir + "/u.f32", u) && write_file(dir + "/rgb.f32", rgb) &&
               write_file(dir + "/d.f32", dd) && write_file(dir + "/pdf.f32", pdf) && write_file(dir + "/w.f32", w) &&
-              write_file(dir + "/pdf2.f32", pdf2) && write_file(dir + "/drgb_dturbidity.f32", djv);
+              write_file(dir + "/pdf2.f32", pdf2) && write_file(dir + "/drgb_dturbidity.f32", djv) &&
+              write_file(dir + "/direct.f32", direct);
     for (float* ptr : {d_wi, d_u, d_rgb, d_d, d_pdf, d_w, d_pdf2, d_jv, d_djv}) (void)hipFree(ptr);
     if (!ok) { std::puts("FAIL writing outputs"); return 1; }
     std::printf("gpu ok w_sky=%.9g\n", em.info().sky_sampling_w);

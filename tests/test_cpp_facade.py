@@ -33,6 +33,10 @@ def test_facade_host_mode(exe):
     assert "host ok" in r.stdout
     assert "Turbidity value 12.000000 is out of range [1, 10]" in r.stdout
     assert "not implemented: sample_position" in r.stdout
+    # hosek_sun_rad (sunsky_v.cpp:19) through the facade == the oracle's HW solar radiance
+    hs = float(r.stdout.split("hosek_sun_rad=")[1].split()[0])
+    assert hs == pytest.approx(O.Oracle(SUN45, "spectral", "jit", "f64").hw_sun_radiance(3.5, 555.0, 0.7, 0.001),
+                               rel=1e-14)
     w = float(r.stdout.split("w_sky=")[1].split()[0])
     o = O.Oracle(SUN45, "rgb", "jit", "f32")
     assert abs(w - o.info()["w_sky"]) < 1e-5
@@ -62,6 +66,11 @@ def test_facade_gpu_mode(exe, tmp_path):
     o32.override_w_sky(w_gpu)
     ref = o32.sample_direction(u)
     assert np.quantile(np.abs(d - ref["d"]).max(axis=1), 0.999) < 2e-6
+    # direct_diffuse through the facade (normals +z, seed 3, 2 spp) vs the oracle's estimator
+    dd = load("direct.f32", 3).T
+    ref = O.direct_diffuse(o32, np.tile(np.array([[0, 0, 1]], np.float32), (n, 1)), 3, 2)
+    rel = (np.abs(dd - ref) / np.maximum(np.abs(ref), 1e-3 * np.abs(ref).max())).max(axis=0)
+    assert np.quantile(rel, 0.995) < 2e-4
     # eval_jvp through the facade: d eval / d turbidity vs fp64 central differences
     djv = load("drgb_dturbidity.f32", 3)
     h = 1e-3

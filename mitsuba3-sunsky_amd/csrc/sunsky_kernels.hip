@@ -180,13 +180,15 @@ __device__ __forceinline__ float render_sun_rgb_compact(const float* table, int 
 }
 
 // Full RGB eval for one local direction (sunsky.cpp:317-323).
+// chans: the 3 channels (K.fsky / K.sky, or an LDS copy in the sampling kernels,
+// whose other constants already fill the SGPR file).
 template <bool FAST>
-__device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const float* sun_tab, float3_ wo, bool mask,
-                                               float out[3]) {
+__device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
+                                               const float* sun_tab, float3_ wo, bool mask, float out[3]) {
     DirTerms t = dir_terms<FAST>(K, wo, mask);
     if constexpr (FAST) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) out[c] = sky_fast(K.fsky[c], t);   // sky_scale and CIE folded
+        for (int c = 0; c < 3; ++c) out[c] = sky_fast(chans[c], t);   // sky_scale and CIE folded
         if (t.hit_sun) {
             add_sun_terms<true>(K, t);
 #pragma unroll 1
@@ -198,7 +200,7 @@ __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const float
     } else {
         const float cie = (float)kCieYNormalization;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) out[c] = sky_ref(K.sky[c], t, K.sky_scale);
+        for (int c = 0; c < 3; ++c) out[c] = sky_ref(chans[c], t, K.sky_scale);
         if (t.hit_sun) {
             float xs;
             int pos = sun_segment(t.cos_theta, &xs);
@@ -211,6 +213,12 @@ __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const float
 #pragma unroll
         for (int c = 0; c < 3; ++c) out[c] = t.active ? out[c] * cie : 0.f;
     }
+}
+
+template <bool FAST>
+__device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const float* sun_tab, float3_ wo, bool mask,
+                                               float out[3]) {
+    eval_rgb_local<FAST>(K, chan_table<FAST>(K), sun_tab, wo, mask, out);
 }
 
 // Spectral sun disc term for channel pair (lo, hi, f): lerp(sun) x limb darkening
@@ -575,8 +583,8 @@ struct SamplerLds {
 template <bool FAST, bool SPEC>
 __device__ __forceinline__ void stage_sampler_lds(const SunskyKArgs& K, SamplerLds<FAST, SPEC>* s) {
     stage_tgmm(K, &s->tgmm);
+    stage_chans<FAST>(K, &s->chans);
     if (SPEC) {
-        stage_chans<FAST>(K, &s->chans);
         stage_spec_dist(K, &s->sdist);
         lds_copy(s->ld, K.sun_ld, kNbWavelengths * kNbSunLdParams);
     }
@@ -807,7 +815,7 @@ __device__ __forceinline__ void sample_direction_body(
         if constexpr (!SPEC) {
             float e[3];
 #ifndef SS_PROBE_NO_WEIGHT
-            eval_rgb_local<FAST>(K, S.sun, wo, act, e);
+            eval_rgb_local<FAST>(K, S.chans.c, S.sun, wo, act, e);
 #else
             e[0] = wo.x; e[1] = wo.y; e[2] = wo.z;
 #endif
@@ -965,7 +973,7 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
         float w[4];
         int nw;
         if constexpr (!SPEC) {
-            eval_rgb_local<FAST>(K, S.sun, wo, act, w);
+            eval_rgb_local<FAST>(K, S.chans.c, S.sun, wo, act, w);
             nw = 3;
             for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = 0.f;
         } else {
@@ -1071,7 +1079,7 @@ __device__ __forceinline__ void direct_diffuse_body(
                 const float3_ wo = to_local(K, d);
                 if constexpr (!SPEC) {
                     float e[3];
-                    eval_rgb_local<FAST>(K, S.sun, wo, act, e);
+                    eval_rgb_local<FAST>(K, S.chans.c, S.sun, wo, act, e);
 #pragma unroll
                     for (int c = 0; c < 3; ++c) {
                         const float w = e[c] / pd;
@@ -1103,7 +1111,7 @@ __device__ __forceinline__ void direct_diffuse_body(
                 const bool up = wo.z >= 0.f;
                 if constexpr (!SPEC) {
                     float e[3];
-                    eval_rgb_local<FAST>(K, S.sun, wo, up, e);
+                    eval_rgb_local<FAST>(K, S.chans.c, S.sun, wo, up, e);
 #pragma unroll
                     for (int c = 0; c < 3; ++c) acc[c] = fmaf(e[c], mis, acc[c]);
                 } else {

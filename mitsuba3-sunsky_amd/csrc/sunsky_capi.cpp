@@ -115,9 +115,16 @@ const char* kKernelNames[K_COUNT] = {
     "sunsky_sample_wavelengths_spec", "sunsky_sample_ray_rgb", "sunsky_sample_ray_spec",
     "sunsky_bake_latlong_rgb", "sunsky_bake_latlong_spec", "sunsky_direct_diffuse_rgb", "sunsky_direct_diffuse_spec"};
 
+// eval kernels instantiated twice: eval(si) negates wi at compile time,
+// eval_direction(ds) uses ds.d as is (the "_dir" kernels)
+bool has_dir_form(KernelId k) {
+    return k == K_EVAL_RGB_V4 || k == K_EVAL_RGB_V1 || k == K_EVAL_SPEC_RAYS_V4 || k == K_EVAL_SPEC_RAYS_V1;
+}
+
 struct DeviceModule {
     hipModule_t module = nullptr;
     hipFunction_t fn[2][K_COUNT] = {};   // [precision][kernel]
+    hipFunction_t fn_dir[2][K_COUNT] = {};   // eval_direction forms (wo = +d) of the eval kernels
     hipFunction_t jvp_rgb = nullptr, jvp_spec = nullptr;   // eval_jvp (reference operation order)
     hipFunction_t vjp_rgb = nullptr, vjp_spec = nullptr, grad_reduce = nullptr;   // eval_vjp
     hipFunction_t latlong_tables = nullptr;                                     // bake_latlong
@@ -139,6 +146,10 @@ DeviceModule* module_for_device(int dev) {
         for (int k = 0; k < K_COUNT; ++k) {
             std::string name = std::string(kKernelNames[k]) + (p == SUNSKY_PRECISION_FAST ? "_fast" : "_ref");
             hip_check(hipModuleGetFunction(&m->fn[p][k], m->module, name.c_str()), name.c_str());
+            if (has_dir_form((KernelId)k)) {
+                std::string dn = std::string(kKernelNames[k]) + (p == SUNSKY_PRECISION_FAST ? "_dir_fast" : "_dir_ref");
+                hip_check(hipModuleGetFunction(&m->fn_dir[p][k], m->module, dn.c_str()), dn.c_str());
+            }
         }
     hip_check(hipModuleGetFunction(&m->jvp_rgb, m->module, "sunsky_eval_jvp_rgb"), "sunsky_eval_jvp_rgb");
     hip_check(hipModuleGetFunction(&m->jvp_spec, m->module, "sunsky_eval_jvp_spec"), "sunsky_eval_jvp_spec");
@@ -263,6 +274,11 @@ struct sunsky_emitter {
     hipFunction_t fn(KernelId k) const {
         if (!mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
         return mod->fn[precision][k];
+    }
+    // eval (sign < 0: wo = -wi) or eval_direction (sign > 0: wo = d) form of an eval kernel
+    hipFunction_t fn_eval(KernelId k, float sign) const {
+        if (!mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
+        return sign < 0.f ? mod->fn[precision][k] : mod->fn_dir[precision][k];
     }
 
     ~sunsky_emitter() {
@@ -466,7 +482,7 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
             if (n4) {
                 const float *x = w.x, *y = w.y, *z = w.z;
                 void* args[] = {&K, &x, &y, &z, &active, &n4, &out, &ostride, &sign};
-                launch(e->fn(K_EVAL_RGB_V4), grid_for(e->mod, K_EVAL_RGB_V4, n4 / 4), s, args);
+                launch(e->fn_eval(K_EVAL_RGB_V4, sign), grid_for(e->mod, K_EVAL_RGB_V4, n4 / 4), s, args);
             }
             if (n4 < n) {
                 const float *x = w.x + n4, *y = w.y + n4, *z = w.z + n4;
@@ -474,7 +490,7 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
                 float* o = out + n4;
                 size_t rem = n - n4;
                 void* args[] = {&K, &x, &y, &z, &a, &rem, &o, &ostride, &sign};
-                launch(e->fn(K_EVAL_RGB_V1), grid_for(e->mod, K_EVAL_RGB_V1, rem), s, args);
+                launch(e->fn_eval(K_EVAL_RGB_V1, sign), grid_for(e->mod, K_EVAL_RGB_V1, rem), s, args);
             }
         } else {
             // VEC = 4 over rays when every plane is 16-byte aligned; VEC = 1 tail
@@ -486,7 +502,7 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
             if (n4) {
                 const float *x = w.x, *y = w.y, *z = w.z;
                 void* args[] = {&K, &x, &y, &z, &lam, &lstride, &nl, &active, &n4, &out, &ostride, &sign};
-                launch(e->fn(K_EVAL_SPEC_RAYS_V4), grid_for(e->mod, K_EVAL_SPEC_RAYS_V4, n4 / 4), s, args);
+                launch(e->fn_eval(K_EVAL_SPEC_RAYS_V4, sign), grid_for(e->mod, K_EVAL_SPEC_RAYS_V4, n4 / 4), s, args);
             }
             if (n4 < n) {
                 const float *x = w.x + n4, *y = w.y + n4, *z = w.z + n4, *l = lam + n4;
@@ -494,7 +510,7 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
                 float* o = out + n4;
                 size_t rem = n - n4;
                 void* args[] = {&K, &x, &y, &z, &l, &lstride, &nl, &a, &rem, &o, &ostride, &sign};
-                launch(e->fn(K_EVAL_SPEC_RAYS_V1), grid_for(e->mod, K_EVAL_SPEC_RAYS_V1, rem), s, args);
+                launch(e->fn_eval(K_EVAL_SPEC_RAYS_V1, sign), grid_for(e->mod, K_EVAL_SPEC_RAYS_V1, rem), s, args);
             }
         }
     });

@@ -41,6 +41,30 @@ __device__ __forceinline__ float fast_rsq(float x) { return __builtin_amdgcn_rsq
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 
+// asin on [0, sqrt(0.5)]: the half chord h = |wo -/+ n| / 2 of unit_angle never
+// exceeds sqrt(2) / 2, so one odd minimax polynomial x + x^3 P(x^2) (degree 7 in
+// x^2; fitted by tools/fit_asin.py) replaces libm's two-range asin (select,
+// sqrt, polynomial, fix-up).  Max error 0.71 ulp over [0, 0.7075] in fp32 (FAST only).
+__device__ __forceinline__ float asin_half_chord(float x) {
+    const float t = x * x;
+    float p = 0.10696864128112793f;
+    p = fmaf(p, t, -0.10311298817396164f);
+    p = fmaf(p, t, 0.0816480815410614f);
+    p = fmaf(p, t, 0.003488607471808791f);
+    p = fmaf(p, t, 0.033441439270973206f);
+    p = fmaf(p, t, 0.04438246041536331f);
+    p = fmaf(p, t, 0.0750100240111351f);
+    p = fmaf(p, t, 0.16666655242443085f);
+    return fmaf(x * t, p, x);
+}
+
+// wo = -wi for eval(si), +d for eval_direction: a compile-time sign folds into
+// the source modifiers of the first use instead of 3 multiplies per direction.
+template <bool NEG>
+__device__ __forceinline__ float3_ flip3(float x, float y, float z) {
+    return NEG ? mk3(-x, -y, -z) : mk3(x, y, z);
+}
+
 template <bool FAST> struct ChanSel { using T = SkyChannel; };
 template <> struct ChanSel<true> { using T = FastChannel; };
 
@@ -64,16 +88,19 @@ __device__ __forceinline__ DirTerms dir_terms(const SunskyKArgs& K, float3_ wo, 
     t.cos_theta = wo.z;
     float d = dot3(sn, wo);
     // unit_angle(n, wo) = 2 asin(|wo -/+ n| / 2)
-    float3_ v = mk3(wo.x - mulsignf_(sn.x, d), wo.y - mulsignf_(sn.y, d), wo.z - mulsignf_(sn.z, d));
+    // wo - mulsign(n, d) as fma(-s, n, wo) with s = +/-1: the product is exact, so this
+    // is the reference's subtraction bit for bit, with one select instead of three
+    const float sg = signbit(d) ? -1.f : 1.f;
+    float3_ v = mk3(fmaf(-sg, sn.x, wo.x), fmaf(-sg, sn.y, wo.y), fmaf(-sg, sn.z, wo.z));
     float h = 0.5f * (FAST ? fast_sqrt(dot3(v, v)) : sqrtf(dot3(v, v)));
     t.h = h;
-    float temp = 2.f * asinf(h);
+    float temp = 2.f * (FAST ? asin_half_chord(h) : asinf(h));
     t.gamma = d >= 0.f ? temp : kPi - temp;
     if (FAST) {
         float c = fmaf(-2.f * h, h, 1.f);   // cos(2 asin h) = 1 - 2 h^2 ; cos(pi - x) = -cos x
         t.cg = d >= 0.f ? c : -c;
         t.r = fast_rcp(t.cos_theta + 0.01f);
-        t.sq = fast_sqrt(fmaxf(t.cos_theta, 0.f));
+        t.sq = fast_sqrt(t.cos_theta);   // NaN below the horizon: those lanes are inactive, their output selected to 0
     } else {
         t.cg = cosf(t.gamma);
         t.r = 1.f / (t.cos_theta + 0.01f);
@@ -314,11 +341,11 @@ __device__ __forceinline__ void load_dirs(const float* wx, const float* wy, cons
 // eval(): RGB.  out plane c at out + c * ostride.  sign = -1 for eval(si)
 // (local_wo = M^-1 (-si.wi)), +1 for eval_direction (wi = -ds.d).
 // ======================================================================
-template <int VEC, bool FAST>
+template <int VEC, bool FAST, bool NEG>
 __device__ __forceinline__ void eval_rgb_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                               const float* __restrict__ wy, const float* __restrict__ wz,
                                               const uint8_t* __restrict__ active, size_t n,
-                                              float* __restrict__ out, size_t ostride, float sign) {
+                                              float* __restrict__ out, size_t ostride) {
     const size_t nvec = n / VEC;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
@@ -329,7 +356,7 @@ __device__ __forceinline__ void eval_rgb_body(const SunskyKArgs& K, const float*
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
             float o[3];
-            eval_rgb_local<FAST>(K, K.sun_table, to_local(K, mk3(sign * x[j], sign * y[j], sign * z[j])), m[j], o);
+            eval_rgb_local<FAST>(K, K.sun_table, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j], o);
             r[j] = o[0]; g[j] = o[1]; b[j] = o[2];
         }
         store_vec<VEC>(out, i, r);
@@ -382,11 +409,11 @@ struct LambdaSet {
     float f[kMaxBroadcastLambda];   // < 0: invalid wavelength (output 0)
 };
 
-template <int VEC, bool FAST>
+template <int VEC, bool FAST, bool NEG>
 __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const LambdaSet& L,
                                                      const float* __restrict__ wx, const float* __restrict__ wy,
                                                      const float* __restrict__ wz, const uint8_t* __restrict__ active,
-                                                     size_t n, float* __restrict__ out, size_t ostride, float sign) {
+                                                     size_t n, float* __restrict__ out, size_t ostride) {
     __shared__ ChanLds<FAST> S;
     const auto* chans = stage_chans<FAST>(K, &S);
     __syncthreads();
@@ -401,7 +428,7 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
         bool any_sun = false;
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
-            t[j] = dir_terms<FAST>(K, to_local(K, mk3(sign * x[j], sign * y[j], sign * z[j])), m[j]);
+            t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);
             any_sun |= t[j].hit_sun;
         }
         if (any_sun) {
@@ -444,11 +471,11 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
 
 // Broadcast at exactly the 11 model wavelengths 320:40:720 nm (lerp factor 0,
 // sunsky.cpp:332-343): channel c -> plane c with compile-time channel indices.
-template <int VEC, bool FAST>
+template <int VEC, bool FAST, bool NEG>
 __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                                      const float* __restrict__ wy, const float* __restrict__ wz,
                                                      const uint8_t* __restrict__ active, size_t n,
-                                                     float* __restrict__ out, size_t ostride, float sign) {
+                                                     float* __restrict__ out, size_t ostride) {
     __shared__ ChanLds<FAST> S;
     const auto* chans = stage_chans<FAST>(K, &S);
     __syncthreads();
@@ -463,7 +490,7 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
         bool any_sun = false;
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
-            t[j] = dir_terms<FAST>(K, to_local(K, mk3(sign * x[j], sign * y[j], sign * z[j])), m[j]);
+            t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);
             any_sun |= t[j].hit_sun;
         }
         if (any_sun) {
@@ -494,12 +521,12 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
 // eval(): spectral with per-ray wavelengths (Mitsuba Spectrum<Float, k>):
 // lambda plane k at lam + k * lstride, out plane k at out + k * ostride.
 // ======================================================================
-template <int VEC, bool FAST>
+template <int VEC, bool FAST, bool NEG>
 __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                                     const float* __restrict__ wy, const float* __restrict__ wz,
                                                     const float* __restrict__ lam, size_t lstride, int nlam,
                                                     const uint8_t* __restrict__ active, size_t n,
-                                                    float* __restrict__ out, size_t ostride, float sign) {
+                                                    float* __restrict__ out, size_t ostride) {
     __shared__ ChanLds<FAST> S;
     const auto* chans = stage_chans<FAST>(K, &S);
     __syncthreads();
@@ -519,7 +546,7 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
         DirTerms t[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
-            t[j] = dir_terms<FAST>(K, to_local(K, mk3(sign * x[j], sign * y[j], sign * z[j])), m[j]);
+            t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);
             add_sun_terms<FAST>(K, t[j]);
         }
         for (int k0 = 0; k0 < nlam; k0 += 4) {
@@ -1595,22 +1622,29 @@ __device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const f
 // ======================================================================
 // extern "C" entry points (hipModuleGetFunction names)
 // ======================================================================
-#define SS_EVAL_RGB(NAME, VEC, FAST)                                                                          \
+#define SS_EVAL_RGB(NAME, VEC, FAST, NEG)                                                                          \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
         SunskyKArgs K, const float* wx, const float* wy, const float* wz, const uint8_t* active, size_t n,     \
         float* out, size_t ostride, float sign) {                                                              \
-        eval_rgb_body<VEC, FAST>(K, wx, wy, wz, active, n, out, ostride, sign);                                \
+        (void)sign;                                                                                            \
+        eval_rgb_body<VEC, FAST, NEG>(K, wx, wy, wz, active, n, out, ostride);                                 \
     }
-SS_EVAL_RGB(sunsky_eval_rgb_v4_fast, 4, true)
-SS_EVAL_RGB(sunsky_eval_rgb_v1_fast, 1, true)
-SS_EVAL_RGB(sunsky_eval_rgb_v4_ref, 4, false)
-SS_EVAL_RGB(sunsky_eval_rgb_v1_ref, 1, false)
+// eval(si): wo = -wi (NEG); eval_direction(ds): wo = ds.d (the _dir kernels)
+SS_EVAL_RGB(sunsky_eval_rgb_v4_fast, 4, true, true)
+SS_EVAL_RGB(sunsky_eval_rgb_v1_fast, 1, true, true)
+SS_EVAL_RGB(sunsky_eval_rgb_v4_ref, 4, false, true)
+SS_EVAL_RGB(sunsky_eval_rgb_v1_ref, 1, false, true)
+SS_EVAL_RGB(sunsky_eval_rgb_v4_dir_fast, 4, true, false)
+SS_EVAL_RGB(sunsky_eval_rgb_v1_dir_fast, 1, true, false)
+SS_EVAL_RGB(sunsky_eval_rgb_v4_dir_ref, 4, false, false)
+SS_EVAL_RGB(sunsky_eval_rgb_v1_dir_ref, 1, false, false)
 
 #define SS_EVAL_SPEC_BCAST(NAME, VEC, FAST)                                                                   \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
         SunskyKArgs K, LambdaSet L, const float* wx, const float* wy, const float* wz, const uint8_t* active,  \
         size_t n, float* out, size_t ostride, float sign) {                                                    \
-        eval_spec_bcast_body<VEC, FAST>(K, L, wx, wy, wz, active, n, out, ostride, sign);                      \
+        (void)sign;   /* always eval(si): wo = -wi */                                                         \
+        eval_spec_bcast_body<VEC, FAST, true>(K, L, wx, wy, wz, active, n, out, ostride);                      \
     }
 SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v4_fast, 4, true)
 SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v1_fast, 1, true)
@@ -1622,21 +1656,27 @@ SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v1_ref, 1, false)
         SunskyKArgs K, LambdaSet L, const float* wx, const float* wy, const float* wz, const uint8_t* active,  \
         size_t n, float* out, size_t ostride, float sign) {                                                    \
         (void)L;                                                                                               \
-        eval_spec_nodes_body<VEC, FAST>(K, wx, wy, wz, active, n, out, ostride, sign);                         \
+        (void)sign;                                                                                            \
+        eval_spec_nodes_body<VEC, FAST, true>(K, wx, wy, wz, active, n, out, ostride);                         \
     }
 SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v4_fast, 4, true)
 SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v4_ref, 4, false)
 
-#define SS_EVAL_SPEC_RAYS(NAME, VEC, FAST)                                                                    \
+#define SS_EVAL_SPEC_RAYS(NAME, VEC, FAST, NEG)                                                                    \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
         SunskyKArgs K, const float* wx, const float* wy, const float* wz, const float* lam, size_t lstride,    \
         int nlam, const uint8_t* active, size_t n, float* out, size_t ostride, float sign) {                   \
-        eval_spec_rays_body<VEC, FAST>(K, wx, wy, wz, lam, lstride, nlam, active, n, out, ostride, sign);      \
+        (void)sign;                                                                                            \
+        eval_spec_rays_body<VEC, FAST, NEG>(K, wx, wy, wz, lam, lstride, nlam, active, n, out, ostride);       \
     }
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_fast, 4, true)
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_fast, 1, true)
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_ref, 4, false)
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_ref, 1, false)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_fast, 4, true, true)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_fast, 1, true, true)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_ref, 4, false, true)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_ref, 1, false, true)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_dir_fast, 4, true, false)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_dir_fast, 1, true, false)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_dir_ref, 4, false, false)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_dir_ref, 1, false, false)
 
 #define SS_SAMPLE_DIRECTION(NAME, FAST, SPEC)                                                                 \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \

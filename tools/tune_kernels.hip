@@ -7,7 +7,7 @@
     extern "C" __global__ __launch_bounds__(SS_BLOCK) ATTR void NAME(                                       \
         SunskyKArgs K, const float* wx, const float* wy, const float* wz, const uint8_t* active, size_t n,  \
         float* out, size_t ostride, float sign) {                                                           \
-        eval_rgb_body<VEC, true>(K, wx, wy, wz, active, n, out, ostride, sign);                             \
+        (void)sign; eval_rgb_body<VEC, true, true>(K, wx, wy, wz, active, n, out, ostride);                             \
     }
 #define NOATTR
 TUNE_RGB(tune_rgb_v4_w8, 4, __attribute__((amdgpu_waves_per_eu(8, 8))))
@@ -20,7 +20,7 @@ TUNE_RGB(tune_rgb_v2_w8, 2, __attribute__((amdgpu_waves_per_eu(8, 8))))
         SunskyKArgs K, LambdaSet L, const float* wx, const float* wy, const float* wz, const uint8_t* active,\
         size_t n, float* out, size_t ostride, float sign) {                                                 \
         (void)L;                                                                                            \
-        eval_spec_nodes_body<VEC, true>(K, wx, wy, wz, active, n, out, ostride, sign);                      \
+        (void)sign; eval_spec_nodes_body<VEC, true, true>(K, wx, wy, wz, active, n, out, ostride);                      \
     }
 TUNE_SPEC(tune_spec_nodes_v2_w8, 2, __attribute__((amdgpu_waves_per_eu(8, 8))))
 TUNE_SPEC(tune_spec_nodes_v4, 4, NOATTR)

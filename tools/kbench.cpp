@@ -11,6 +11,7 @@
 // Build: make -C tools kbench
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -180,6 +181,37 @@ int main(int argc, char** argv) {
                         argv[a], mult, grid, us, bytes / (us * 1e-6) / 1e9, (spec ? 11.0 : 1.0) * n / (us * 1e-6),
                         maxrel);
             std::fflush(stdout);
+            // KB_AB=<other.hsaco>: the same kernel from a second code object, timed in
+            // alternating bursts (KB_AB_ROUNDS of them) so clock and thermal drift hit
+            // both alike; prints medians and the median per-round ratio other/this.
+            if (const char* ab = std::getenv("KB_AB")) {
+                hipModule_t mod_b;
+                CK(hipModuleLoad(&mod_b, ab));
+                hipFunction_t fb;
+                CK(hipModuleGetFunction(&fb, mod_b, argv[a]));
+                const int rounds = std::getenv("KB_AB_ROUNDS") ? std::atoi(std::getenv("KB_AB_ROUNDS")) : 20;
+                std::vector<double> ta, tb, ratio;
+                auto burst = [&](hipFunction_t fn) {
+                    CK(hipEventRecord(e0, nullptr));
+                    for (int it = 0; it < iters; ++it)
+                        CK(hipModuleLaunchKernel(fn, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
+                    CK(hipEventRecord(e1, nullptr));
+                    CK(hipEventSynchronize(e1));
+                    float t = 0;
+                    CK(hipEventElapsedTime(&t, e0, e1));
+                    return 1e3 * t / iters;
+                };
+                for (int w = 0; w < 3; ++w) CK(hipModuleLaunchKernel(fb, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
+                for (int r = 0; r < rounds; ++r) {
+                    double x = burst(f), y = burst(fb);
+                    ta.push_back(x); tb.push_back(y); ratio.push_back(y / x);
+                }
+                auto median = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
+                std::printf("  A/B %-30s this %8.2f us  other %8.2f us  median(other/this) %.4f  (%d rounds x %d)\n",
+                            argv[a], median(ta), median(tb), median(ratio), rounds, iters);
+                std::fflush(stdout);
+                CK(hipModuleUnload(mod_b));
+            }
         }
     }
     return 0;

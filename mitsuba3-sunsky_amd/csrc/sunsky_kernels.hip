@@ -97,7 +97,7 @@ __device__ __forceinline__ DirTerms dir_terms(const SunskyKArgs& K, float3_ wo, 
     float temp = 2.f * (FAST ? asin_half_chord(h) : asinf(h));
     t.gamma = d >= 0.f ? temp : kPi - temp;
     if (FAST) {
-        float c = fmaf(-2.f * h, h, 1.f);   // cos(2 asin h) = 1 - 2 h^2 ; cos(pi - x) = -cos x
+        float c = fmaf(h * h, -2.f, 1.f);   // cos(2 asin h) = 1 - 2 h^2 ; cos(pi - x) = -cos x
         t.cg = d >= 0.f ? c : -c;
         t.r = fast_rcp(t.cos_theta + 0.01f);
         t.sq = fast_sqrt(t.cos_theta);   // NaN below the horizon: those lanes are inactive, their output selected to 0

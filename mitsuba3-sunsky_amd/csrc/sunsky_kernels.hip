@@ -58,6 +58,106 @@ __device__ __forceinline__ float asin_half_chord(float x) {
     return fmaf(x * t, p, x);
 }
 
+// atan on [0, 1]: t + t^3 P(t^2), degree 7 in t^2 (tools/fit_atan.py; 1.07 ulp).
+__device__ __forceinline__ float atan_unit(float t) {
+    const float u = t * t;
+    float p = 0.0025049929972738028f;
+    p = fmaf(p, u, -0.014686254784464836f);
+    p = fmaf(p, u, 0.040442489087581635f);
+    p = fmaf(p, u, -0.07314199209213257f);
+    p = fmaf(p, u, 0.1055244505405426f);
+    p = fmaf(p, u, -0.14181630313396454f);
+    p = fmaf(p, u, 0.19990065693855286f);
+    p = fmaf(p, u, -0.3333298861980438f);
+    return fmaf(t * u, p, t);
+}
+
+// FAST atan2 for the TGMM pdf's azimuth: octant reduction t = min / max with
+// v_rcp_f32, atan_unit, then pi/2 - a and pi - a fix-ups (max error 4.4 ulp,
+// 3.5e-7 absolute over the circle; tools/fit_atan.py).  atan2(0, 0) returns a
+// finite value: the callers mask sin(theta) = 0 directions out (sunsky.cpp:717).
+__device__ __forceinline__ float atan2_fast(float y, float x) {
+    const float ax = fabsf(x), ay = fabsf(y);
+    const float t = fminf(fminf(ax, ay) * fast_rcp(fmaxf(ax, ay)), 1.f);
+    float a = atan_unit(t);
+    a = ay > ax ? kHalfPi - a : a;
+    a = x < 0.f ? kPi - a : a;
+    return copysignf(a, y);
+}
+
+// FAST sincos for the sampling transforms (sphdir, the concentric disk): one
+// Cody-Waite reduction by pi/2 (two fp32 constants, fma), then sin r = r + r^3 S(r^2)
+// and cos r = 1 - r^2/2 + r^4 C(r^2) on [-pi/4, pi/4] (tools/fit_sincos.py: max
+// 1.5 ulp, 9.2e-8 absolute for |x| <= 8 pi) and the quadrant swap / signs.  The
+// arguments here stay within a few pi, far from where the two-constant reduction
+// loses bits.
+__device__ __forceinline__ void sincos_fast(float x, float* s, float* c) {
+    const float k = rintf(x * 0.636619772f);
+    float r = fmaf(-k, 1.57079637f, x);
+    r = fmaf(-k, -4.37113883e-8f, r);
+    const float r2 = r * r;
+    float ps = 2.715222990445909e-06f;
+    ps = fmaf(ps, r2, -0.00019838963635265827f);
+    ps = fmaf(ps, r2, 0.008333328180015087f);
+    ps = fmaf(ps, r2, -0.1666666716337204f);
+    float pc = -2.7188141871192784e-07f;
+    pc = fmaf(pc, r2, 2.4799224775051698e-05f);
+    pc = fmaf(pc, r2, -0.001388888224028051f);
+    pc = fmaf(pc, r2, 0.0416666679084301f);
+    const float sn = fmaf(r * r2, ps, r);
+    const float cs = fmaf(r2 * r2, pc, fmaf(-0.5f, r2, 1.f));
+    const int q = (int)k;
+    const float sv = (q & 1) ? cs : sn, cv = (q & 1) ? sn : cs;
+    *s = (q & 2) ? -sv : sv;
+    *c = ((q + 1) & 2) ? -cv : cv;
+}
+
+template <bool FAST>
+__device__ __forceinline__ void sincos_sel(float x, float* s, float* c) {
+    if constexpr (FAST) sincos_fast(x, s, c);
+    else sincosf(x, s, c);
+}
+
+// FAST erfinv: Giles' single-precision polynomials (erfinvf_, sunsky_math.h) with
+// w = -log(1 - x^2) from v_log_f32 (log2) times ln 2 instead of libm's logf.  The
+// result's relative sensitivity to w is ~0.3 dw, so the hardware log's few-ulp
+// error stays at the 1e-7 level.
+__device__ __forceinline__ float erfinv_fast(float x) {
+    float w = -0.693147180559945309f * __builtin_amdgcn_logf(fmaf(x, -x, 1.f)), p;
+    if (w < 5.f) {
+        w = w - 2.5f;
+        p = 2.81022636e-08f;
+        p = fmaf(p, w, 3.43273939e-07f);
+        p = fmaf(p, w, -3.5233877e-06f);
+        p = fmaf(p, w, -4.39150654e-06f);
+        p = fmaf(p, w, 0.00021858087f);
+        p = fmaf(p, w, -0.00125372503f);
+        p = fmaf(p, w, -0.00417768164f);
+        p = fmaf(p, w, 0.246640727f);
+        p = fmaf(p, w, 1.50140941f);
+    } else {
+        w = fast_sqrt(w) - 3.f;
+        p = -0.000200214257f;
+        p = fmaf(p, w, 0.000100950558f);
+        p = fmaf(p, w, 0.00134934322f);
+        p = fmaf(p, w, -0.00367342844f);
+        p = fmaf(p, w, 0.00573950773f);
+        p = fmaf(p, w, -0.0076224613f);
+        p = fmaf(p, w, 0.00943887047f);
+        p = fmaf(p, w, 1.00167406f);
+        p = fmaf(p, w, 2.83297682f);
+    }
+    return p * x;
+}
+
+// Polar angle of an upper-hemisphere direction (unit_angle_z for z >= 0, sunsky.h:87):
+// 2 asin(|v - e_z| / 2), whose half chord is <= sqrt(1/2), so asin_half_chord applies.
+// Lanes with z < 0 get a meaningless finite angle: compute_pdfs masks them.
+__device__ __forceinline__ float theta_upper_fast(float3_ v) {
+    const float dz = v.z - 1.f;
+    return 2.f * asin_half_chord(0.5f * fast_sqrt(fmaf(v.x, v.x, fmaf(v.y, v.y, dz * dz))));
+}
+
 // wo = -wi for eval(si), +d for eval_direction: a compile-time sign folds into
 // the source modifiers of the first use instead of 3 multiplies per direction.
 template <bool NEG>
@@ -206,21 +306,76 @@ __device__ __forceinline__ float render_sun_rgb_compact(const float* table, int 
     return res;
 }
 
+// RGB sun-table segments [K.sun_row_lo, K.sun_row_lo + kSunRowsStaged) in LDS with
+// the three channels interleaved: r[row][k][j] = (S[c=0], S[c=1], S[c=2], 0) of
+// render_sun's 45x3x4x6 table.  One 16-byte LDS read feeds all three channels:
+// a packed FMA for channels 0/1 and a scalar FMA for channel 2, in the same
+// Horner order per channel as render_sun_rgb_compact (bitwise the same values).
+struct SunRowsRgb {
+    float4 r[kSunRowsStaged][kNbSunCtrlPts][kNbSunLdParams];
+};
+
+__device__ __forceinline__ void stage_sun_rows(const SunskyKArgs& K, SunRowsRgb* s) {
+    constexpr int per_row = kNbSunCtrlPts * kNbSunLdParams;
+    for (int e = threadIdx.x; e < kSunRowsStaged * per_row; e += blockDim.x) {
+        const int row = e / per_row, kj = e % per_row;
+        const int pos = min(K.sun_row_lo + row, kNbSunSegments - 1);
+        const float* src = K.sun_table + pos * 3 * per_row + kj;
+        reinterpret_cast<float4*>(s->r)[e] = make_float4(src[0], src[per_row], src[2 * per_row], 0.f);
+    }
+}
+
+__device__ __forceinline__ void render_sun_rgb_rows(const SunRowsRgb& R, int row, float x, float cpsi,
+                                                    float out[3]) {
+    f32x2 res01 = {0.f, 0.f};
+    float res2 = 0.f;
+#pragma unroll 1
+    for (int k = kNbSunCtrlPts - 1; k >= 0; --k) {
+        const float4* q = R.r[row][k];
+        const float4 a = q[kNbSunLdParams - 1];
+        f32x2 in01 = {a.x, a.y};
+        float in2 = a.z;
+#pragma unroll
+        for (int j = kNbSunLdParams - 2; j >= 0; --j) {
+            const float4 b = q[j];
+            in01 = __builtin_elementwise_fma(in01, f32x2{cpsi, cpsi}, f32x2{b.x, b.y});
+            in2 = fmaf(in2, cpsi, b.z);
+        }
+        res01 = __builtin_elementwise_fma(res01, f32x2{x, x}, in01);
+        res2 = fmaf(res2, x, in2);
+    }
+    out[0] = res01.x;
+    out[1] = res01.y;
+    out[2] = res2;
+}
+
 // Full RGB eval for one local direction (sunsky.cpp:317-323).
 // chans: the 3 channels (K.fsky / K.sky, or an LDS copy in the sampling kernels,
 // whose other constants already fill the SGPR file).
 template <bool FAST>
 __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
-                                               const float* sun_tab, float3_ wo, bool mask, float out[3]) {
+                                               const float* sun_tab, float3_ wo, bool mask, float out[3],
+                                               const SunRowsRgb* rows = nullptr) {
     DirTerms t = dir_terms<FAST>(K, wo, mask);
     if constexpr (FAST) {
 #pragma unroll
         for (int c = 0; c < 3; ++c) out[c] = sky_fast(chans[c], t);   // sky_scale and CIE folded
+#ifdef SS_PROBE_NO_SUN_DISC   // probe builds (tools/Makefile) only: cost ablations
+        t.hit_sun = false;
+#endif
         if (t.hit_sun) {
             add_sun_terms<true>(K, t);
+            const int row = t.sun_pos - K.sun_row_lo;
+            if (rows && row >= 0 && row < kSunRowsStaged) {
+                float sr[3];
+                render_sun_rgb_rows(*rows, row, t.sun_x, t.sun_cpsi, sr);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) out[c] += K.sun_mul * sr[c];
+            } else {
 #pragma unroll 1
-            for (int c = 0; c < 3; ++c)
-                out[c] += K.sun_mul * render_sun_rgb_compact(sun_tab, t.sun_pos, c, t.sun_x, t.sun_cpsi);
+                for (int c = 0; c < 3; ++c)
+                    out[c] += K.sun_mul * render_sun_rgb_compact(sun_tab, t.sun_pos, c, t.sun_x, t.sun_cpsi);
+            }
         }
 #pragma unroll
         for (int c = 0; c < 3; ++c) out[c] = t.active ? out[c] : 0.f;
@@ -570,31 +725,51 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
 // ======================================================================
 // Sampling: TGMM sky + uniform-cone sun (sunsky.cpp:354-451, 661-763)
 // ======================================================================
-// TGMM tables in LDS.  tg/tc are the FAST form of tgmm_pdf's per-gaussian
-// terms: tg = {mu_phi, mu_theta, c / sigma_phi, c / sigma_theta} with
-// c = sqrt(log2(e) / 2), tc = weight / (volume * 2 pi), so that a gaussian
-// costs exp2(-(sx^2 + sy^2)) and one fma.
-// tg/tc/tref hold only the K.tgmm_count gaussians with a non-zero coefficient
+// TGMM tables in LDS.  tp holds the FAST form of tgmm_pdf's per-gaussian terms
+// in PAIRS of gaussians (g, g + 1), each field a float2 so the pair's arithmetic
+// runs as packed FP32 (v_pk_add/mul/fma_f32: two lanes' worth per issue):
+//   sx = (phi - mu_phi) k_phi,  sy = (theta - mu_theta) k_theta,
+//   pdf += c exp2(-(sx^2 + sy^2)),
+// with k = sqrt(log2(e) / 2) / sigma and c = weight / (volume * 2 pi).  The
+// packed ops are IEEE fp32 like their scalar forms and the accumulation into
+// pdf stays one fma per gaussian in mixture order, so the result is bitwise
+// that of the scalar loop.  An odd count is padded with a zero gaussian
+// (k = 0, c = 0: fma(0, exp2(-0), pdf) = pdf exactly).
+// tp/tref hold only the K.tgmm_count gaussians with a non-zero coefficient
 // (SunskyKArgs::tgmm_idx), so tgmm_pdf loops over those.
+struct TgPair {
+    f32x2 mphi, mth, kphi, kth, c;
+};
+
 struct TgmmLds {
     Gaussian gauss[kNbMixture];                  // full mixture: sample_sky
-    float4 tg[kNbMixture];
-    float tc[kNbMixture];
+    TgPair tp[kNbMixture / 2];
     Gaussian tref[kNbMixture];                   // compacted, reference-order tgmm_pdf
     float cdf[kNbMixture], pmf[kNbMixture];
+    uint8_t guide[kGaussGuideSize];
 };
 
 __device__ __forceinline__ void stage_tgmm(const SunskyKArgs& K, TgmmLds* s) {
     lds_copy(s->gauss, K.gauss, kNbMixture);
     lds_copy(s->cdf, K.gauss_cdf, kNbMixture);
     lds_copy(s->pmf, K.gauss_pmf, kNbMixture);
+    lds_copy(reinterpret_cast<uint32_t*>(s->guide), reinterpret_cast<const uint32_t*>(K.gauss_guide),
+             kGaussGuideSize / 4);
     const int i = threadIdx.x;
-    if (i < K.tgmm_count) {
+    if (i < kNbMixture) {
         const float c = 0.84932180028801904272f;   // sqrt(log2(e) / 2)
-        const Gaussian& g = K.gauss[K.tgmm_idx[i]];
-        s->tg[i] = make_float4(g.mu_phi, g.mu_theta, g.inv_sigma_phi * c, g.inv_sigma_theta * c);
-        s->tc[i] = g.coef * kInvTwoPi;
-        s->tref[i] = g;
+        float* pair = reinterpret_cast<float*>(&s->tp[i >> 1]) + (i & 1);
+        if (i < K.tgmm_count) {
+            const Gaussian& g = K.gauss[K.tgmm_idx[i]];
+            pair[0] = g.mu_phi;
+            pair[2] = g.mu_theta;
+            pair[4] = g.inv_sigma_phi * c;
+            pair[6] = g.inv_sigma_theta * c;
+            pair[8] = g.coef * kInvTwoPi;
+            s->tref[i] = g;
+        } else {
+            pair[0] = pair[2] = pair[4] = pair[6] = pair[8] = 0.f;
+        }
     }
 }
 
@@ -603,7 +778,8 @@ struct SamplerLds {
     TgmmLds tgmm;
     ChanLds<FAST> chans;                          // spectral weights (per-lane channel index)
     SpecDistLds sdist;
-    float sun[SPEC ? kSunSpecTableSize : kSunRgbTableSize];
+    float sun[SPEC ? kSunSpecTableSize : 4];      // spectral: the whole turbidity-lerped table
+    SunRowsRgb rows[SPEC ? 0 : 1];                // RGB: the disc's segments, channels interleaved
     float ld[kNbWavelengths * kNbSunLdParams];
 };
 
@@ -615,32 +791,38 @@ __device__ __forceinline__ void stage_sampler_lds(const SunskyKArgs& K, SamplerL
         stage_spec_dist(K, &s->sdist);
         lds_copy(s->ld, K.sun_ld, kNbWavelengths * kNbSunLdParams);
     }
-    lds_copy(s->sun, K.sun_table, SPEC ? kSunSpecTableSize : kSunRgbTableSize);
+    if constexpr (SPEC) lds_copy(s->sun, K.sun_table, kSunSpecTableSize);
+    else stage_sun_rows(K, s->rows);
     __syncthreads();
 }
 
 // DiscreteDistribution::sample_reuse (distr_1d.h:173-183): JIT predicate
-// ((cdf < s) || cdf == 0) && cdf != sum over [0, n-1] (:116-136) -- a prefix
-// count against the broadcast CDF; scalar variants search [first, last].
+// ((cdf < s) || cdf == 0) && cdf != sum over [0, n-1) (:116-136), scalar
+// variants search [first, last] with cdf < s.  Both predicates are true on a
+// prefix of the entries and monotone in s, so the index is a prefix count that
+// starts from the host's guide-table bound for the sample's bucket
+// (SunskyKArgs::gauss_guide) and tests at most gauss_guide_span further entries:
+// the same result as the full scan, ~1-2 LDS reads per lane instead of 19.
 template <bool FAST>
 __device__ __forceinline__ int discrete_sample_reuse(const SunskyKArgs& K, const TgmmLds& T, float value,
                                                      float* reused) {
     const float s = value * K.gauss_sum;
-    int idx;
-    if (K.semantics == kJit) {
-        idx = 0;
-        bool run = true;
-#pragma unroll 4
-        for (int i = 0; i < kNbMixture - 1; ++i) {
-            const float c = T.cdf[i];
-            run = run && ((c < s) || c == 0.f) && (c != K.gauss_sum);
-            idx += run ? 1 : 0;
-        }
-    } else {
-        idx = K.gauss_first;
-#pragma unroll 4
-        for (int i = 0; i < kNbMixture; ++i)
-            if (i >= K.gauss_first && i < K.gauss_last && T.cdf[i] < s) idx = i + 1;
+    const bool jit = K.semantics == kJit;
+    const int end = jit ? kNbMixture - 1 : K.gauss_last;
+    int idx, cnt;
+    if (value >= 0.f && value < 1.f) {
+        idx = T.guide[(int)(value * (float)kGaussGuideSize)];
+        cnt = K.gauss_guide_span;
+    } else {   // outside [0, 1) (or NaN): the full search
+        idx = jit ? 0 : K.gauss_first;
+        cnt = kNbMixture;
+    }
+    for (int k = 0; k < cnt; ++k) {
+        if (idx >= end) break;
+        const float c = T.cdf[idx];
+        const bool p = jit ? (((c < s) || c == 0.f) && (c != K.gauss_sum)) : (c < s);
+        if (!p) break;
+        ++idx;
     }
     const float pmf = T.pmf[idx];
     const float cdf_prev = idx > 0 ? T.cdf[idx - 1] : 0.f;
@@ -649,10 +831,11 @@ __device__ __forceinline__ int discrete_sample_reuse(const SunskyKArgs& K, const
 }
 
 // sphdir(theta, phi) with shared sin/cos reductions
+template <bool FAST>
 __device__ __forceinline__ float3_ sphdir_dev(float theta, float phi) {
     float st, ct, sp, cp;
-    sincosf(theta, &st, &ct);
-    sincosf(phi, &sp, &cp);
+    sincos_sel<FAST>(theta, &st, &ct);
+    sincos_sel<FAST>(phi, &sp, &cp);
     return mk3(cp * st, sp * st, ct);
 }
 
@@ -666,17 +849,19 @@ __device__ __forceinline__ float3_ sample_sky(const SunskyKArgs& K, const TgmmLd
     float sy = lerpf_(g.cdf_a_theta, g.cdf_b_theta, uy);
     sx = fminf(fmaxf(sx, kEpsilon), kOneMinusEpsilon);
     sy = fminf(fmaxf(sy, kEpsilon), kOneMinusEpsilon);
-    float phi = kSqrtTwo * erfinvf_(2.f * sx - 1.f) * g.sigma_phi + g.mu_phi;
-    float theta = kSqrtTwo * erfinvf_(2.f * sy - 1.f) * g.sigma_theta + g.mu_theta;
+    const float ex = FAST ? erfinv_fast(2.f * sx - 1.f) : erfinvf_(2.f * sx - 1.f);
+    const float ey = FAST ? erfinv_fast(2.f * sy - 1.f) : erfinvf_(2.f * sy - 1.f);
+    float phi = kSqrtTwo * ex * g.sigma_phi + g.mu_phi;
+    float theta = kSqrtTwo * ey * g.sigma_theta + g.mu_theta;
     phi += K.sun_phi - 0.5f * kPi;
     theta = fminf(theta, 0.5f * kPi - kEpsilon);
-    return sphdir_dev(theta, phi);
+    return sphdir_dev<FAST>(theta, phi);
 }
 
-// square_to_uniform_cone (warp.h:533-551) with the concentric disk of
-// warp.h:54-90 using one shared sin/cos reduction.
+// square_to_uniform_disk_concentric (warp.h:54-90) with one shared sin/cos
+// reduction (FAST: v_rcp_f32 division and sincos_fast).
 template <bool FAST>
-__device__ __forceinline__ float3_ uniform_cone_dev(float sx, float sy, float cos_cutoff) {
+__device__ __forceinline__ void disk_concentric_dev(float sx, float sy, float* px, float* py) {
     float x = fmaf(2.f, sx, -1.f), y = fmaf(2.f, sy, -1.f);
     bool is_zero = (x == 0.f) && (y == 0.f);
     bool q13 = fabsf(x) < fabsf(y);
@@ -685,8 +870,16 @@ __device__ __forceinline__ float3_ uniform_cone_dev(float sx, float sy, float co
     if (q13) phi = 0.5f * kPi - phi;
     if (is_zero) phi = 0.f;
     float s, c;
-    sincosf(phi, &s, &c);
-    float px = r * c, py = r * s;
+    sincos_sel<FAST>(phi, &s, &c);
+    *px = r * c;
+    *py = r * s;
+}
+
+// square_to_uniform_cone (warp.h:533-551)
+template <bool FAST>
+__device__ __forceinline__ float3_ uniform_cone_dev(float sx, float sy, float cos_cutoff) {
+    float px, py;
+    disk_concentric_dev<FAST>(sx, sy, &px, &py);
     float omc = 1.f - cos_cutoff;
     float pn = fmaf(px, px, py * py);
     float z = cos_cutoff + omc * (1.f - pn);
@@ -699,6 +892,23 @@ template <bool FAST>
 __device__ __forceinline__ float3_ sample_sun(const SunskyKArgs& K, float ux, float uy) {
     return frame_to_world(mk3(K.sun_s[0], K.sun_s[1], K.sun_s[2]), mk3(K.sun_t[0], K.sun_t[1], K.sun_t[2]),
                           mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), uniform_cone_dev<FAST>(ux, uy, K.cos_cutoff));
+}
+
+// The FAST mixture sum of tgmm_pdf at a wrapped (phi, theta): one PAIR of
+// gaussians per iteration, sx / sy / q as packed FP32 for both, then one fma per
+// gaussian in mixture order.
+__device__ __forceinline__ float tgmm_sum_fast(const SunskyKArgs& K, const TgmmLds& T, float phi, float theta) {
+    float pdf = 0.f;
+    const int np = (K.tgmm_count + 1) >> 1;
+#pragma unroll 2
+    for (int p = 0; p < np; ++p) {
+        const TgPair P = T.tp[p];
+        const f32x2 sx = (phi - P.mphi) * P.kphi, sy = (theta - P.mth) * P.kth;
+        const f32x2 q = __builtin_elementwise_fma(sy, sy, sx * sx);
+        pdf = fmaf(P.c.x, fast_exp2(-q.x), pdf);
+        pdf = fmaf(P.c.y, fast_exp2(-q.y), pdf);
+    }
+    return pdf;
 }
 
 // tgmm_pdf, sunsky.cpp:732-763, with the per-gaussian truncation volume hoisted
@@ -714,12 +924,7 @@ __device__ __forceinline__ float tgmm_pdf(const SunskyKArgs& K, const TgmmLds& T
     // Partially unrolled so the 20 gaussians' LDS reads are not hoisted out of
     // the ray loop into ~100 VGPRs.
     if constexpr (FAST) {
-#pragma unroll 4
-        for (int i = 0; i < K.tgmm_count; ++i) {
-            const float4 a = T.tg[i];
-            float sx = (phi - a.x) * a.z, sy = (theta - a.y) * a.w;
-            pdf = fmaf(T.tc[i], fast_exp2(-fmaf(sy, sy, sx * sx)), pdf);
-        }
+        pdf = tgmm_sum_fast(K, T, phi, theta);
     } else {
 #pragma unroll 4
         for (int i = 0; i < K.tgmm_count; ++i) {
@@ -739,7 +944,14 @@ __device__ __forceinline__ void compute_pdfs(const SunskyKArgs& K, const TgmmLds
     float sin_theta = safe_sqrtf_(fmaf(d.x, d.x, d.y * d.y));
     active = active && (d.z >= 0.f) && (sin_theta != 0.f);
     sin_theta = fmaxf(sin_theta, kEpsilon);
-    float phi = atan2f(d.y, d.x), theta = unit_angle_z(d);
+    float phi, theta;
+    if constexpr (FAST) {
+        phi = atan2_fast(d.y, d.x);
+        theta = theta_upper_fast(d);
+    } else {
+        phi = atan2f(d.y, d.x);
+        theta = unit_angle_z(d);
+    }
     *sky_pdf = fdiv<FAST>(tgmm_pdf<FAST>(K, T, phi, theta, active), sin_theta);
     float cosg = dot3(mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), d);
     *sun_pdf = (!check_sun || cosg >= K.cos_cutoff) ? K.sun_pdf : 0.f;
@@ -842,7 +1054,7 @@ __device__ __forceinline__ void sample_direction_body(
         if constexpr (!SPEC) {
             float e[3];
 #ifndef SS_PROBE_NO_WEIGHT
-            eval_rgb_local<FAST>(K, S.chans.c, S.sun, wo, act, e);
+            eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, wo, act, e, S.rows);
 #else
             e[0] = wo.x; e[1] = wo.y; e[2] = wo.z;
 #endif
@@ -891,24 +1103,47 @@ __device__ __forceinline__ void pdf_direction_body(const SunskyKArgs& K, const f
             float st = safe_sqrtf_(fmaf(d.x, d.x, d.y * d.y));
             bool a = (d.z >= 0.f) && (st != 0.f);
             sin_theta[j] = fmaxf(st, kEpsilon);
-            float ph = atan2f(d.y, d.x) - (K.sun_phi - 0.5f * kPi);
+            float ph = (FAST ? atan2_fast(d.y, d.x) : atan2f(d.y, d.x)) - (K.sun_phi - 0.5f * kPi);
             ph = ph < 0.f ? ph + kTwoPi : ph;
             phi[j] = ph > kTwoPi ? ph - kTwoPi : ph;
-            theta[j] = unit_angle_z(d);
+            theta[j] = FAST ? theta_upper_fast(d) : unit_angle_z(d);
             ok[j] = a && (theta[j] >= 0.f) && (theta[j] <= 0.5f * kPi);
             sunp[j] = dot3(sn, d) >= K.cos_cutoff ? K.sun_pdf : 0.f;
             acc[j] = 0.f;
         }
         if constexpr (FAST) {
-#pragma unroll 2
-            for (int g = 0; g < K.tgmm_count; ++g) {
-                const float4 a = T.tg[g];
-                const float c = T.tc[g];
+            static_assert(VEC % 2 == 0 || VEC == 1, "direction pairs");
+            if constexpr (VEC == 1) {
+                acc[0] = tgmm_sum_fast(K, T, phi[0], theta[0]);
+            } else {
+                // directions in pairs: each gaussian's sx, sy, q and the accumulation
+                // run as packed FP32 over two directions (bitwise the scalar loop)
+                constexpr int NP = VEC / 2;
+                f32x2 ph2[NP], th2[NP], ac2[NP];
 #pragma unroll
-                for (int j = 0; j < VEC; ++j) {
-                    float sx = (phi[j] - a.x) * a.z, sy = (theta[j] - a.y) * a.w;
-                    acc[j] = fmaf(c, fast_exp2(-fmaf(sy, sy, sx * sx)), acc[j]);
+                for (int j = 0; j < NP; ++j) {
+                    ph2[j] = f32x2{phi[2 * j], phi[2 * j + 1]};
+                    th2[j] = f32x2{theta[2 * j], theta[2 * j + 1]};
+                    ac2[j] = f32x2{0.f, 0.f};
                 }
+                const int np = (K.tgmm_count + 1) >> 1;
+#pragma unroll 1
+                for (int p = 0; p < np; ++p) {
+                    const TgPair P = T.tp[p];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const float mphi = P.mphi[h], mth = P.mth[h], kphi = P.kphi[h], kth = P.kth[h], c = P.c[h];
+#pragma unroll
+                        for (int j = 0; j < NP; ++j) {
+                            const f32x2 sx = (ph2[j] - mphi) * kphi, sy = (th2[j] - mth) * kth;
+                            const f32x2 q = __builtin_elementwise_fma(sy, sy, sx * sx);
+                            const f32x2 e = f32x2{fast_exp2(-q.x), fast_exp2(-q.y)};
+                            ac2[j] = __builtin_elementwise_fma(f32x2{c, c}, e, ac2[j]);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < NP; ++j) { acc[2 * j] = ac2[j].x; acc[2 * j + 1] = ac2[j].y; }
             }
         } else {
 #pragma unroll 2
@@ -983,7 +1218,7 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool act = active ? active[i] != 0 : true;
         float offx, offy;
-        disk_concentric(s2x[i], s2y[i], &offx, &offy);
+        disk_concentric_dev<FAST>(s2x[i], s2y[i], &offx, &offy);
         const float sx = s3x[i], sy = s3y[i];
         const bool pick_sky = sx < K.w_sky;
         float3_ d;
@@ -1000,7 +1235,7 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
         float w[4];
         int nw;
         if constexpr (!SPEC) {
-            eval_rgb_local<FAST>(K, S.chans.c, S.sun, wo, act, w);
+            eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, wo, act, w, S.rows);
             nw = 3;
             for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = 0.f;
         } else {
@@ -1106,7 +1341,7 @@ __device__ __forceinline__ void direct_diffuse_body(
                 const float3_ wo = to_local(K, d);
                 if constexpr (!SPEC) {
                     float e[3];
-                    eval_rgb_local<FAST>(K, S.chans.c, S.sun, wo, act, e);
+                    eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, wo, act, e, S.rows);
 #pragma unroll
                     for (int c = 0; c < 3; ++c) {
                         const float w = e[c] / pd;
@@ -1125,7 +1360,7 @@ __device__ __forceinline__ void direct_diffuse_body(
             }
             // ---- BSDF sampling: square_to_cosine_hemisphere (warp.h:412-420), then the miss
             float px, py;
-            disk_concentric(u2, u3, &px, &py);
+            disk_concentric_dev<FAST>(u2, u3, &px, &py);
             const float lz = safe_sqrtf_(1.f - fmaf(px, px, py * py));
             const float bpdf = kInvPi * lz;
             if (bpdf > 0.f) {
@@ -1138,7 +1373,7 @@ __device__ __forceinline__ void direct_diffuse_body(
                 const bool up = wo.z >= 0.f;
                 if constexpr (!SPEC) {
                     float e[3];
-                    eval_rgb_local<FAST>(K, S.chans.c, S.sun, wo, up, e);
+                    eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, wo, up, e, S.rows);
 #pragma unroll
                     for (int c = 0; c < 3; ++c) acc[c] = fmaf(e[c], mis, acc[c]);
                 } else {

@@ -438,6 +438,16 @@ void SunskyModel::stage() {
                      : sun_scale_ * k_.area_ratio;
     // ---------------- sun radiance (compute_sun_params)
     compute_sun_params(sun_rad_ds_, spec ? kSunSpecTableSize : kSunRgbTableSize, turbidity_, &sun_table_);
+    {
+        // Lowest segment of render_sun's search (sunsky.cpp:579-587) over the elevations of
+        // directions inside the disc, [eta - aperture / 2, eta + aperture / 2], with a margin
+        // far above fp32 rounding: the sampling kernels stage kSunRowsStaged segments from
+        // here (a lane outside them reads the device table).
+        const double lo = std::max(0.0, (double)eta - (double)sun_half_aperture_ - 1e-3);
+        const double seg = std::cbrt(2.0 * std::min(lo, 0.5 * 3.14159265358979323846) / 3.14159265358979323846) *
+                           (double)kNbSunSegments;
+        k_.sun_row_lo = std::min((int)std::floor(seg), kNbSunSegments - 1);
+    }
 
     // ---------------- TGMM, sunsky.h:438-501
     {
@@ -503,11 +513,47 @@ void SunskyModel::stage() {
         }
         k_.gauss_sum = k_.gauss_cdf[k_.gauss_last];
         k_.gauss_norm = 1.f / k_.gauss_sum;
+        build_gauss_guide();
     }
 
     k_.sun_table = nullptr;   // device pointers are patched in by the C-ABI layer
     k_.sun_ld = nullptr;
     estimate_sky_sun_ratio();
+}
+
+// Index returned by the kernels' discrete_sample_reuse for s = value * sum:
+// JIT, the prefix count of ((cdf < s) || cdf == 0) && cdf != sum over [0, n-1)
+// (distr_1d.h:116-136); scalar, first + #{i in [first, last) : cdf[i] < s}.
+// Both are monotone in s (cdf is non-decreasing).
+int SunskyModel::gauss_search(float s) const {
+    if (semantics_ == kJit) {
+        int idx = 0;
+        for (int i = 0; i < kNbMixture - 1; ++i) {
+            const float c = k_.gauss_cdf[i];
+            if (!(((c < s) || c == 0.f) && (c != k_.gauss_sum))) break;
+            ++idx;
+        }
+        return idx;
+    }
+    int idx = k_.gauss_first;
+    for (int i = k_.gauss_first; i < k_.gauss_last; ++i)
+        if (k_.gauss_cdf[i] < s) idx = i + 1;
+    return idx;
+}
+
+// Guide table for the device search (SunskyKArgs::gauss_guide).  For value in
+// [b/B, (b+1)/B) the fp32 product s = value * sum lies in [fl(b/B sum),
+// fl((b+1)/B sum)] (rounding is monotone; b/B is exact), so the index lies in
+// [search(s_lo), search(s_hi)].
+void SunskyModel::build_gauss_guide() {
+    int span = 0;
+    for (int b = 0; b < kGaussGuideSize; ++b) {
+        const float v0 = (float)b / (float)kGaussGuideSize, v1 = (float)(b + 1) / (float)kGaussGuideSize;
+        const int lo = gauss_search(v0 * k_.gauss_sum), hi = gauss_search(v1 * k_.gauss_sum);
+        k_.gauss_guide[b] = (uint8_t)lo;
+        span = std::max(span, hi - lo);
+    }
+    k_.gauss_guide_span = span;
 }
 
 // estimate_sky_sun_ratio, sunsky.cpp:772-886

@@ -68,6 +68,8 @@ private:
     void extract_albedo(const Properties& props);
     void update_angles(const float local_sun[3]);
     void stage();                 // radiance + sun + TGMM + sampling weight
+    int gauss_search(float s) const;
+    void build_gauss_guide();
     void estimate_sky_sun_ratio();
     void validate() const;
 

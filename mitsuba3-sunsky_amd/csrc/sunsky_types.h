@@ -39,6 +39,8 @@ constexpr int kSunRgbTableSize = kNbSunSegments * 3 * kNbSunCtrlPts * kNbSunLdPa
 constexpr int kSunSpecTableSize = kNbSunSegments * kNbWavelengths * kNbSunCtrlPts;       // 1980
 constexpr int kMaxLambdaPerRay = 16;   // Mitsuba uses 4 (Spectrum<Float, 4>)
 constexpr int kMaxBroadcastLambda = 32;
+constexpr int kGaussGuideSize = 256;   // CDF-inversion guide buckets (power of two)
+constexpr int kSunRowsStaged = 8;      // RGB sun-table segments staged for the disc (sampling kernels)
 
 enum Variant : int { kRGB = 0, kSpectral = 1 };
 enum Semantics : int { kJit = 0, kScalar = 1 };
@@ -99,12 +101,19 @@ struct SunskyKArgs {
     float sun_mul;           // sun_scale * area_ratio (* SPEC_TO_RGB_SUN_CONV * CIE_Y_NORMALIZATION for RGB)
     const float* sun_table;  // device: 45x3x4x6 (RGB) or 45x11x4 (spectral), turbidity-lerped
     const float* sun_ld;     // device: 11x6 limb darkening (spectral only)
+    int   sun_row_lo;        // first elevation segment a direction inside the sun disc can reach
     // -------- sky sampling (TGMM + DiscreteDistribution)
     Gaussian gauss[kNbMixture];
     float gauss_cdf[kNbMixture];   // unnormalised inclusive prefix sum
     float gauss_pmf[kNbMixture];
     float gauss_sum, gauss_norm;
     int   gauss_first, gauss_last; // scalar-variant search bounds (distr_1d.h:233-265)
+    // Guide table of the CDF inversion: for value in [b/256, (b+1)/256) the sampled
+    // index lies in [gauss_guide[b], gauss_guide[b] + gauss_guide_span] (the search
+    // predicate is monotone in value), so a lane tests at most gauss_guide_span
+    // entries instead of all 20.  Same predicate, same result.
+    int   gauss_guide_span;
+    uint8_t gauss_guide[kGaussGuideSize];
     // tgmm_pdf terms with a non-zero coefficient, in mixture order: a gaussian whose
     // corner weight is 0 (integer turbidity / table-node elevation) adds exactly +0
     int   tgmm_count;

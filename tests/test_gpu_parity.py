@@ -219,6 +219,77 @@ def test_sample_direction_and_pdf_parity(variant, semantics, precision):
     assert_parity(gw, wref32, wref64, inside_sun, rtol=2e-5)
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("elev_deg", [0.1, 0.6, 3.0, 20.0, 60.0, 89.5])
+def test_sun_disc_weights_across_elevations(elev_deg, precision):
+    """Sun-picked samples (sunsky.cpp:697-701) at sun elevations whose disc spans one to
+    many of render_sun's 45 segments: the sampling kernels read the disc's segments from
+    LDS (SunskyKArgs::sun_row_lo, kSunRowsStaged) and fall back to the device table for a
+    disc wider than the staged rows (low sun).  Weights vs eval / pdf of the oracle."""
+    d = angles_dict(3.0, 0.4, np.deg2rad(90.0 - elev_deg), 0.3, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, "rgb", "jit", precision=precision)
+    o32, o64 = O.Oracle(d, "rgb", "jit", "f32"), O.Oracle(d, "rgb", "jit", "f64")
+    w_o = em.sky_sampling_w
+    rng = np.random.default_rng(11)
+    n = 1 << 14
+    u = rng.random((n, 2), dtype=np.float32)
+    u[:, 0] = (w_o + (1 - w_o) * u[:, 0]).astype(np.float32)
+    u = u[u[:, 0] > w_o]
+    ds, w = em.sample_direction(ss.Interaction3f(), soa(u))
+    gd, gp, gw = host(ds.d).T, host(ds.pdf), host(w).T
+    info = o32.info()
+    inside = (gd @ info["sun_dir_local"]) >= info["cos_cutoff"]
+    up = gd[:, 2] >= 0
+    assert inside[up].mean() > 0.99
+    e32, e64 = o32.eval(-gd), o64.eval(-gd)
+    wref32 = (e32 / gp[:, None]).astype(np.float32)
+    wref64 = e64 / gp[:, None].astype(np.float64)
+    # cone samples the fp32 disc test puts just outside the disc sit at the horizon for a
+    # low sun, where exp(B / (cos theta + 0.01)) is ill-conditioned: compare the disc lanes
+    keep = up & (gp > 0) & inside
+    g, a, b = gw[keep].astype(np.float64), wref32[keep].astype(np.float64), wref64[keep]
+    # The sun's blue channel at a low sun is a near-cancelling sum of 24 polynomial terms
+    # of the size of the lane's largest channel: its rounding floor is relative to that.
+    scale = np.maximum(np.abs(b), 1e-2 * np.abs(b).max(axis=1, keepdims=True))
+    bound = 2e-5 * scale + 4 * np.abs(a - b) + 1e-30
+    worst = (np.abs(g - b) / bound).max()
+    assert worst <= 1.0, f"sun-disc weights {worst:.2f}x over bound"
+
+
+@pytest.mark.parametrize("turb", [3.0, 4.5])
+@pytest.mark.parametrize("semantics", ["jit", "scalar"])
+def test_discrete_inversion_at_guide_and_cdf_edges(semantics, turb):
+    """The device CDF inversion starts from a guide-table bound (SunskyKArgs::gauss_guide):
+    samples at every guide-bucket edge and a few ulps around every CDF entry pick the
+    same gaussian as the oracle's full search (distr_1d.h:116-183)."""
+    d = angles_dict(turb, 0.7, np.deg2rad(33), 0.3, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, "rgb", semantics)
+    o32 = O.Oracle(d, "rgb", semantics, "f32")
+    w = np.float32(em.sky_sampling_w)
+    o32.override_w_sky(float(w))
+    info = o32.info()
+    cdf = info["gauss_cdf"].astype(np.float32)
+    tot = np.float32(info["gauss_sum"])
+    edges = np.arange(257, dtype=np.float32) / np.float32(256)
+    vals = [edges, np.nextafter(edges, np.float32(0))]
+    for k in range(-3, 4):
+        e = (cdf / tot).astype(np.float32)
+        for _ in range(abs(k)):
+            e = np.nextafter(e, np.float32(np.sign(k) * 2))
+        vals.append(e)
+    v = np.concatenate(vals).astype(np.float32)
+    v = v[(v >= 0) & (v < 1)]
+    ux = np.concatenate([(v * w).astype(np.float32), np.nextafter((v * w).astype(np.float32), np.float32(0))])
+    ux = ux[(ux >= 0) & (ux < w)]
+    rng = np.random.default_rng(3)
+    u = np.stack([ux, rng.random(ux.size, dtype=np.float32)], axis=1)
+    ds, _ = em.sample_direction(ss.Interaction3f(), soa(u))
+    gd = host(ds.d).T
+    ref = o32.sample_direction(u)
+    # a different gaussian moves the direction by O(0.1); rounding near erfinv's poles by < 1e-4
+    assert np.abs(gd - ref["d"]).max() < 1e-3
+
+
 @pytest.mark.parametrize("variant", ["rgb", "spectral"])
 def test_sample_ray_parity(variant):
     d = angles_dict(4.0, 0.3, np.deg2rad(40), 0.3, 1.0, 1.0)

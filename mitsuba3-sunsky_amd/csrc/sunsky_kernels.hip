@@ -308,9 +308,9 @@ __device__ __forceinline__ float render_sun_rgb_compact(const float* table, int 
 
 // RGB sun-table segments [K.sun_row_lo, K.sun_row_lo + kSunRowsStaged) in LDS with
 // the three channels interleaved: r[row][k][j] = (S[c=0], S[c=1], S[c=2], 0) of
-// render_sun's 45x3x4x6 table.  One 16-byte LDS read feeds all three channels:
-// a packed FMA for channels 0/1 and a scalar FMA for channel 2, in the same
-// Horner order per channel as render_sun_rgb_compact (bitwise the same values).
+// render_sun's 45x3x4x6 table.  One 16-byte LDS read feeds all three channels'
+// FMAs, in the same Horner order per channel as render_sun_rgb_compact (bitwise
+// the same values).
 struct SunRowsRgb {
     float4 r[kSunRowsStaged][kNbSunCtrlPts][kNbSunLdParams];
 };
@@ -327,26 +327,26 @@ __device__ __forceinline__ void stage_sun_rows(const SunskyKArgs& K, SunRowsRgb*
 
 __device__ __forceinline__ void render_sun_rgb_rows(const SunRowsRgb& R, int row, float x, float cpsi,
                                                     float out[3]) {
-    f32x2 res01 = {0.f, 0.f};
-    float res2 = 0.f;
+    float r0 = 0.f, r1 = 0.f, r2 = 0.f;
 #pragma unroll 1
     for (int k = kNbSunCtrlPts - 1; k >= 0; --k) {
         const float4* q = R.r[row][k];
         const float4 a = q[kNbSunLdParams - 1];
-        f32x2 in01 = {a.x, a.y};
-        float in2 = a.z;
+        float i0 = a.x, i1 = a.y, i2 = a.z;
 #pragma unroll
         for (int j = kNbSunLdParams - 2; j >= 0; --j) {
             const float4 b = q[j];
-            in01 = __builtin_elementwise_fma(in01, f32x2{cpsi, cpsi}, f32x2{b.x, b.y});
-            in2 = fmaf(in2, cpsi, b.z);
+            i0 = fmaf(i0, cpsi, b.x);
+            i1 = fmaf(i1, cpsi, b.y);
+            i2 = fmaf(i2, cpsi, b.z);
         }
-        res01 = __builtin_elementwise_fma(res01, f32x2{x, x}, in01);
-        res2 = fmaf(res2, x, in2);
+        r0 = fmaf(r0, x, i0);
+        r1 = fmaf(r1, x, i1);
+        r2 = fmaf(r2, x, i2);
     }
-    out[0] = res01.x;
-    out[1] = res01.y;
-    out[2] = res2;
+    out[0] = r0;
+    out[1] = r1;
+    out[2] = r2;
 }
 
 // Full RGB eval for one local direction (sunsky.cpp:317-323).
@@ -726,15 +726,14 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
 // Sampling: TGMM sky + uniform-cone sun (sunsky.cpp:354-451, 661-763)
 // ======================================================================
 // TGMM tables in LDS.  tp holds the FAST form of tgmm_pdf's per-gaussian terms
-// in PAIRS of gaussians (g, g + 1), each field a float2 so the pair's arithmetic
-// runs as packed FP32 (v_pk_add/mul/fma_f32: two lanes' worth per issue):
+// for PAIRS of gaussians (g, g + 1), so one 40-byte LDS read serves two terms:
 //   sx = (phi - mu_phi) k_phi,  sy = (theta - mu_theta) k_theta,
 //   pdf += c exp2(-(sx^2 + sy^2)),
-// with k = sqrt(log2(e) / 2) / sigma and c = weight / (volume * 2 pi).  The
-// packed ops are IEEE fp32 like their scalar forms and the accumulation into
-// pdf stays one fma per gaussian in mixture order, so the result is bitwise
-// that of the scalar loop.  An odd count is padded with a zero gaussian
-// (k = 0, c = 0: fma(0, exp2(-0), pdf) = pdf exactly).
+// with k = sqrt(log2(e) / 2) / sigma and c = weight / (volume * 2 pi), one fma per
+// gaussian in mixture order.  An odd count is padded with a zero gaussian
+// (k = 0, c = 0: fma(0, exp2(-0), pdf) = pdf exactly).  Scalar FP32 on purpose:
+// on gfx950 v_fma_f32 issues in ~2.6 cycles per wave and v_pk_fma_f32 in ~4.7
+// (tools/valu_probe.hip), so packing two lanes' work gains nothing.
 // tp/tref hold only the K.tgmm_count gaussians with a non-zero coefficient
 // (SunskyKArgs::tgmm_idx), so tgmm_pdf loops over those.
 struct TgPair {
@@ -894,19 +893,19 @@ __device__ __forceinline__ float3_ sample_sun(const SunskyKArgs& K, float ux, fl
                           mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), uniform_cone_dev<FAST>(ux, uy, K.cos_cutoff));
 }
 
-// The FAST mixture sum of tgmm_pdf at a wrapped (phi, theta): one PAIR of
-// gaussians per iteration, sx / sy / q as packed FP32 for both, then one fma per
-// gaussian in mixture order.
+// The FAST mixture sum of tgmm_pdf at a wrapped (phi, theta), one pair of
+// gaussians per iteration, one fma per gaussian in mixture order.
 __device__ __forceinline__ float tgmm_sum_fast(const SunskyKArgs& K, const TgmmLds& T, float phi, float theta) {
     float pdf = 0.f;
     const int np = (K.tgmm_count + 1) >> 1;
 #pragma unroll 2
     for (int p = 0; p < np; ++p) {
         const TgPair P = T.tp[p];
-        const f32x2 sx = (phi - P.mphi) * P.kphi, sy = (theta - P.mth) * P.kth;
-        const f32x2 q = __builtin_elementwise_fma(sy, sy, sx * sx);
-        pdf = fmaf(P.c.x, fast_exp2(-q.x), pdf);
-        pdf = fmaf(P.c.y, fast_exp2(-q.y), pdf);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float sx = (phi - P.mphi[h]) * P.kphi[h], sy = (theta - P.mth[h]) * P.kth[h];
+            pdf = fmaf(P.c[h], fast_exp2(-fmaf(sy, sy, sx * sx)), pdf);
+        }
     }
     return pdf;
 }
@@ -1116,8 +1115,10 @@ __device__ __forceinline__ void pdf_direction_body(const SunskyKArgs& K, const f
             if constexpr (VEC == 1) {
                 acc[0] = tgmm_sum_fast(K, T, phi[0], theta[0]);
             } else {
-                // directions in pairs: each gaussian's sx, sy, q and the accumulation
-                // run as packed FP32 over two directions (bitwise the scalar loop)
+                // directions in pairs: each gaussian's sx, sy, q and the accumulation run as
+                // packed FP32 over two directions (bitwise the scalar loop).  Measured 2.6 %
+                // faster than the scalar form here (interleaved A/B, tools/gpu_ab2.sh), unlike
+                // the per-lane sums and the spectral channels, where packing lost.
                 constexpr int NP = VEC / 2;
                 f32x2 ph2[NP], th2[NP], ac2[NP];
 #pragma unroll

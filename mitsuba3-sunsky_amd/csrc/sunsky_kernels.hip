@@ -85,6 +85,27 @@ __device__ __forceinline__ float atan2_fast(float y, float x) {
     return copysignf(a, y);
 }
 
+// Correctly rounded a / b from rb = RN(1 / b) (Markstein's theorem: q = RN(a rb),
+// r = a - q b exact by fma, RN(q + r rb) = RN(a / b)), valid while r does not
+// underflow: |a| >= 2^-100 and rb normal; otherwise the plain division.  The FAST
+// sampling transforms divide by the wave-uniform w_sky / 1 - w_sky and by the picked
+// gaussian's pmf, whose reciprocals are computed once per wave / workgroup.  Exact,
+// so the sample transform keeps the correctly rounded quotients it needs (one ulp in
+// the reused sample moves sky directions by up to 2e-5).
+__device__ __forceinline__ float div_by_rcp(float a, float b, float rb) {
+    if (fabsf(a) >= 0x1p-100f && fabsf(rb) <= 0x1p100f) {
+        const float q = a * rb;
+        return fmaf(fmaf(-q, b, a), rb, q);
+    }
+    return a / b;
+}
+
+template <bool FAST>
+__device__ __forceinline__ float div_exact(float a, float b, float rb) {
+    if constexpr (FAST) return div_by_rcp(a, b, rb);
+    else return a / b;
+}
+
 // FAST sincos for the sampling transforms (sphdir, the concentric disk): one
 // Cody-Waite reduction by pi/2 (two fp32 constants, fma), then sin r = r + r^3 S(r^2)
 // and cos r = 1 - r^2/2 + r^4 C(r^2) on [-pi/4, pi/4] (tools/fit_sincos.py: max
@@ -745,6 +766,7 @@ struct TgmmLds {
     TgPair tp[kNbMixture / 2];
     Gaussian tref[kNbMixture];                   // compacted, reference-order tgmm_pdf
     float cdf[kNbMixture], pmf[kNbMixture];
+    float inv_pmfn[kNbMixture];                  // 1 / RN(pmf * gauss_norm) (div_by_rcp)
     uint8_t guide[kGaussGuideSize];
 };
 
@@ -755,6 +777,7 @@ __device__ __forceinline__ void stage_tgmm(const SunskyKArgs& K, TgmmLds* s) {
     lds_copy(reinterpret_cast<uint32_t*>(s->guide), reinterpret_cast<const uint32_t*>(K.gauss_guide),
              kGaussGuideSize / 4);
     const int i = threadIdx.x;
+    if (i < kNbMixture) s->inv_pmfn[i] = 1.f / (K.gauss_pmf[i] * K.gauss_norm);
     if (i < kNbMixture) {
         const float c = 0.84932180028801904272f;   // sqrt(log2(e) / 2)
         float* pair = reinterpret_cast<float*>(&s->tp[i >> 1]) + (i & 1);
@@ -825,7 +848,15 @@ __device__ __forceinline__ int discrete_sample_reuse(const SunskyKArgs& K, const
     }
     const float pmf = T.pmf[idx];
     const float cdf_prev = idx > 0 ? T.cdf[idx - 1] : 0.f;
-    *reused = (value - cdf_prev * K.gauss_norm) / (pmf * K.gauss_norm);   // exact: see sample_direction_body
+    // eval_cdf_normalized / eval_pmf_normalized are rounded products of their own in the
+    // reference (distr_1d.h:179-182): no fma contraction of the numerator, whose
+    // rounding the near-pole erfinv of the reused sample amplifies
+    float num;
+    {
+#pragma clang fp contract(off)
+        num = value - cdf_prev * K.gauss_norm;
+    }
+    *reused = div_exact<FAST>(num, pmf * K.gauss_norm, T.inv_pmfn[idx]);
     return idx;
 }
 
@@ -1014,6 +1045,7 @@ __device__ __forceinline__ void sample_direction_body(
     float* __restrict__ weight, size_t wstride) {
     __shared__ SamplerLds<FAST, SPEC> S;
     stage_sampler_lds<FAST, SPEC>(K, &S);
+    const float w_sun = 1.f - K.w_sky, inv_w = 1.f / K.w_sky, inv_w_sun = 1.f / w_sun;   // div_exact
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool act = active ? active[i] != 0 : true;
@@ -1024,10 +1056,10 @@ __device__ __forceinline__ void sample_direction_body(
         // sx / w and the reused sample stay correctly rounded even in FAST: the
         // discrete-distribution reuse divides by the picked gaussian's pmf, so one
         // ulp here moves sky directions by up to ~1e-5 (measured).
-        if (pick_sky) sd = sample_sky<FAST>(K, S.tgmm, sx / K.w_sky, sy);
+        if (pick_sky) sd = sample_sky<FAST>(K, S.tgmm, div_exact<FAST>(sx, K.w_sky, inv_w), sy);
         else
 #endif
-            sd = sample_sun<FAST>(K, (sx - K.w_sky) / (1.f - K.w_sky), sy);
+            sd = sample_sun<FAST>(K, div_exact<FAST>(sx - K.w_sky, w_sun, inv_w_sun), sy);
         act = act && (sd.z >= 0.f);
         float3_ d = to_world(K, sd);
         float skyp, sunp;
@@ -1215,6 +1247,7 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
                                                 float* __restrict__ weight, size_t wstride) {
     __shared__ SamplerLds<FAST, SPEC> S;
     stage_sampler_lds<FAST, SPEC>(K, &S);
+    const float w_sun = 1.f - K.w_sky, inv_w = 1.f / K.w_sky, inv_w_sun = 1.f / w_sun;   // div_exact
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool act = active ? active[i] != 0 : true;
@@ -1223,8 +1256,8 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
         const float sx = s3x[i], sy = s3y[i];
         const bool pick_sky = sx < K.w_sky;
         float3_ d;
-        if (pick_sky) d = sample_sky<FAST>(K, S.tgmm, sx / K.w_sky, sy);
-        else d = sample_sun<FAST>(K, (sx - K.w_sky) / (1.f - K.w_sky), sy);
+        if (pick_sky) d = sample_sky<FAST>(K, S.tgmm, div_exact<FAST>(sx, K.w_sky, inv_w), sy);
+        else d = sample_sun<FAST>(K, div_exact<FAST>(sx - K.w_sky, w_sun, inv_w_sun), sy);
         float3_ dw = to_world(K, mk3(-d.x, -d.y, -d.z));
         act = act && (d.z >= 0.f);
         float skyp, sunp;
@@ -1305,6 +1338,7 @@ __device__ __forceinline__ void direct_diffuse_body(
     uint32_t spp, size_t n, float* __restrict__ out, size_t ostride) {
     __shared__ SamplerLds<FAST, SPEC> S;
     stage_sampler_lds<FAST, SPEC>(K, &S);
+    const float w_sun = 1.f - K.w_sky, inv_w = 1.f / K.w_sky, inv_w_sun = 1.f / w_sun;   // div_exact
     constexpr int C = SPEC ? 4 : 3;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -1328,8 +1362,8 @@ __device__ __forceinline__ void direct_diffuse_body(
             const float u2 = rng.next_float(), u3 = rng.next_float();
             // ---- emitter sampling: sample_direction (sunsky.cpp:399-441)
             const bool pick_sky = u0 < K.w_sky;
-            float3_ sd = pick_sky ? sample_sky<FAST>(K, S.tgmm, u0 / K.w_sky, u1)
-                                  : sample_sun<FAST>(K, (u0 - K.w_sky) / (1.f - K.w_sky), u1);
+            float3_ sd = pick_sky ? sample_sky<FAST>(K, S.tgmm, div_exact<FAST>(u0, K.w_sky, inv_w), u1)
+                                  : sample_sun<FAST>(K, div_exact<FAST>(u0 - K.w_sky, w_sun, inv_w_sun), u1);
             bool act = sd.z >= 0.f;
             const float3_ d = to_world(K, sd);
             float skyp, sunp;

@@ -432,6 +432,7 @@ void SunskyModel::stage() {
         FastChannel& f = k_.fsky[c];
         f.A = ch.A; f.Bl2 = ch.Bl2; f.El2 = ch.El2; f.P = ch.P; f.Q = ch.Q;
         f.Cs = ch.C * Rs; f.Ds = ch.D * Rs; f.Fs = ch.F * Rs; f.Gs = ch.G * Rs; f.Hs = ch.H * Rs;
+        f.pad[0] = f.pad[1] = 0.f;
     }
     k_.sun_mul = variant_ == kRGB
                      ? sun_scale_ * k_.area_ratio * (float)kSpecToRgbSunConv * (float)kCieYNormalization

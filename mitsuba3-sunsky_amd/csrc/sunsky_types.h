@@ -64,10 +64,14 @@ struct SkyChannel {
 // The same channel with the output scale folded in for the FAST kernels:
 // Rs = rad * sky_scale (* MI_CIE_Y_NORMALIZATION for RGB) multiplies C..H, so
 // L = (1 + A exp2(Bl2 r)) (Cs + Ds exp2(El2 g) + Fs cos^2 g + Gs chi + Hs sqrt(cos_theta)).
-struct FastChannel {
+// 48 bytes, 16-byte aligned: a per-lane channel gather from LDS is three
+// ds_read_b128 (full LDS read rate) instead of five ds_read2_b32 (half rate).
+struct alignas(16) FastChannel {
     float A, Bl2, El2, P, Q;
     float Cs, Ds, Fs, Gs, Hs;
+    float pad[2];
 };
+static_assert(sizeof(FastChannel) == 48, "FastChannel LDS stride");
 
 // One truncated Gaussian of the TGMM (sunsky.cpp:661-689, :732-763) with
 // its per-gaussian truncation constants hoisted out of the per-lane loop.

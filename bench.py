@@ -450,26 +450,39 @@ def main():
         if world > 1:
             dist.barrier()
         te = (time.perf_counter() - t0) / reps
-        tg, own_ok = 0.0, True
+        tg, tcat, own_ok = 0.0, 0.0, True
         if world > 1:
+            from sunsky_amd.sharding import gather_shards, shard_sizes
             t = torch.tensor([te], device=coll_dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             te = float(t.item())
-            dist.barrier()
-            t0 = time.perf_counter()
-            full = gather_radiance(out5.to(coll_dev), n5 * world)
-            torch.cuda.synchronize()
-            tg = time.perf_counter() - t0
+            send = out5.to(coll_dev)
+            bufs = gather_shards(send, n5 * world)           # untimed: connection setup
+            tgs = []
+            for _ in range(3):                                 # the collective alone, preallocated
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                gather_shards(send, n5 * world, bufs=bufs)
+                torch.cuda.synchronize()
+                tgs.append(time.perf_counter() - t0)
+            tg = sorted(tgs)[1]
             if rank == 0:
+                t0 = time.perf_counter()
+                full = torch.cat([b[:, :s] for b, s in zip(bufs, shard_sizes(n5 * world, world))], dim=1)
+                torch.cuda.synchronize()
+                tcat = time.perf_counter() - t0
                 own_ok = bool(torch.equal(full[:, :n5].to(dev), out5))
-            del full
+                del full
+            del bufs, send
         if rank == 0:
             nbytes = 11 * n5 * 4 * (world - 1)
             result["c5_spectral_shard_gather"] = {
                 "dirs_per_gpu": n5, "lambdas": 11, "eval_s": te,
                 "evals_per_s_whole_job": 11 * n5 * world / te,
                 "gather_s": tg, "gather_bytes_to_root": nbytes, "gather_GBps": nbytes / tg / 1e9 if tg else None,
-                "end_to_end_s": te + tg, "bitwise_own_shard": own_ok,
+                "gather_timing": "median of 3 dist.gather into preallocated per-rank buffers after one untimed call",
+                "reassemble_planes_s": tcat, "end_to_end_s": te + tg + tcat, "bitwise_own_shard": own_ok,
                 "note": "configs[4]: per-GPU spectral eval (weak scaling) then gather of the radiance to rank 0"}
         del wi5, out5
 

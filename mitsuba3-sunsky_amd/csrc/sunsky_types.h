@@ -75,7 +75,7 @@ static_assert(sizeof(FastChannel) == 48, "FastChannel LDS stride");
 
 // One truncated Gaussian of the TGMM (sunsky.cpp:661-689, :732-763) with
 // its per-gaussian truncation constants hoisted out of the per-lane loop.
-struct Gaussian {
+struct alignas(16) Gaussian {
     float mu_phi, mu_theta, sigma_phi, sigma_theta;
     float weight;                          // mixture weight x corner lerp factor
     float inv_sigma_phi, inv_sigma_theta;

@@ -31,9 +31,10 @@ def shard_sizes(n, world):
     return [shard_range(n, r, world)[1] - shard_range(n, r, world)[0] for r in range(world)]
 
 
-def gather_radiance(local, n_total, dst=0, group=None):
-    """Gather every rank's (C, n_r) radiance shard into the (C, n_total) buffer on `dst`
-    (None elsewhere).  Shards are padded to the largest size for the collective."""
+def gather_shards(local, n_total, dst=0, group=None, bufs=None):
+    """The collective alone: every rank's (C, n_r) shard, padded to the largest shard, into
+    `dst`'s list of per-rank (C, m) buffers (rank-major, as ncclGather lays them out).
+    Returns that list on `dst` (None elsewhere); `bufs` may be a preallocated list."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     sizes = shard_sizes(n_total, world)
@@ -46,8 +47,17 @@ def gather_radiance(local, n_total, dst=0, group=None):
         send = torch.zeros((c, m), dtype=local.dtype, device=local.device)
         send[:, : local.shape[1]] = local
     send = send.contiguous()
-    bufs = [torch.empty((c, m), dtype=local.dtype, device=local.device) for _ in range(world)] if rank == dst else None
-    dist.gather(send, bufs, dst=dst, group=group)
-    if rank != dst:
+    if rank == dst and bufs is None:
+        bufs = [torch.empty((c, m), dtype=local.dtype, device=local.device) for _ in range(world)]
+    dist.gather(send, bufs if rank == dst else None, dst=dst, group=group)
+    return bufs if rank == dst else None
+
+
+def gather_radiance(local, n_total, dst=0, group=None):
+    """Gather every rank's (C, n_r) radiance shard into the (C, n_total) buffer on `dst`
+    (None elsewhere).  Shards are padded to the largest size for the collective."""
+    bufs = gather_shards(local, n_total, dst, group)
+    if bufs is None:
         return None
+    sizes = shard_sizes(n_total, dist.get_world_size(group))
     return torch.cat([b[:, :s] for b, s in zip(bufs, sizes)], dim=1)

@@ -115,7 +115,14 @@ def cpu_baseline(wi_host, budget_s=12.0):
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "dir-evals/s", "cores": threads, "kind": "port",
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), model)
+    except OSError:
+        pass
+    return {"value": done / dt, "unit": "dir-evals/s", "cores": threads, "kind": "port", "cpu_model": model,
+            "host_cpus_visible": len(os.sched_getaffinity(0)),
             "sample": f"{done} RGB evals ({n_sample} of the headline directions x T in {{2,6,10}}, "
                       f"repeated for >= {budget_s:.0f}s), oracle/sunsky_oracle.c fp32, {threads} OpenMP threads"}
 

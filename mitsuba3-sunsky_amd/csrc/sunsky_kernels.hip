@@ -30,6 +30,12 @@
 using namespace sunsky;
 
 #define SS_BLOCK 256
+#ifndef SS_NODES_ATTR       // tuning builds only (tools/gpu_ab2.sh): occupancy attributes
+#define SS_NODES_ATTR
+#endif
+#ifndef SS_RGB_ATTR
+#define SS_RGB_ATTR
+#endif
 constexpr float kLog2e = 1.44269504088896340736f;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -1893,7 +1899,7 @@ __device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const f
 // extern "C" entry points (hipModuleGetFunction names)
 // ======================================================================
 #define SS_EVAL_RGB(NAME, VEC, FAST, NEG)                                                                          \
-    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_RGB_ATTR void NAME(                                               \
         SunskyKArgs K, const float* wx, const float* wy, const float* wz, const uint8_t* active, size_t n,     \
         float* out, size_t ostride, float sign) {                                                              \
         (void)sign;                                                                                            \
@@ -1910,7 +1916,7 @@ SS_EVAL_RGB(sunsky_eval_rgb_v4_dir_ref, 4, false, false)
 SS_EVAL_RGB(sunsky_eval_rgb_v1_dir_ref, 1, false, false)
 
 #define SS_EVAL_SPEC_BCAST(NAME, VEC, FAST)                                                                   \
-    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_NODES_ATTR void NAME(                                               \
         SunskyKArgs K, LambdaSet L, const float* wx, const float* wy, const float* wz, const uint8_t* active,  \
         size_t n, float* out, size_t ostride, float sign) {                                                    \
         (void)sign;   /* always eval(si): wo = -wi */                                                         \
@@ -1922,7 +1928,7 @@ SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v4_ref, 4, false)
 SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v1_ref, 1, false)
 
 #define SS_EVAL_SPEC_NODES(NAME, VEC, FAST)                                                                   \
-    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_NODES_ATTR void NAME(                                               \
         SunskyKArgs K, LambdaSet L, const float* wx, const float* wy, const float* wz, const uint8_t* active,  \
         size_t n, float* out, size_t ostride, float sign) {                                                    \
         (void)L;                                                                                               \

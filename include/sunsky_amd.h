@@ -15,8 +15,13 @@
  *   - `active` is an optional per-ray uint8 mask (NULL = all active), the
  *     `Mask active` argument of the reference methods;
  *   - `stream` is a hipStream_t (NULL = default stream); every batch call is
- *     asynchronous and stream-ordered, allocates nothing and may be captured
- *     into a hipGraph;
+ *     asynchronous and stream-ordered.  The hot-path calls (eval,
+ *     eval_direction, eval_spectral_broadcast, sample_direction, pdf_direction,
+ *     sample_ray, sample_wavelengths, direct_diffuse) allocate nothing, make no
+ *     host-synchronous call and may be captured into a hipGraph
+ *     (tests/test_graph_capture.py); a graph snapshots the emitter's parameters
+ *     at capture, so recapture after parameters_changed().  eval_jvp, eval_vjp
+ *     and bake_latlong upload per-call tables first and are not capturable;
  *   - create/update/destroy are host-synchronous and must not race batch calls
  *     on the same emitter (the reference's parameters_changed() contract).
  */

@@ -1,0 +1,66 @@
+"""The hot-path entry points are stream-ordered, allocate nothing on the device and make
+no host-synchronous calls, so a caller can capture them into a hipGraph
+(include/sunsky_amd.h).  Captured with torch.cuda.graph (hipStreamBeginCapture on ROCm):
+replays equal the eager calls bit for bit, and a replay after the inputs change in place
+equals an eager call on the new inputs."""
+import numpy as np
+import pytest
+import torch
+
+import sunsky_amd as ss
+from helpers import angles_dict, hemisphere_wo
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+
+
+def _inputs(n, seed):
+    wo = np.ascontiguousarray(hemisphere_wo(n, seed).T.astype(np.float32))
+    u = np.random.default_rng(seed + 100).random((2, n), dtype=np.float32)
+    return torch.from_numpy(-wo).cuda(), torch.from_numpy(u).cuda()
+
+
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+def test_eval_and_sampling_replay_bitwise(variant):
+    em = ss.SunskyEmitter(angles_dict(3.0, 0.3, np.deg2rad(50), 0.3, 1.0, 1.0), variant)
+    n = 1 << 16
+    wi, u = _inputs(n, 1)
+    lam = torch.full((4, n), 550.0, device="cuda") + torch.arange(4, device="cuda").view(4, 1) * 37.0
+
+    def step():
+        si = ss.SurfaceInteraction3f(wi=wi, wavelengths=lam if variant == "spectral" else None)
+        it = ss.Interaction3f(wavelengths=lam if variant == "spectral" else None)
+        e = em.eval(si)
+        ds, w = em.sample_direction(it, u)
+        p = em.pdf_direction(it, ds)
+        return e, ds.d, ds.pdf, w, p
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()                                   # warm-up outside the capture
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        captured = step()
+    g.replay()
+    torch.cuda.synchronize()
+    eager = step()
+    torch.cuda.synchronize()
+    for a, b in zip(captured, eager):
+        assert torch.equal(a, b)
+    wi2, u2 = _inputs(n, 2)
+    wi.copy_(wi2)
+    u.copy_(u2)
+    g.replay()
+    torch.cuda.synchronize()
+    eager2 = step()
+    torch.cuda.synchronize()
+    for a, b, old in zip(captured, eager2, eager):
+        assert torch.equal(a, b)
+        assert not torch.equal(a, old)

@@ -85,7 +85,11 @@ def pmc_traffic(kernel):
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over this same bench command,
     corrected per MI355X_MICROARCH.md "HBM").  None when no summary exists."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    import re
+
+    def version(path):   # natural order: r01_v9 < r01_v12
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")), key=version)
     if not files:
         return None, None
     with open(files[-1]) as fh:

@@ -105,7 +105,7 @@ enum KernelId {
     K_EVAL_RGB_V4, K_EVAL_RGB_V1, K_EVAL_SPEC_BCAST_V4, K_EVAL_SPEC_BCAST_V1, K_EVAL_SPEC_NODES_V4,
     K_EVAL_SPEC_RAYS_V4, K_EVAL_SPEC_RAYS_V1, K_SAMPLE_DIRECTION_RGB, K_SAMPLE_DIRECTION_SPEC, K_PDF_DIRECTION_V4, K_PDF_DIRECTION_V1, K_SAMPLE_WAVELENGTHS_RGB,
     K_SAMPLE_WAVELENGTHS_SPEC, K_SAMPLE_RAY_RGB, K_SAMPLE_RAY_SPEC, K_BAKE_RGB, K_BAKE_SPEC,
-    K_DIRECT_DIFFUSE_RGB, K_DIRECT_DIFFUSE_SPEC, K_COUNT
+    K_DIRECT_DIFFUSE_RGB, K_DIRECT_DIFFUSE_SPEC, K_SAMPLE_DIRECTION_RGB_LEAN, K_SAMPLE_DIRECTION_SPEC_LEAN, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
@@ -113,7 +113,8 @@ const char* kKernelNames[K_COUNT] = {
     "sunsky_sample_direction_spec", "sunsky_pdf_direction_v4", "sunsky_pdf_direction_v1",
     "sunsky_sample_wavelengths_rgb",
     "sunsky_sample_wavelengths_spec", "sunsky_sample_ray_rgb", "sunsky_sample_ray_spec",
-    "sunsky_bake_latlong_rgb", "sunsky_bake_latlong_spec", "sunsky_direct_diffuse_rgb", "sunsky_direct_diffuse_spec"};
+    "sunsky_bake_latlong_rgb", "sunsky_bake_latlong_spec", "sunsky_direct_diffuse_rgb", "sunsky_direct_diffuse_spec",
+    "sunsky_sample_direction_rgb_lean", "sunsky_sample_direction_spec_lean"};
 
 // eval kernels instantiated twice: eval(si) negates wi at compile time,
 // eval_direction(ds) uses ds.d as is (the "_dir" kernels)
@@ -182,6 +183,7 @@ int blocks_per_cu(KernelId k) {
         case K_EVAL_RGB_V4: case K_EVAL_RGB_V1: return 64;
         case K_EVAL_SPEC_BCAST_V4: case K_EVAL_SPEC_BCAST_V1: case K_EVAL_SPEC_NODES_V4: return 64;
         case K_SAMPLE_DIRECTION_RGB: case K_SAMPLE_DIRECTION_SPEC: case K_PDF_DIRECTION_V4: case K_PDF_DIRECTION_V1:
+        case K_SAMPLE_DIRECTION_RGB_LEAN: case K_SAMPLE_DIRECTION_SPEC_LEAN:
             return 64;
         case K_BAKE_RGB: case K_BAKE_SPEC: return 64;
         case K_DIRECT_DIFFUSE_RGB: case K_DIRECT_DIFFUSE_SPEC: return 64;
@@ -583,7 +585,11 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
         int nl = spec ? nlam : 0;
         void* args[] = {&K, &ux, &uy, (void*)&it_p.x, (void*)&it_p.y, (void*)&it_p.z, &lam, &lstride, &nl, &active, &n,
                         &ds_d.x, &ds_d.y, &ds_d.z, &ds_pdf, &ds_dist, &ds_p.x, &ds_p.y, &ds_p.z, &weight, &wstride};
-        const KernelId k = spec ? K_SAMPLE_DIRECTION_SPEC : K_SAMPLE_DIRECTION_RGB;
+        // the common call (no it.p, ds.dist, ds.p or mask) takes the kernel with those
+        // paths compiled out: same results, no SGPR spills (sampling)
+        const bool lean = !it_p.x && !ds_dist && !ds_p.x && !active;
+        const KernelId k = spec ? (lean ? K_SAMPLE_DIRECTION_SPEC_LEAN : K_SAMPLE_DIRECTION_SPEC)
+                                : (lean ? K_SAMPLE_DIRECTION_RGB_LEAN : K_SAMPLE_DIRECTION_RGB);
         launch(e->fn(k), grid_for(e->mod, k, n), (hipStream_t)stream, args);
     });
 }

@@ -1041,7 +1041,10 @@ __device__ __forceinline__ void sample_wavelengths_one(const SunskyKArgs& K, con
 }
 
 // sample_direction, sunsky.cpp:399-441.  Weight planes: 3 (RGB) or nlam (spectral).
-template <bool FAST, bool SPEC>
+// LEAN: the host found it_p, ds.dist, ds.p and the active mask all NULL (the common
+// call, u -> d, pdf, weight); the optional pointers and their branches are compiled
+// out, which frees the SGPRs the kernel otherwise spills through v_writelane/v_readlane.
+template <bool FAST, bool SPEC, bool LEAN = false>
 __device__ __forceinline__ void sample_direction_body(
     const SunskyKArgs& K, const float* __restrict__ ux, const float* __restrict__ uy,
     const float* __restrict__ px, const float* __restrict__ py, const float* __restrict__ pz,
@@ -1049,6 +1052,11 @@ __device__ __forceinline__ void sample_direction_body(
     float* __restrict__ dx, float* __restrict__ dy, float* __restrict__ dz, float* __restrict__ pdf,
     float* __restrict__ dist, float* __restrict__ opx, float* __restrict__ opy, float* __restrict__ opz,
     float* __restrict__ weight, size_t wstride) {
+    if constexpr (LEAN) {
+        px = py = pz = nullptr;
+        active = nullptr;
+        dist = opx = opy = opz = nullptr;
+    }
     __shared__ SamplerLds<FAST, SPEC> S;
     stage_sampler_lds<FAST, SPEC>(K, &S);
     const float w_sun = 1.f - K.w_sky, inv_w = 1.f / K.w_sky, inv_w_sun = 1.f / w_sun;   // div_exact
@@ -1954,18 +1962,22 @@ SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_dir_fast, 1, true, false)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_dir_ref, 4, false, false)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_dir_ref, 1, false, false)
 
-#define SS_SAMPLE_DIRECTION(NAME, FAST, SPEC)                                                                 \
+#define SS_SAMPLE_DIRECTION(NAME, FAST, SPEC, LEAN)                                                           \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
         SunskyKArgs K, const float* ux, const float* uy, const float* px, const float* py, const float* pz,   \
         const float* lam, size_t lstride, int nlam, const uint8_t* active, size_t n, float* dx, float* dy,     \
         float* dz, float* pdf, float* dist, float* opx, float* opy, float* opz, float* weight, size_t wstride) { \
-        sample_direction_body<FAST, SPEC>(K, ux, uy, px, py, pz, lam, lstride, nlam, active, n, dx, dy, dz,    \
-                                          pdf, dist, opx, opy, opz, weight, wstride);                          \
+        sample_direction_body<FAST, SPEC, LEAN>(K, ux, uy, px, py, pz, lam, lstride, nlam, active, n, dx, dy,  \
+                                                dz, pdf, dist, opx, opy, opz, weight, wstride);                \
     }
-SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_fast, true, false)
-SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_ref, false, false)
-SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_fast, true, true)
-SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_ref, false, true)
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_fast, true, false, false)
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_ref, false, false, false)
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_fast, true, true, false)
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_ref, false, true, false)
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_fast, true, false, true)
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_ref, false, false, true)
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_fast, true, true, true)
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_ref, false, true, true)
 
 #define SS_PDF_DIRECTION(NAME, VEC, FAST)                                                                     \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \

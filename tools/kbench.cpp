@@ -188,7 +188,9 @@ int main(int argc, char** argv) {
                 hipModule_t mod_b;
                 CK(hipModuleLoad(&mod_b, ab));
                 hipFunction_t fb;
-                CK(hipModuleGetFunction(&fb, mod_b, argv[a]));
+                // KB_AB_NAME: a different kernel of the other code object (e.g. a variant)
+                const char* bname = std::getenv("KB_AB_NAME") ? std::getenv("KB_AB_NAME") : argv[a];
+                CK(hipModuleGetFunction(&fb, mod_b, bname));
                 const int rounds = std::getenv("KB_AB_ROUNDS") ? std::atoi(std::getenv("KB_AB_ROUNDS")) : 20;
                 std::vector<double> ta, tb, ratio;
                 auto burst = [&](hipFunction_t fn) {
@@ -207,8 +209,8 @@ int main(int argc, char** argv) {
                     ta.push_back(x); tb.push_back(y); ratio.push_back(y / x);
                 }
                 auto median = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
-                std::printf("  A/B %-30s this %8.2f us  other %8.2f us  median(other/this) %.4f  (%d rounds x %d)\n",
-                            argv[a], median(ta), median(tb), median(ratio), rounds, iters);
+                std::printf("  A/B %-30s this %8.2f us  other(%s) %8.2f us  median(other/this) %.4f  (%d rounds x %d)\n",
+                            argv[a], median(ta), bname, median(tb), median(ratio), rounds, iters);
                 std::fflush(stdout);
                 CK(hipModuleUnload(mod_b));
             }

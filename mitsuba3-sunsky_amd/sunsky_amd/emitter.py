@@ -392,8 +392,11 @@ class SunskyEmitter:
                                                    _ptr(out), out.stride(0), self._stream()))
         return out
 
-    def sample_direction(self, it, sample, active=None):
-        """sample_direction(it, sample, active) -- sunsky.cpp:399-441 -> (ds, weight)."""
+    def sample_direction(self, it, sample, active=None, positions=True):
+        """sample_direction(it, sample, active) -- sunsky.cpp:399-441 -> (ds, weight).
+
+        positions=False leaves ds.p and ds.dist unset (None): with no mask and no it.p
+        the C ABI then runs the LEAN kernel (d, pdf and weight bitwise the same)."""
         sample = self._f32(sample)
         if sample.dim() != 2 or sample.shape[0] != 2:
             raise ValueError("sample is a (2, n) tensor")
@@ -405,9 +408,14 @@ class SunskyEmitter:
         else:
             pin = Vec3In(None, None, None)
         d = torch.empty((3, n), dtype=torch.float32, device=self.device)
-        pos = torch.empty((3, n), dtype=torch.float32, device=self.device)
         pdf = torch.empty(n, dtype=torch.float32, device=self.device)
-        dist = torch.empty(n, dtype=torch.float32, device=self.device)
+        if positions:
+            pos = torch.empty((3, n), dtype=torch.float32, device=self.device)
+            dist = torch.empty(n, dtype=torch.float32, device=self.device)
+            pout = Vec3Out(pos[0].data_ptr(), pos[1].data_ptr(), pos[2].data_ptr())
+        else:
+            pos = dist = None
+            pout = Vec3Out(None, None, None)
         wl = None
         k = 3
         if self.is_spectral:
@@ -417,7 +425,7 @@ class SunskyEmitter:
         check(lib().sunsky_sample_direction(
             self._h, _ptr(sample[0]), _ptr(sample[1]), pin, _ptr(wl), k if self.is_spectral else 0, n,
             _ptr(m), n, Vec3Out(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr()), _ptr(pdf), _ptr(dist),
-            Vec3Out(pos[0].data_ptr(), pos[1].data_ptr(), pos[2].data_ptr()), _ptr(w), n, self._stream()))
+            pout, _ptr(w), n, self._stream()))
         ds = DirectionSample3f(p=pos, n=-d, uv=sample, time=getattr(it, "time", None), pdf=pdf, delta=False,
                                d=d, dist=dist, emitter=self)
         return ds, w

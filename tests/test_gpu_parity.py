@@ -219,6 +219,29 @@ def test_sample_direction_and_pdf_parity(variant, semantics, precision):
     assert_parity(gw, wref32, wref64, inside_sun, rtol=2e-5)
 
 
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_sample_direction_lean_kernel_bitwise(variant, precision):
+    """The LEAN sample_direction kernels (it.p, ds.p, ds.dist and the mask compiled out,
+    chosen by the C ABI when all are NULL) return d, pdf and weight bit for bit equal to
+    the general kernel, for a rotated emitter (to_world) and an identity one."""
+    for rot in (False, True):
+        d = angles_dict(3.0, 1.1, np.deg2rad(35), 0.3, 1.0, 1.0)
+        if rot:
+            d["to_world"] = np.array([[0, 0, 1, 0], [1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 0, 1]], np.float64)
+        em = ss.SunskyEmitter(d, variant, precision=precision)
+        rng = np.random.default_rng(5)
+        n = (1 << 14) + 3
+        u = soa(rng.random((n, 2), dtype=np.float32))
+        lam = torch.from_numpy(rng.uniform(360, 720, (4, n)).astype(np.float32)).cuda()
+        it = ss.Interaction3f(wavelengths=lam if variant == "spectral" else None)
+        ds_full, w_full = em.sample_direction(it, u)
+        ds_lean, w_lean = em.sample_direction(it, u, positions=False)
+        assert ds_lean.p is None and ds_lean.dist is None
+        for a, b in ((ds_full.d, ds_lean.d), (ds_full.pdf, ds_lean.pdf), (w_full, w_lean)):
+            assert np.array_equal(host(a).view(np.uint32), host(b).view(np.uint32))
+
+
 @pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("elev_deg", [0.1, 0.6, 3.0, 20.0, 60.0, 89.5])
 def test_sun_disc_weights_across_elevations(elev_deg, precision):

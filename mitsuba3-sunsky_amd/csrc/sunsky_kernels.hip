@@ -490,6 +490,14 @@ __device__ __forceinline__ void store_vec(float* p, size_t i, const float v[VEC]
     }
 }
 
+// One non-temporal fp32 store (the per-sample kernels).
+__device__ __forceinline__ void store_nt(float v, float* p) {
+#ifdef SS_PROBE_NOSTORE
+    if (v != -1234.5f) return;
+#endif
+    __builtin_nontemporal_store(v, p);
+}
+
 template <int VEC>
 __device__ __forceinline__ void load_mask(const uint8_t* m, size_t i, bool v[VEC]) {
     if (!m) {
@@ -930,6 +938,60 @@ __device__ __forceinline__ float3_ sample_sun(const SunskyKArgs& K, float ux, fl
                           mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), uniform_cone_dev<FAST>(ux, uy, K.cos_cutoff));
 }
 
+// sample_sky (sunsky.cpp:661-689) or sample_sun (:697-701) per lane, with the
+// sky's sincos(theta) and the concentric disk's sincos(phi) (warp.h:54-90) as ONE
+// call on a per-lane argument: a wave holding both kinds of lanes (nearly every
+// wave, ~1 - w_sky of them are sun picks) runs two sincos instead of three.  The
+// quotient u.x / w_sky or (u.x - w_sky) / (1 - w_sky) is one div_exact on selected
+// operands.  Same functions on the same arguments as sample_sky / sample_sun: bitwise
+// the same directions.
+template <bool FAST>
+__device__ __forceinline__ float3_ sample_sky_or_sun(const SunskyKArgs& K, const TgmmLds& T, bool pick_sky,
+                                                     float ux, float uy, float inv_w, float inv_w_sun) {
+    const float a = div_exact<FAST>(pick_sky ? ux : ux - K.w_sky, pick_sky ? K.w_sky : 1.f - K.w_sky,
+                                    pick_sky ? inv_w : inv_w_sun);
+    float arg, phi = 0.f, r = 0.f;
+    if (pick_sky) {
+        float temp;
+        const int idx = discrete_sample_reuse<FAST>(K, T, a, &temp);
+        const Gaussian& g = T.gauss[idx];
+        float sx = lerpf_(g.cdf_a_phi, g.cdf_b_phi, temp);
+        float sy = lerpf_(g.cdf_a_theta, g.cdf_b_theta, uy);
+        sx = fminf(fmaxf(sx, kEpsilon), kOneMinusEpsilon);
+        sy = fminf(fmaxf(sy, kEpsilon), kOneMinusEpsilon);
+        const float ex = FAST ? erfinv_fast(2.f * sx - 1.f) : erfinvf_(2.f * sx - 1.f);
+        const float ey = FAST ? erfinv_fast(2.f * sy - 1.f) : erfinvf_(2.f * sy - 1.f);
+        phi = kSqrtTwo * ex * g.sigma_phi + g.mu_phi;
+        float theta = kSqrtTwo * ey * g.sigma_theta + g.mu_theta;
+        phi += K.sun_phi - 0.5f * kPi;
+        arg = fminf(theta, 0.5f * kPi - kEpsilon);
+    } else {
+        const float x = fmaf(2.f, a, -1.f), y = fmaf(2.f, uy, -1.f);
+        const bool is_zero = (x == 0.f) && (y == 0.f);
+        const bool q13 = fabsf(x) < fabsf(y);
+        r = q13 ? y : x;
+        const float rp = q13 ? x : y;
+        float pd = fdiv<FAST>(0.25f * kPi * rp, r);
+        if (q13) pd = 0.5f * kPi - pd;
+        arg = is_zero ? 0.f : pd;
+    }
+    float s1, c1;
+    sincos_sel<FAST>(arg, &s1, &c1);
+    if (pick_sky) {
+        float sp, cp;
+        sincos_sel<FAST>(phi, &sp, &cp);
+        return mk3(cp * s1, sp * s1, c1);
+    }
+    // square_to_uniform_cone (warp.h:533-551) of the disk point, then Frame(sun).to_world
+    const float px = r * c1, py = r * s1;
+    const float omc = 1.f - K.cos_cutoff;
+    const float pn = fmaf(px, px, py * py);
+    const float z = K.cos_cutoff + omc * (1.f - pn);
+    const float sc = safe_sqrtf_(omc * (2.f - omc * pn));
+    return frame_to_world(mk3(K.sun_s[0], K.sun_s[1], K.sun_s[2]), mk3(K.sun_t[0], K.sun_t[1], K.sun_t[2]),
+                          mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), mk3(px * sc, py * sc, z));
+}
+
 // The FAST mixture sum of tgmm_pdf at a wrapped (phi, theta), one pair of
 // gaussians per iteration, one fma per gaussian in mixture order.
 __device__ __forceinline__ float tgmm_sum_fast(const SunskyKArgs& K, const TgmmLds& T, float phi, float theta) {
@@ -1065,15 +1127,14 @@ __device__ __forceinline__ void sample_direction_body(
         bool act = active ? active[i] != 0 : true;
         const float sx = ux[i], sy = uy[i];
         const bool pick_sky = sx < K.w_sky;
-        float3_ sd;
-#ifndef SS_PROBE_NO_SKY_SAMPLE   // probe builds (tools/Makefile) only: cost ablations
         // sx / w and the reused sample stay correctly rounded even in FAST: the
         // discrete-distribution reuse divides by the picked gaussian's pmf, so one
         // ulp here moves sky directions by up to ~1e-5 (measured).
-        if (pick_sky) sd = sample_sky<FAST>(K, S.tgmm, div_exact<FAST>(sx, K.w_sky, inv_w), sy);
-        else
+#ifndef SS_PROBE_NO_SKY_SAMPLE   // probe builds (tools/Makefile) only: cost ablations
+        const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
+#else
+        const float3_ sd = sample_sun<FAST>(K, div_exact<FAST>(sx - K.w_sky, w_sun, inv_w_sun), sy);
 #endif
-            sd = sample_sun<FAST>(K, div_exact<FAST>(sx - K.w_sky, w_sun, inv_w_sun), sy);
         act = act && (sd.z >= 0.f);
         float3_ d = to_world(K, sd);
         float skyp, sunp;
@@ -1083,10 +1144,10 @@ __device__ __forceinline__ void sample_direction_body(
         skyp = sd.z; sunp = K.sun_pdf;
 #endif
         float pd = lerpf_(sunp, skyp, K.w_sky);
-        __builtin_nontemporal_store(d.x, dx + i);
-        __builtin_nontemporal_store(d.y, dy + i);
-        __builtin_nontemporal_store(d.z, dz + i);
-        __builtin_nontemporal_store(pd, pdf + i);
+        store_nt(d.x, dx + i);
+        store_nt(d.y, dy + i);
+        store_nt(d.z, dz + i);
+        store_nt(pd, pdf + i);
         if (dist || opx) {
             float3_ itp = mk3(px ? px[i] : 0.f, py ? py[i] : 0.f, pz ? pz[i] : 0.f);
             float3_ rel = mk3(itp.x - K.bs_center[0], itp.y - K.bs_center[1], itp.z - K.bs_center[2]);
@@ -1107,7 +1168,7 @@ __device__ __forceinline__ void sample_direction_body(
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 float w = FAST ? e[c] * inv_pd : e[c] / pd;
-                __builtin_nontemporal_store(isfinite(w) ? w : 0.f, weight + (size_t)c * wstride + i);
+                store_nt(isfinite(w) ? w : 0.f, weight + (size_t)c * wstride + i);
             }
         } else {
             DirTerms t = dir_terms<FAST>(K, wo, act);
@@ -1269,9 +1330,7 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
         disk_concentric_dev<FAST>(s2x[i], s2y[i], &offx, &offy);
         const float sx = s3x[i], sy = s3y[i];
         const bool pick_sky = sx < K.w_sky;
-        float3_ d;
-        if (pick_sky) d = sample_sky<FAST>(K, S.tgmm, div_exact<FAST>(sx, K.w_sky, inv_w), sy);
-        else d = sample_sun<FAST>(K, div_exact<FAST>(sx - K.w_sky, w_sun, inv_w_sun), sy);
+        const float3_ d = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
         float3_ dw = to_world(K, mk3(-d.x, -d.y, -d.z));
         act = act && (d.z >= 0.f);
         float skyp, sunp;
@@ -1376,8 +1435,7 @@ __device__ __forceinline__ void direct_diffuse_body(
             const float u2 = rng.next_float(), u3 = rng.next_float();
             // ---- emitter sampling: sample_direction (sunsky.cpp:399-441)
             const bool pick_sky = u0 < K.w_sky;
-            float3_ sd = pick_sky ? sample_sky<FAST>(K, S.tgmm, div_exact<FAST>(u0, K.w_sky, inv_w), u1)
-                                  : sample_sun<FAST>(K, div_exact<FAST>(u0 - K.w_sky, w_sun, inv_w_sun), u1);
+            float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, u0, u1, inv_w, inv_w_sun);
             bool act = sd.z >= 0.f;
             const float3_ d = to_world(K, sd);
             float skyp, sunp;

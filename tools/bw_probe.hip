@@ -41,13 +41,26 @@ __global__ __launch_bounds__(256) void rw2(const float* x, const float* y, const
     }
 }
 
+// sample_direction's shape: read 2 planes (u), write 7 (d, pdf, RGB weight), VEC per lane
+template <int VEC>
+__global__ __launch_bounds__(256) void samp(const float* x, const float* y, const float* z, float* out, size_t n) {
+    typedef float fv __attribute__((ext_vector_type(VEC)));
+    size_t nv = n / VEC, stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+        fv a = *(const fv*)(x + VEC * v), b = *(const fv*)(y + VEC * v);
+        fv s = a + b;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) __builtin_nontemporal_store(s * (float)(k + 1), (fv*)(out + (size_t)k * n + VEC * v));
+    }
+}
+
 // cold: rotate over 4 input batches (805 MB > the 256 MiB Infinity Cache)
 static const float *g_cx[4], *g_cy[4], *g_cz[4];
 static int g_cold = 1;
 
 template <typename F>
 int run(const char* name, F kern, int vec, int K, const float* x, const float* y, const float* z, float* out,
-        size_t n, int cu) {
+        size_t n, int cu, double bpe = 0) {
     for (int mult : {8, 16, 32, 64}) {
         unsigned grid = (unsigned)std::min<size_t>((n / vec + 255) / 256, (size_t)cu * mult);
         for (int w = 0; w < 3; ++w) kern<<<grid, 256>>>(x, y, z, out, n);
@@ -63,7 +76,7 @@ int run(const char* name, F kern, int vec, int K, const float* x, const float* y
         CK(hipEventSynchronize(e1));
         float ms;
         CK(hipEventElapsedTime(&ms, e0, e1));
-        double us = 1e3 * ms / it, bytes = (12.0 + 4.0 * K) * n;
+        double us = 1e3 * ms / it, bytes = (bpe > 0 ? bpe : 12.0 + 4.0 * K) * n;
         printf("%-14s K=%2d vec=%d bpcu=%-3d %8.2f us  %7.1f GB/s\n", name, K, vec, mult, us, bytes / (us * 1e-6) / 1e9);
     }
     return 0;
@@ -91,5 +104,13 @@ int main() {
     run("rw4_plain", rw4<11, false>, 4, 11, x, y, z, out, n, cu);
     run("rw2_nt", rw2<11, true>, 2, 11, x, y, z, out, n, cu);
     run("rw2_plain", rw2<11, false>, 2, 11, x, y, z, out, n, cu);
+    // sampling shape at C4's 64M samples: 8 B read + 28 B written per sample
+    const size_t ns = (size_t)1 << 26;
+    float *sx, *sy, *so;
+    CK(hipMalloc(&sx, ns * 4)); CK(hipMalloc(&sy, ns * 4)); CK(hipMalloc(&so, ns * 4 * 7));
+    CK(hipMemset(sx, 0, ns * 4)); CK(hipMemset(sy, 0, ns * 4));
+    run("samp_r2w7", samp<1>, 1, 7, sx, sy, sy, so, ns, cu, 36.0);
+    run("samp_r2w7", samp<2>, 2, 7, sx, sy, sy, so, ns, cu, 36.0);
+    run("samp_r2w7", samp<4>, 4, 7, sx, sy, sy, so, ns, cu, 36.0);
     return 0;
 }

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Sampling parity tests, then A/B of sample_direction (product vs tools/build/ab_base.hsaco).
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out
+export SUNSKY_AMD_DATASET=$R/mitsuba3-sunsky_amd/data/sunsky_datasets.pack
+cd $R
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/ > gpurun_out/t.log 2>&1 || exit 1
+H=$R/mitsuba3-sunsky_amd/build/sunsky_kernels.hsaco
+for k in ${KERNELS:-sunsky_sample_direction_rgb_lean_fast}; do
+  KB_AB=$R/tools/build/ab_base.hsaco KB_AB_ROUNDS=${ROUNDS:-20} timeout -k 10 200 \
+      $R/tools/build/kbench $H ${MODE:-sample} 67108864 10 64 $k >> gpurun_out/ab.log 2>&1 || exit 1
+done

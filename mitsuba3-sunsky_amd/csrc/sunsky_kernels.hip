@@ -64,6 +64,29 @@ __device__ __forceinline__ float asin_half_chord(float x) {
     return fmaf(x * t, p, x);
 }
 
+// FAST sun elevation pi/2 - acos(z) for z = cos(theta) in [0, 1] (sun-disc lanes are above
+// the horizon), as asin z: asin_half_chord(z) up to z = sqrt(1/2), above it
+// pi/2 - 2 asin(sqrt((1 - z) / 2)) (argument <= sqrt(1/2); 0.5 - 0.5 z exact there).  One
+// polynomial on a selected argument instead of libm's two-range acosf.  asin z does not
+// cancel near the horizon, where pi/2 - acos z loses ~1e-7 absolute (measured 2x over
+// the sun-disc bound at 0.1 degrees with a fast acos).
+__device__ __forceinline__ float elevation_fast(float z) {
+    const bool big = z > 0.70710678f;
+    const float p = asin_half_chord(big ? fast_sqrt(fmaf(-0.5f, z, 0.5f)) : z);
+    return big ? fmaf(-2.f, p, kHalfPi) : p;
+}
+
+// FAST cbrt on [0, 1] for the sun segment index (sunsky.cpp:579-587): exp2(log2(x) / 3)
+// with v_log_f32 / v_exp_f32, then one Newton step c - (c^3 - x) / (3 c^2).  No
+// denormal rescaling, sign handling or class fix-ups: the argument is 2 elevation / pi
+// in [0, 1], and x <= 2^-126 (a sun on the horizon) gives segment 0 either way.
+__device__ __forceinline__ float cbrt_unit_fast(float x) {
+    const float c = fast_exp2(__builtin_amdgcn_logf(x) * (1.f / 3.f));
+    const float r = fmaf(c * c, c, -x);
+    const float c1 = fmaf(-r * (1.f / 3.f), fast_rcp(c * c), c);
+    return x > 0x1p-126f ? c1 : 0.f;
+}
+
 // atan on [0, 1]: t + t^3 P(t^2), degree 7 in t^2 (tools/fit_atan.py; 1.07 ulp).
 __device__ __forceinline__ float atan_unit(float t) {
     const float u = t * t;
@@ -254,8 +277,8 @@ template <bool FAST>
 __device__ __forceinline__ void add_sun_terms(const SunskyKArgs& K, DirTerms& t) {
     if (t.hit_sun) {
         if constexpr (FAST) {
-            float elevation = kHalfPi - acosf(t.cos_theta);
-            float seg = cbrtf(2.f * elevation * kInvPi) * (float)kNbSunSegments;
+            float elevation = elevation_fast(t.cos_theta);
+            float seg = cbrt_unit_fast(2.f * elevation * kInvPi) * (float)kNbSunSegments;
             int pos = seg > 0.f ? (int)floorf(seg) : 0;
             pos = pos < kNbSunSegments - 1 ? pos : kNbSunSegments - 1;
             float frac = (float)pos * (1.f / (float)kNbSunSegments);
@@ -263,7 +286,7 @@ __device__ __forceinline__ void add_sun_terms(const SunskyKArgs& K, DirTerms& t)
             t.sun_x = elevation - kHalfPi * (frac * frac * frac);
             float h2 = t.h * t.h;
             float sg2 = 4.f * h2 * (1.f - h2);                    // sin^2(gamma)
-            t.sun_cpsi = safe_sqrtf_(fmaf(-K.inv_sin2_half_ap, sg2, 1.f));
+            t.sun_cpsi = fast_sqrt(fmaxf(fmaf(-K.inv_sin2_half_ap, sg2, 1.f), 0.f));   // v_sqrt_f32, 1 ulp
         } else {
             t.sun_pos = sun_segment(t.cos_theta, &t.sun_x);
             t.sun_cpsi = cos_psi(t.gamma, K.inv_sin2_half_ap);

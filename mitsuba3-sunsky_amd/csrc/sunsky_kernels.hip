@@ -47,6 +47,14 @@ __device__ __forceinline__ float fast_rsq(float x) { return __builtin_amdgcn_rsq
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
 
+// safe_sqrt (sunsky.h / Dr.Jit): correctly rounded in the reference kernels, v_sqrt_f32
+// (1 ulp) in FAST, which skips the ~16-instruction rounding fix-up sequence.
+template <bool FAST>
+__device__ __forceinline__ float safe_sqrt_sel(float x) {
+    if constexpr (FAST) return __builtin_amdgcn_sqrtf(fmaxf(x, 0.f));
+    else return sqrtf(x > 0.f ? x : 0.f);
+}
+
 // asin on [0, sqrt(0.5)]: the half chord h = |wo -/+ n| / 2 of unit_angle never
 // exceeds sqrt(2) / 2, so one odd minimax polynomial x + x^3 P(x^2) (degree 7 in
 // x^2; fitted by tools/fit_asin.py) replaces libm's two-range asin (select,
@@ -950,7 +958,7 @@ __device__ __forceinline__ float3_ uniform_cone_dev(float sx, float sy, float co
     float omc = 1.f - cos_cutoff;
     float pn = fmaf(px, px, py * py);
     float z = cos_cutoff + omc * (1.f - pn);
-    float sc = safe_sqrtf_(omc * (2.f - omc * pn));
+    float sc = safe_sqrt_sel<FAST>(omc * (2.f - omc * pn));
     return mk3(px * sc, py * sc, z);
 }
 
@@ -1010,7 +1018,7 @@ __device__ __forceinline__ float3_ sample_sky_or_sun(const SunskyKArgs& K, const
     const float omc = 1.f - K.cos_cutoff;
     const float pn = fmaf(px, px, py * py);
     const float z = K.cos_cutoff + omc * (1.f - pn);
-    const float sc = safe_sqrtf_(omc * (2.f - omc * pn));
+    const float sc = safe_sqrt_sel<FAST>(omc * (2.f - omc * pn));
     return frame_to_world(mk3(K.sun_s[0], K.sun_s[1], K.sun_s[2]), mk3(K.sun_t[0], K.sun_t[1], K.sun_t[2]),
                           mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), mk3(px * sc, py * sc, z));
 }
@@ -1062,7 +1070,7 @@ __device__ __forceinline__ float tgmm_pdf(const SunskyKArgs& K, const TgmmLds& T
 template <bool FAST>
 __device__ __forceinline__ void compute_pdfs(const SunskyKArgs& K, const TgmmLds& T, float3_ d, bool check_sun,
                                              bool active, float* sky_pdf, float* sun_pdf) {
-    float sin_theta = safe_sqrtf_(fmaf(d.x, d.x, d.y * d.y));
+    float sin_theta = safe_sqrt_sel<FAST>(fmaf(d.x, d.x, d.y * d.y));
     active = active && (d.z >= 0.f) && (sin_theta != 0.f);
     sin_theta = fmaxf(sin_theta, kEpsilon);
     float phi, theta;
@@ -1229,7 +1237,7 @@ __device__ __forceinline__ void pdf_direction_body(const SunskyKArgs& K, const f
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
             float3_ d = to_local(K, mk3(x[j], y[j], z[j]));
-            float st = safe_sqrtf_(fmaf(d.x, d.x, d.y * d.y));
+            float st = safe_sqrt_sel<FAST>(fmaf(d.x, d.x, d.y * d.y));
             bool a = (d.z >= 0.f) && (st != 0.f);
             sin_theta[j] = fmaxf(st, kEpsilon);
             float ph = (FAST ? atan2_fast(d.y, d.x) : atan2f(d.y, d.x)) - (K.sun_phi - 0.5f * kPi);
@@ -1491,7 +1499,7 @@ __device__ __forceinline__ void direct_diffuse_body(
             // ---- BSDF sampling: square_to_cosine_hemisphere (warp.h:412-420), then the miss
             float px, py;
             disk_concentric_dev<FAST>(u2, u3, &px, &py);
-            const float lz = safe_sqrtf_(1.f - fmaf(px, px, py * py));
+            const float lz = safe_sqrt_sel<FAST>(1.f - fmaf(px, px, py * py));
             const float bpdf = kInvPi * lz;
             if (bpdf > 0.f) {
                 const float3_ dw = frame_to_world(fs, ft, nrm, mk3(px, py, lz));

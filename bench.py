@@ -498,7 +498,7 @@ def main():
         del wi5, out5
 
     if rank == 0:
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:   # the CPU baseline: rank 0 at N=1 only
             result["cpu_baseline"] = cpu_baseline(wi.T.cpu().numpy())
         print(json.dumps(result), flush=True)
     if world > 1:

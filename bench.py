@@ -302,6 +302,24 @@ def main():
                                          "achieved_GBps": 12 * bw * bh / (ms * 1e-3) / 1e9,
                                          "note": "sunsky_bake_latlong: directions generated on device, RGB writes only"}
         del bake_out
+        # Reverse-mode AD (f2): sum(d_out * d eval / d params) over the headline directions,
+        # 16 parameter slots accumulated on device (vjp kernel + deterministic block reduce)
+        d_out = torch.ones((3, n), dtype=torch.float32, device=dev)
+        si_v = ss.SurfaceInteraction3f(wi=wi)
+        grad = ems[0].eval_vjp(si_v, d_out)[0]
+        ems[0].eval_vjp(si_v, d_out, grad=grad)
+        tm = KernelTimer()
+        reps = max(3, args.steps // 4)
+        tm.begin()
+        for _ in range(reps):
+            ems[0].eval_vjp(si_v, d_out, grad=grad)
+        tm.end(reps)
+        ms = tm.mean_ms()
+        sec["eval_vjp_rgb_16M"] = {"kernel_ms": ms, "dirs_per_s": n / (ms * 1e-3),
+                                   "achieved_GBps": 24 * n / (ms * 1e-3) / 1e9,
+                                   "note": "sunsky_eval_vjp (RGB): reads wi + d_out (24 B/dir), gradients of "
+                                           "turbidity, albedo, sun_direction; full-precision AD kernels, not tuned"}
+        del d_out, grad
         # C3: spectral eval, 11 model wavelengths broadcast
         spec = ss.SunskyEmitter(dict(sun_dict(3.0), albedo=0.3), "spectral", precision=args.precision, device=dev)
         lams = [float(x) for x in range(320, 721, 40)]

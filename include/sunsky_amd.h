@@ -20,8 +20,11 @@
  *     sample_ray, sample_wavelengths, direct_diffuse) allocate nothing, make no
  *     host-synchronous call and may be captured into a hipGraph
  *     (tests/test_graph_capture.py); a graph snapshots the emitter's parameters
- *     at capture, so recapture after parameters_changed().  eval_jvp, eval_vjp
- *     and bake_latlong upload per-call tables first and are not capturable;
+ *     at capture, so recapture after parameters_changed().  eval_jvp and
+ *     eval_vjp stage their tangent tables host-synchronously when the emitter
+ *     state (or, for eval_jvp, the tangent) changed since the previous call,
+ *     and order successive AD calls through an event; bake_latlong uploads
+ *     per-call tables.  These three are not capturable;
  *   - create/update/destroy are host-synchronous and must not race batch calls
  *     on the same emitter (the reference's parameters_changed() contract).
  */

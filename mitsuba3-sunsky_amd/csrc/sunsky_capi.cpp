@@ -253,6 +253,14 @@ struct sunsky_emitter {
     mutable size_t partials_cap = 0;
     mutable float* d_bake = nullptr;       // bake_latlong angle tables
     mutable size_t bake_cap = 0;
+    // AD tangent tables depend only on the emitter state: restaged when `rev` (bumped by
+    // every upload) or, for the JVP, the requested tangent changes.  `ad_done` is recorded
+    // after each AD launch; the next AD call's stream waits on it, so a later call on
+    // another stream cannot overwrite d_jvp / d_partials under an in-flight kernel.
+    uint64_t rev = 0;
+    mutable uint64_t vjp_rev = ~0ull, jvp_rev = ~0ull;
+    mutable std::vector<float> jvp_key;
+    mutable hipEvent_t ad_done = nullptr;
 
     void upload() {
         int cur = 0;
@@ -268,6 +276,7 @@ struct sunsky_emitter {
         hip_check(hipMemcpy(d_sun_ld, ld.data(), sizeof(float) * std::min<size_t>(ld.size(), kNbWavelengths * kNbSunLdParams),
                             hipMemcpyHostToDevice), "hipMemcpy");
         kargs = model->kargs();
+        ++rev;
         kargs.sun_table = d_sun_table;
         kargs.sun_ld = d_sun_ld;
         if (cur != device) (void)hipSetDevice(cur);
@@ -290,7 +299,15 @@ struct sunsky_emitter {
         if (d_vjp) (void)hipFree(d_vjp);
         if (d_partials) (void)hipFree(d_partials);
         if (d_bake) (void)hipFree(d_bake);
+        if (ad_done) (void)hipEventDestroy(ad_done);
     }
+
+    // Order this AD call after the previous one (any stream), then mark its end.
+    void ad_begin(hipStream_t st) const {
+        if (!ad_done) hip_check(hipEventCreateWithFlags(&ad_done, hipEventDisableTiming), "hipEventCreate");
+        else hip_check(hipStreamWaitEvent(st, ad_done, 0), "hipStreamWaitEvent");
+    }
+    void ad_end(hipStream_t st) const { hip_check(hipEventRecord(ad_done, st), "hipEventRecord"); }
 };
 
 extern "C" {
@@ -667,17 +684,27 @@ int sunsky_eval_jvp(const sunsky_emitter* e, int param, const float* tangent, in
     if (n && nout > 1 && ostride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "out_stride < n");
     if (n && spec && nlam > 1 && lstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "wl_stride < n");
     return guarded([&] {
-        EvalTangent tan = e->model->eval_tangent(param, tangent, tangent_count);   // validates param / count
+        std::vector<float> key(tangent, tangent + std::max(0, tangent_count));
+        key.push_back((float)param);
+        const bool stage = !e->d_jvp || e->jvp_rev != e->rev || key != e->jvp_key;
+        EvalTangent tan;
+        if (stage || n == 0) tan = e->model->eval_tangent(param, tangent, tangent_count);   // validates param / count
         if (n == 0) return;
         if (!e->mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
-        std::vector<float> buf(128 + kSunRgbTableSize, 0.f);
-        std::memcpy(buf.data(), tan.dsky.data(), sizeof(float) * tan.dsky.size());
-        std::memcpy(buf.data() + kNbWavelengths * 10, tan.dsun_local, 3 * sizeof(float));
-        std::memcpy(buf.data() + 128, tan.dsun.data(), sizeof(float) * tan.dsun.size());
-        if (!e->d_jvp) hip_check(hipMalloc(&e->d_jvp, sizeof(float) * buf.size()), "hipMalloc");
-        // a previous eval_jvp of this emitter may still read the buffer
-        hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-        hip_check(hipMemcpy(e->d_jvp, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice), "hipMemcpy");
+        hipStream_t st = (hipStream_t)stream;
+        if (stage) {
+            std::vector<float> buf(128 + kSunRgbTableSize, 0.f);
+            std::memcpy(buf.data(), tan.dsky.data(), sizeof(float) * tan.dsky.size());
+            std::memcpy(buf.data() + kNbWavelengths * 10, tan.dsun_local, 3 * sizeof(float));
+            std::memcpy(buf.data() + 128, tan.dsun.data(), sizeof(float) * tan.dsun.size());
+            if (!e->d_jvp) hip_check(hipMalloc(&e->d_jvp, sizeof(float) * buf.size()), "hipMalloc");
+            // a previous eval_jvp of this emitter may still read the buffer
+            hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+            hip_check(hipMemcpy(e->d_jvp, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice), "hipMemcpy");
+            e->jvp_key = key;
+            e->jvp_rev = e->rev;
+        }
+        e->ad_begin(st);
         SunskyKArgs K = e->kargs;
         const float* jvp = e->d_jvp;
         const float *x = wi.x, *y = wi.y, *z = wi.z;
@@ -690,6 +717,7 @@ int sunsky_eval_jvp(const sunsky_emitter* e, int param, const float* tangent, in
             void* args[] = {&K, &jvp, &x, &y, &z, &lam, &lstride, &nl, &active, &n, &out, &d_out, &ostride, &sign};
             launch(e->mod->jvp_spec, grid_for(e->mod, K_EVAL_SPEC_RAYS_V1, n), (hipStream_t)stream, args);
         }
+        e->ad_end(st);
     });
 }
 
@@ -712,40 +740,45 @@ int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam
         const SunskyModel& M = *e->model;
         const int nch = M.nch();
         const size_t blk = (size_t)kNbWavelengths * 10;
-        std::vector<float> buf(576 + kSunRgbTableSize, 0.f);
-        const float one = 1.f;
-        EvalTangent tT = M.eval_tangent(kJvpTurbidity, &one, 1);
-        std::memcpy(buf.data(), tT.dsky.data(), sizeof(float) * tT.dsky.size());
-        std::memcpy(buf.data() + 576, tT.dsun.data(), sizeof(float) * tT.dsun.size());
-        std::vector<float> ones(nch, 1.f);
-        EvalTangent tA = M.eval_tangent(kJvpAlbedo, ones.data(), nch);
-        std::memcpy(buf.data() + blk, tA.dsky.data(), sizeof(float) * tA.dsky.size());
-        if (!M.active_record())
-            for (int k = 0; k < 3; ++k) {
-                float axis[3] = {0.f, 0.f, 0.f};
-                axis[k] = 1.f;
-                EvalTangent tS = M.eval_tangent(kJvpSunDirection, axis, 3);
-                std::memcpy(buf.data() + (2 + k) * blk, tS.dsky.data(), sizeof(float) * tS.dsky.size());
-                std::memcpy(buf.data() + 5 * blk + 3 * k, tS.dsun_local, 3 * sizeof(float));
-            }
         const KernelId kid = spec ? K_EVAL_SPEC_RAYS_V1 : K_EVAL_RGB_V1;
         const unsigned grid = grid_for(e->mod, kid, n);
-        if (!e->d_vjp) hip_check(hipMalloc(&e->d_vjp, sizeof(float) * buf.size()), "hipMalloc");
-        // a previous eval_vjp of this emitter may still read the tables / partials
-        hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        hipStream_t st = (hipStream_t)stream;
+        const bool stage = !e->d_vjp || e->vjp_rev != e->rev;
+        if (stage || e->partials_cap < grid)
+            hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");   // in-flight readers of the old buffers
         if (e->partials_cap < grid) {
             if (e->d_partials) hip_check(hipFree(e->d_partials), "hipFree");
             e->d_partials = nullptr;
             hip_check(hipMalloc(&e->d_partials, sizeof(float) * 16 * grid), "hipMalloc");
             e->partials_cap = grid;
         }
-        hip_check(hipMemcpy(e->d_vjp, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice), "hipMemcpy");
+        if (stage) {
+            std::vector<float> buf(576 + kSunRgbTableSize, 0.f);
+            const float one = 1.f;
+            EvalTangent tT = M.eval_tangent(kJvpTurbidity, &one, 1);
+            std::memcpy(buf.data(), tT.dsky.data(), sizeof(float) * tT.dsky.size());
+            std::memcpy(buf.data() + 576, tT.dsun.data(), sizeof(float) * tT.dsun.size());
+            std::vector<float> ones(nch, 1.f);
+            EvalTangent tA = M.eval_tangent(kJvpAlbedo, ones.data(), nch);
+            std::memcpy(buf.data() + blk, tA.dsky.data(), sizeof(float) * tA.dsky.size());
+            if (!M.active_record())
+                for (int k = 0; k < 3; ++k) {
+                    float axis[3] = {0.f, 0.f, 0.f};
+                    axis[k] = 1.f;
+                    EvalTangent tS = M.eval_tangent(kJvpSunDirection, axis, 3);
+                    std::memcpy(buf.data() + (2 + k) * blk, tS.dsky.data(), sizeof(float) * tS.dsky.size());
+                    std::memcpy(buf.data() + 5 * blk + 3 * k, tS.dsun_local, 3 * sizeof(float));
+                }
+            if (!e->d_vjp) hip_check(hipMalloc(&e->d_vjp, sizeof(float) * buf.size()), "hipMalloc");
+            hip_check(hipMemcpy(e->d_vjp, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice), "hipMemcpy");
+            e->vjp_rev = e->rev;
+        }
+        e->ad_begin(st);
         SunskyKArgs K = e->kargs;
         const float* vjp = e->d_vjp;
         float* partials = e->d_partials;
         const float *x = wi.x, *y = wi.y, *z = wi.z;
         float sign = -1.f;
-        hipStream_t st = (hipStream_t)stream;
         if (!spec) {
             void* args[] = {&K, &vjp, &x, &y, &z, &active, &n, &d_out, &ostride, &sign, &partials};
             launch(e->mod->vjp_rgb, grid, st, args);
@@ -756,8 +789,9 @@ int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam
         }
         unsigned nb = grid;
         void* rargs[] = {&partials, &nb, &grad};
-        hip_check(hipModuleLaunchKernel(e->mod->grad_reduce, 1, 1, 1, 64, 1, 1, 0, st, rargs, nullptr),
+        hip_check(hipModuleLaunchKernel(e->mod->grad_reduce, 1, 1, 1, 256, 1, 1, 0, st, rargs, nullptr),
                   "hipModuleLaunchKernel");
+        e->ad_end(st);
     });
 }
 

@@ -1645,24 +1645,41 @@ __device__ __forceinline__ float unit_angle_tangent(float3_ a, float3_ b, float3
     return d >= 0.f ? dtemp : -dtemp;
 }
 
+// Value terms of render_sky (sunsky.cpp:550-554) for one channel and direction: they do
+// not depend on the tangent, so the reverse-mode kernels, which differentiate along 5
+// basis tangents per channel, evaluate the exps and the pow once instead of 5 times.
+struct SkyVal { float e1, c1, e2, b, pb, chi, c2; };
+
+__device__ __forceinline__ SkyVal sky_val(const SkyChannel& k, const DirTerms& t) {
+    SkyVal s;
+    s.e1 = expf(k.B * t.r);
+    s.c1 = 1.f + k.A * s.e1;
+    s.e2 = expf(k.E * t.gamma);
+    s.b = 1.f + k.I * k.I - 2.f * k.I * t.cg;
+    s.pb = powf(s.b, 1.5f);
+    s.chi = t.u / s.pb;
+    s.c2 = k.C + k.D * s.e2 + k.F * t.cg2 + k.G * s.chi + k.H * t.sq;
+    return s;
+}
+
+// Tangent of render_sky (dk = d{A..I, rad}, dgamma), unscaled, from its value terms
+__device__ __forceinline__ float sky_tan(const SkyChannel& k, const float* dk, const DirTerms& t, const SkyVal& s,
+                                         float dgamma, float sg) {
+    const float cg = t.cg, dcg = -sg * dgamma;
+    const float dc1 = dk[0] * s.e1 + k.A * s.e1 * t.r * dk[1];
+    const float db = 2.f * k.I * dk[8] - 2.f * dk[8] * cg - 2.f * k.I * dcg;
+    const float dchi = 2.f * cg * dcg / s.pb - 1.5f * s.chi * db / s.b;
+    const float dc2 = dk[2] + dk[3] * s.e2 + k.D * s.e2 * (dk[4] * t.gamma + k.E * dgamma) + dk[5] * t.cg2 +
+                      k.F * 2.f * cg * dcg + dk[6] * s.chi + k.G * dchi + dk[7] * t.sq;
+    return (dc1 * s.c2 + s.c1 * dc2) * k.rad + s.c1 * s.c2 * dk[9];
+}
+
 // render_sky and its tangent (dk = d{A..I, rad}), unscaled
 __device__ __forceinline__ void sky_jvp(const SkyChannel& k, const float* dk, const DirTerms& t, float dgamma,
                                         float sg, float* L, float* dL) {
-    const float cg = t.cg, dcg = -sg * dgamma;
-    const float e1 = expf(k.B * t.r);
-    const float c1 = 1.f + k.A * e1;
-    const float dc1 = dk[0] * e1 + k.A * e1 * t.r * dk[1];
-    const float e2 = expf(k.E * t.gamma);
-    const float b = 1.f + k.I * k.I - 2.f * k.I * cg;
-    const float pb = powf(b, 1.5f);
-    const float chi = t.u / pb;
-    const float db = 2.f * k.I * dk[8] - 2.f * dk[8] * cg - 2.f * k.I * dcg;
-    const float dchi = 2.f * cg * dcg / pb - 1.5f * chi * db / b;
-    const float c2 = k.C + k.D * e2 + k.F * t.cg2 + k.G * chi + k.H * t.sq;
-    const float dc2 = dk[2] + dk[3] * e2 + k.D * e2 * (dk[4] * t.gamma + k.E * dgamma) + dk[5] * t.cg2 +
-                      k.F * 2.f * cg * dcg + dk[6] * chi + k.G * dchi + dk[7] * t.sq;
-    *L = c1 * c2 * k.rad;
-    *dL = (dc1 * c2 + c1 * dc2) * k.rad + c1 * c2 * dk[9];
+    const SkyVal s = sky_val(k, t);
+    *L = s.c1 * s.c2 * k.rad;
+    *dL = sky_tan(k, dk, t, s, dgamma, sg);
 }
 
 // cos_psi (sunsky.h:385-392) and its tangent
@@ -1881,16 +1898,13 @@ __device__ __forceinline__ void eval_vjp_rgb_body(const SunskyKArgs& K, const fl
 #pragma unroll 1
         for (int c = 0; c < 3; ++c) {
             const float cot = dout[(size_t)c * ostride + i] * cie;
-            float v, d;
-            sky_jvp(K.sky[c], L.dsky[0] + c * 10, t, 0.f, sg, &v, &d);
-            g[0] += cot * K.sky_scale * d;
-            sky_jvp(K.sky[c], L.dsky[1] + c * 10, t, 0.f, sg, &v, &d);
-            g[1 + c] += cot * K.sky_scale * d;
+            const SkyChannel& kc = K.sky[c];
+            const SkyVal sv = sky_val(kc, t);   // once for the 5 tangents
+            const float cs = cot * K.sky_scale;
+            g[0] += cs * sky_tan(kc, L.dsky[0] + c * 10, t, sv, 0.f, sg);
+            g[1 + c] += cs * sky_tan(kc, L.dsky[1] + c * 10, t, sv, 0.f, sg);
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                sky_jvp(K.sky[c], L.dsky[2 + k] + c * 10, t, dgs[k], sg, &v, &d);
-                g[12 + k] += cot * K.sky_scale * d;
-            }
+            for (int k = 0; k < 3; ++k) g[12 + k] += cs * sky_tan(kc, L.dsky[2 + k] + c * 10, t, sv, dgs[k], sg);
             if (t.hit_sun) {
                 const float* S = K.sun_table + pos * (3 * kNbSunCtrlPts * kNbSunLdParams) + c * (kNbSunCtrlPts * kNbSunLdParams);
                 const float* dS = dsun_tab + pos * (3 * kNbSunCtrlPts * kNbSunLdParams) + c * (kNbSunCtrlPts * kNbSunLdParams);
@@ -1949,22 +1963,27 @@ __device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const f
             float f = nw - (float)lo;
             const bool has_hi = f != 0.f && hi < kNbWavelengths;
             const float wlo = f != 0.f ? 1.f - f : 1.f, whi = f;   // lerp weights (f = 0: low channel only)
-            float v, da, db = 0.f;
-            // turbidity, albedo (diagonal), sun axes: each lerped over the two channels
-            sky_jvp(K.sky[lo], L.dsky[0] + lo * 10, t, 0.f, sg, &v, &da);
-            if (has_hi) sky_jvp(K.sky[hi], L.dsky[0] + hi * 10, t, 0.f, sg, &v, &db);
+            float da, db = 0.f;
+            // turbidity, albedo (diagonal), sun axes: each lerped over the two channels; the
+            // value terms of each channel once for its 5 tangents
+            const SkyChannel &klo = K.sky[lo], &khi = K.sky[has_hi ? hi : lo];
+            const SkyVal slo = sky_val(klo, t);
+            SkyVal shi = slo;
+            if (has_hi) shi = sky_val(khi, t);
+            da = sky_tan(klo, L.dsky[0] + lo * 10, t, slo, 0.f, sg);
+            if (has_hi) db = sky_tan(khi, L.dsky[0] + hi * 10, t, shi, 0.f, sg);
             g[0] += cot * K.sky_scale * (wlo * da + whi * db);
-            sky_jvp(K.sky[lo], L.dsky[1] + lo * 10, t, 0.f, sg, &v, &da);
+            da = sky_tan(klo, L.dsky[1] + lo * 10, t, slo, 0.f, sg);
             g[1 + lo] += cot * K.sky_scale * wlo * da;
             if (has_hi) {
-                sky_jvp(K.sky[hi], L.dsky[1] + hi * 10, t, 0.f, sg, &v, &db);
+                db = sky_tan(khi, L.dsky[1] + hi * 10, t, shi, 0.f, sg);
                 g[1 + hi] += cot * K.sky_scale * whi * db;
             }
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 db = 0.f;
-                sky_jvp(K.sky[lo], L.dsky[2 + k] + lo * 10, t, dgs[k], sg, &v, &da);
-                if (has_hi) sky_jvp(K.sky[hi], L.dsky[2 + k] + hi * 10, t, dgs[k], sg, &v, &db);
+                da = sky_tan(klo, L.dsky[2 + k] + lo * 10, t, slo, dgs[k], sg);
+                if (has_hi) db = sky_tan(khi, L.dsky[2 + k] + hi * 10, t, shi, dgs[k], sg);
                 g[12 + k] += cot * K.sky_scale * (wlo * da + whi * db);
             }
             if (t.hit_sun) {
@@ -2137,13 +2156,23 @@ extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_vjp_spec(
     eval_vjp_spec_body(K, vjp, wx, wy, wz, lam, lstride, nlam, active, n, dout, ostride, sign, partials);
 }
 // grad[p] += sum over blocks (in block order) of partials[block][p]; one wave.
-extern "C" __global__ __launch_bounds__(64) void sunsky_grad_reduce(const float* partials, unsigned nblocks,
-                                                                     float* grad) {
-    const int p = threadIdx.x;
-    if (p < kGradCount) {
-        float acc = 0.f;
-        for (unsigned b = 0; b < nblocks; ++b) acc += partials[(size_t)b * kGradCount + p];
-        grad[p] += acc;
+// grad[p] += sum over blocks of partials[b][p], one 256-thread workgroup: thread (s, p)
+// sums blocks s, s + 16, s + 32, ... in order, then thread p adds the 16 segment sums
+// in order.  A fixed summation order (deterministic), 16 independent load streams per
+// gradient instead of one serial chain over all blocks.
+extern "C" __global__ __launch_bounds__(256) void sunsky_grad_reduce(const float* partials, unsigned nblocks,
+                                                                      float* grad) {
+    constexpr int kSeg = 256 / kGradCount;
+    __shared__ float seg[kSeg][kGradCount];
+    const int p = threadIdx.x % kGradCount, sgi = threadIdx.x / kGradCount;
+    float acc = 0.f;
+    for (unsigned b = sgi; b < nblocks; b += kSeg) acc += partials[(size_t)b * kGradCount + p];
+    seg[sgi][p] = acc;
+    __syncthreads();
+    if (threadIdx.x < kGradCount) {
+        float t = 0.f;
+        for (int k = 0; k < kSeg; ++k) t += seg[k][threadIdx.x];
+        grad[threadIdx.x] += t;
     }
 }
 

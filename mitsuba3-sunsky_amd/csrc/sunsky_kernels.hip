@@ -1656,7 +1656,7 @@ __device__ __forceinline__ SkyVal sky_val(const SkyChannel& k, const DirTerms& t
     s.c1 = 1.f + k.A * s.e1;
     s.e2 = expf(k.E * t.gamma);
     s.b = 1.f + k.I * k.I - 2.f * k.I * t.cg;
-    s.pb = powf(s.b, 1.5f);
+    s.pb = s.b * sqrtf(s.b);   // b^1.5 (b > 0): within 2 ulp of powf, without its log/exp registers
     s.chi = t.u / s.pb;
     s.c2 = k.C + k.D * s.e2 + k.F * t.cg2 + k.G * s.chi + k.H * t.sq;
     return s;
@@ -1689,11 +1689,18 @@ __device__ __forceinline__ void cos_psi_jvp(const SunskyKArgs& K, const DirTerms
     *dcp = *cp > 0.f ? -K.inv_sin2_half_ap * sg * t.cg * dgamma / *cp : 0.f;
 }
 
+// sin(gamma) for gamma = 2 asin(h) or pi - 2 asin(h): 2 h sqrt(1 - h^2), a few ulp from
+// sinf(gamma) without libm's large-argument reduction (whose registers set the AD
+// kernels' VGPR count).  Only the tangents use it.
+__device__ __forceinline__ float sin_gamma(const DirTerms& t) {
+    return 2.f * t.h * sqrtf(fmaxf(1.f - t.h * t.h, 0.f));
+}
+
 // Shared per-direction setup: reference-order DirTerms (cg = cos(gamma)), sin(gamma), d gamma.
 __device__ __forceinline__ DirTerms jvp_dir(const SunskyKArgs& K, const JvpLds& J, float3_ wo, bool m, float* sg,
                                             float* dgamma) {
     DirTerms t = dir_terms<false>(K, wo, m);
-    *sg = sinf(t.gamma);
+    *sg = sin_gamma(t);
     *dgamma = unit_angle_tangent(mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), wo,
                                  mk3(J.dsun_local[0], J.dsun_local[1], J.dsun_local[2]));
     return t;
@@ -1883,7 +1890,7 @@ __device__ __forceinline__ void eval_vjp_rgb_body(const SunskyKArgs& K, const fl
         float3_ wo = to_local(K, mk3(sign * wx[i], sign * wy[i], sign * wz[i]));
         DirTerms t = dir_terms<false>(K, wo, m);
         if (!t.active) continue;
-        const float sg = sinf(t.gamma);
+        const float sg = sin_gamma(t);
         float dgs[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) dgs[k] = unit_angle_tangent(sn, wo, mk3(L.dlocal[k][0], L.dlocal[k][1], L.dlocal[k][2]));
@@ -1943,7 +1950,7 @@ __device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const f
         float3_ wo = to_local(K, mk3(sign * wx[i], sign * wy[i], sign * wz[i]));
         DirTerms t = dir_terms<false>(K, wo, m);
         if (!t.active) continue;
-        const float sg = sinf(t.gamma);
+        const float sg = sin_gamma(t);
         float dgs[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) dgs[k] = unit_angle_tangent(sn, wo, mk3(L.dlocal[k][0], L.dlocal[k][1], L.dlocal[k][2]));

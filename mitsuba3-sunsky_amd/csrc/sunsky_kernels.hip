@@ -1631,7 +1631,9 @@ __device__ __forceinline__ void bake_spec_body(const SunskyKArgs& K, LatLong G, 
 // ======================================================================
 constexpr int kJvpSunOffset = 128;
 
-struct JvpLds { float dsky[kNbWavelengths * 10]; float dsun_local[4]; };
+// sky: the channel constants, indexed per lane by the spectral AD kernels (a per-lane
+// index into the kernarg block would gather from memory, 13 loads per channel).
+struct JvpLds { float dsky[kNbWavelengths * 10]; float dsun_local[4]; SkyChannel sky[kNbWavelengths]; };
 
 // d unit_angle(a, b) along da (sunsky.cpp:311): gamma = 2 asin(h) or pi - 2 asin(h),
 // h = |b -/+ a| / 2.
@@ -1706,7 +1708,8 @@ __device__ __forceinline__ DirTerms jvp_dir(const SunskyKArgs& K, const JvpLds& 
     return t;
 }
 
-__device__ __forceinline__ void stage_jvp(const float* jvp, JvpLds* J, int nch) {
+__device__ __forceinline__ void stage_jvp(const SunskyKArgs& K, const float* jvp, JvpLds* J, int nch) {
+    lds_copy(J->sky, K.sky, kNbWavelengths);
     for (int i = threadIdx.x; i < nch * 10; i += blockDim.x) J->dsky[i] = jvp[i];
     if (threadIdx.x < 3) J->dsun_local[threadIdx.x] = jvp[kNbWavelengths * 10 + threadIdx.x];
     __syncthreads();
@@ -1718,7 +1721,7 @@ __device__ __forceinline__ void eval_jvp_rgb_body(const SunskyKArgs& K, const fl
                                                   size_t n, float* __restrict__ out, float* __restrict__ dout,
                                                   size_t ostride, float sign) {
     __shared__ JvpLds J;
-    stage_jvp(jvp, &J, 3);
+    stage_jvp(K, jvp, &J, 3);
     const float* dsun_tab = jvp + kJvpSunOffset;
     const float cie = (float)kCieYNormalization, conv = (float)kSpecToRgbSunConv;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -1770,7 +1773,7 @@ __device__ __forceinline__ void eval_jvp_spec_body(const SunskyKArgs& K, const f
                                                    size_t n, float* __restrict__ out, float* __restrict__ dout,
                                                    size_t ostride, float sign) {
     __shared__ JvpLds J;
-    stage_jvp(jvp, &J, kNbWavelengths);
+    stage_jvp(K, jvp, &J, kNbWavelengths);
     const float* dsun_tab = jvp + kJvpSunOffset;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -1793,8 +1796,8 @@ __device__ __forceinline__ void eval_jvp_spec_body(const SunskyKArgs& K, const f
                 int lo = (int)floorf(nw), hi = lo + 1;
                 float f = nw - (float)lo;
                 float la, dla, lb = 0.f, dlb = 0.f;
-                sky_jvp(K.sky[lo], J.dsky + lo * 10, t, dg, sg, &la, &dla);
-                if (hi < kNbWavelengths) sky_jvp(K.sky[hi], J.dsky + hi * 10, t, dg, sg, &lb, &dlb);
+                sky_jvp(J.sky[lo], J.dsky + lo * 10, t, dg, sg, &la, &dla);
+                if (hi < kNbWavelengths) sky_jvp(J.sky[hi], J.dsky + hi * 10, t, dg, sg, &lb, &dlb);
                 res = K.sky_scale * (f != 0.f ? lerpf_(la, lb, f) : la);
                 dres = K.sky_scale * (f != 0.f ? lerpf_(dla, dlb, f) : dla);
                 if (t.hit_sun) {
@@ -1838,6 +1841,7 @@ constexpr int kGradCount = 16;           // 0: T, 1..11: albedo channel, 12..14:
 constexpr int kVjpSunOffset = 576;
 
 struct VjpLds {
+    SkyChannel sky[kNbWavelengths];   // per-lane channel index in the spectral kernel (see JvpLds)
     float dsky[5][kNbWavelengths * 10];
     float dlocal[3][3];
     float red[SS_BLOCK / 64][kGradCount];
@@ -1865,7 +1869,8 @@ __device__ __forceinline__ void block_reduce_grad(VjpLds& L, const float g[kGrad
     }
 }
 
-__device__ __forceinline__ void stage_vjp(const float* vjp, VjpLds* L) {
+__device__ __forceinline__ void stage_vjp(const SunskyKArgs& K, const float* vjp, VjpLds* L) {
+    lds_copy(L->sky, K.sky, kNbWavelengths);
     for (int i = threadIdx.x; i < 5 * kNbWavelengths * 10; i += blockDim.x) (&L->dsky[0][0])[i] = vjp[i];
     if (threadIdx.x < 9) (&L->dlocal[0][0])[threadIdx.x] = vjp[5 * kNbWavelengths * 10 + threadIdx.x];
     __syncthreads();
@@ -1877,7 +1882,7 @@ __device__ __forceinline__ void eval_vjp_rgb_body(const SunskyKArgs& K, const fl
                                                   size_t n, const float* __restrict__ dout, size_t ostride,
                                                   float sign, float* __restrict__ partials) {
     __shared__ VjpLds L;
-    stage_vjp(vjp, &L);
+    stage_vjp(K, vjp, &L);
     const float* dsun_tab = vjp + kVjpSunOffset;
     const float cie = (float)kCieYNormalization, conv = (float)kSpecToRgbSunConv;
     const float3_ sn = mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]);
@@ -1938,7 +1943,7 @@ __device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const f
                                                    size_t n, const float* __restrict__ dout, size_t ostride,
                                                    float sign, float* __restrict__ partials) {
     __shared__ VjpLds L;
-    stage_vjp(vjp, &L);
+    stage_vjp(K, vjp, &L);
     const float* dsun_tab = vjp + kVjpSunOffset;
     const float3_ sn = mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]);
     float g[kGradCount];
@@ -1973,7 +1978,7 @@ __device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const f
             float da, db = 0.f;
             // turbidity, albedo (diagonal), sun axes: each lerped over the two channels; the
             // value terms of each channel once for its 5 tangents
-            const SkyChannel &klo = K.sky[lo], &khi = K.sky[has_hi ? hi : lo];
+            const SkyChannel &klo = L.sky[lo], &khi = L.sky[has_hi ? hi : lo];
             const SkyVal slo = sky_val(klo, t);
             SkyVal shi = slo;
             if (has_hi) shi = sky_val(khi, t);

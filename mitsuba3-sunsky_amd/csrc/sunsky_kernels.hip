@@ -1650,7 +1650,7 @@ __device__ __forceinline__ float unit_angle_tangent(float3_ a, float3_ b, float3
 // Value terms of render_sky (sunsky.cpp:550-554) for one channel and direction: they do
 // not depend on the tangent, so the reverse-mode kernels, which differentiate along 5
 // basis tangents per channel, evaluate the exps and the pow once instead of 5 times.
-struct SkyVal { float e1, c1, e2, b, pb, chi, c2; };
+struct SkyVal { float e1, c1, e2, b, pb, chi, c2, inv_pb, inv_b; };
 
 __device__ __forceinline__ SkyVal sky_val(const SkyChannel& k, const DirTerms& t) {
     SkyVal s;
@@ -1661,6 +1661,8 @@ __device__ __forceinline__ SkyVal sky_val(const SkyChannel& k, const DirTerms& t
     s.pb = s.b * sqrtf(s.b);   // b^1.5 (b > 0): within 2 ulp of powf, without its log/exp registers
     s.chi = t.u / s.pb;
     s.c2 = k.C + k.D * s.e2 + k.F * t.cg2 + k.G * s.chi + k.H * t.sq;
+    s.inv_pb = 1.f / s.pb;   // the tangents multiply: 2 divisions per tangent and channel fewer
+    s.inv_b = 1.f / s.b;
     return s;
 }
 
@@ -1670,10 +1672,29 @@ __device__ __forceinline__ float sky_tan(const SkyChannel& k, const float* dk, c
     const float cg = t.cg, dcg = -sg * dgamma;
     const float dc1 = dk[0] * s.e1 + k.A * s.e1 * t.r * dk[1];
     const float db = 2.f * k.I * dk[8] - 2.f * dk[8] * cg - 2.f * k.I * dcg;
-    const float dchi = 2.f * cg * dcg / s.pb - 1.5f * s.chi * db / s.b;
+    const float dchi = 2.f * cg * dcg * s.inv_pb - 1.5f * s.chi * db * s.inv_b;
     const float dc2 = dk[2] + dk[3] * s.e2 + k.D * s.e2 * (dk[4] * t.gamma + k.E * dgamma) + dk[5] * t.cg2 +
                       k.F * 2.f * cg * dcg + dk[6] * s.chi + k.G * dchi + dk[7] * t.sq;
     return (dc1 * s.c2 + s.c1 * dc2) * k.rad + s.c1 * s.c2 * dk[9];
+}
+
+// unit_angle_tangent split for several tangents da of one (a, b): the per-direction part
+// (the chord v and 1 / (2 h sqrt(1 - h^2)) with the branch sign) once, then one dot per tangent.
+struct UnitAngleTan { float3_ v; float f, sd; };
+
+__device__ __forceinline__ UnitAngleTan unit_angle_tan_setup(float3_ a, float3_ b) {
+    UnitAngleTan u;
+    const float d = dot3(a, b);
+    u.v = mk3(b.x - mulsignf_(a.x, d), b.y - mulsignf_(a.y, d), b.z - mulsignf_(a.z, d));
+    u.sd = d;
+    const float h = 0.5f * sqrtf(dot3(u.v, u.v));
+    u.f = h > 0.f ? (d >= 0.f ? 1.f : -1.f) / (2.f * h * sqrtf(1.f - h * h)) : 0.f;
+    return u;
+}
+
+__device__ __forceinline__ float unit_angle_tan_apply(const UnitAngleTan& u, float3_ da) {
+    const float3_ dv = mk3(-mulsignf_(da.x, u.sd), -mulsignf_(da.y, u.sd), -mulsignf_(da.z, u.sd));
+    return dot3(u.v, dv) * u.f;
 }
 
 // render_sky and its tangent (dk = d{A..I, rad}), unscaled
@@ -1897,8 +1918,9 @@ __device__ __forceinline__ void eval_vjp_rgb_body(const SunskyKArgs& K, const fl
         if (!t.active) continue;
         const float sg = sin_gamma(t);
         float dgs[3];
+        const UnitAngleTan ua = unit_angle_tan_setup(sn, wo);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) dgs[k] = unit_angle_tangent(sn, wo, mk3(L.dlocal[k][0], L.dlocal[k][1], L.dlocal[k][2]));
+        for (int k = 0; k < 3; ++k) dgs[k] = unit_angle_tan_apply(ua, mk3(L.dlocal[k][0], L.dlocal[k][1], L.dlocal[k][2]));
         int pos = 0;
         float xs = 0.f, cp = 0.f, dcps[3] = {0.f, 0.f, 0.f};
         if (t.hit_sun) {
@@ -1957,8 +1979,9 @@ __device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const f
         if (!t.active) continue;
         const float sg = sin_gamma(t);
         float dgs[3];
+        const UnitAngleTan ua = unit_angle_tan_setup(sn, wo);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) dgs[k] = unit_angle_tangent(sn, wo, mk3(L.dlocal[k][0], L.dlocal[k][1], L.dlocal[k][2]));
+        for (int k = 0; k < 3; ++k) dgs[k] = unit_angle_tan_apply(ua, mk3(L.dlocal[k][0], L.dlocal[k][1], L.dlocal[k][2]));
         int pos = 0;
         float xs = 0.f, cp = 0.f, dcps[3] = {0.f, 0.f, 0.f};
         if (t.hit_sun) {

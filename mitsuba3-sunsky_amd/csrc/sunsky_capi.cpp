@@ -740,10 +740,10 @@ int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam
         const SunskyModel& M = *e->model;
         const int nch = M.nch();
         const size_t blk = (size_t)kNbWavelengths * 10;
-        // 4 workgroups per CU (the ~200-VGPR kernels hold 2 per CU at a time): few per-block
+        // 6 workgroups per CU (the RGB kernel holds 3 per CU at a time, 134 VGPRs): few per-block
         // partials, so the one-workgroup reduce below stays short (16384 partials took 0.3 ms)
         const unsigned grid = (unsigned)std::max<size_t>(
-            1, std::min<size_t>((n + kBlock - 1) / kBlock, (size_t)e->mod->cu_count * 4));
+            1, std::min<size_t>((n + kBlock - 1) / kBlock, (size_t)e->mod->cu_count * 6));
         hipStream_t st = (hipStream_t)stream;
         const bool stage = !e->d_vjp || e->vjp_rev != e->rev;
         if (stage || e->partials_cap < grid)

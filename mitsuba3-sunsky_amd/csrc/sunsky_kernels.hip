@@ -1943,7 +1943,9 @@ __device__ __forceinline__ void eval_vjp_rgb_body(const SunskyKArgs& K, const fl
                 const float* S = K.sun_table + pos * (3 * kNbSunCtrlPts * kNbSunLdParams) + c * (kNbSunCtrlPts * kNbSunLdParams);
                 const float* dS = dsun_tab + pos * (3 * kNbSunCtrlPts * kNbSunLdParams) + c * (kNbSunCtrlPts * kNbSunLdParams);
                 float dT = 0.f, dC = 0.f;   // d/dT, d/d cos_psi
+#pragma unroll 1
                 for (int kk = 0; kk < kNbSunCtrlPts; ++kk)
+#pragma unroll 1
                     for (int j = 0; j < kNbSunLdParams; ++j) {
                         const float xk = powif_(xs, kk);
                         dT += xk * powif_(cp, j) * dS[kk * kNbSunLdParams + j];
@@ -1989,6 +1991,7 @@ __device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const f
 #pragma unroll
             for (int k = 0; k < 3; ++k) cos_psi_jvp(K, t, sg, dgs[k], &cp, &dcps[k]);
         }
+#pragma unroll 1
         for (int q = 0; q < nlam; ++q) {
             const float cot = dout[(size_t)q * ostride + i];
             const float lambda = lam[(size_t)q * lstride + i];
@@ -2031,6 +2034,7 @@ __device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const f
                     dsun = lerpf_(dsa, dsb, f);
                 }
                 float ld = sun_limb_darkening(K.sun_ld, lo, hi, f, cp), dldc = 0.f;
+#pragma unroll 1
                 for (int j = 1; j < kNbSunLdParams; ++j) {
                     float a = K.sun_ld[lo * kNbSunLdParams + j], coef = a;
                     if (f != 0.f) coef = lerpf_(a, hi < kNbWavelengths ? K.sun_ld[hi * kNbSunLdParams + j] : 0.f, f);

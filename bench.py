@@ -318,7 +318,7 @@ def main():
         sec["eval_vjp_rgb_16M"] = {"kernel_ms": ms, "dirs_per_s": n / (ms * 1e-3),
                                    "achieved_GBps": 24 * n / (ms * 1e-3) / 1e9,
                                    "note": "sunsky_eval_vjp (RGB): reads wi + d_out (24 B/dir), gradients of "
-                                           "turbidity, albedo, sun_direction; full-precision AD kernels, not tuned"}
+                                           "turbidity, albedo, sun_direction (full-precision AD kernel + deterministic reduce)"}
         del d_out, grad
         # C3: spectral eval, 11 model wavelengths broadcast
         spec = ss.SunskyEmitter(dict(sun_dict(3.0), albedo=0.3), "spectral", precision=args.precision, device=dev)

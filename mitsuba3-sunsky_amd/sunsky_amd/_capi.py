@@ -23,6 +23,7 @@ TABLES = {"sky_params": 0, "sky_radiance": 1, "sun_radiance": 2, "sun_ld": 3, "g
           "gaussian_cdf": 5, "spectral_pdf": 6, "spectral_cdf": 7, "albedo": 8}
 FLAG_INFINITE, FLAG_SPATIALLY_VARYING = 0x04, 0x10
 PARAMS = {"turbidity": 0, "albedo": 1, "sun_direction": 2}   # sunsky_param (differentiable, sunsky.cpp:220-240)
+MAX_LAMBDA_PER_RAY = 16   # kMaxLambdaPerRay (csrc/sunsky_types.h)
 GRAD_COUNT, GRAD_TURBIDITY, GRAD_ALBEDO, GRAD_SUN_DIRECTION = 16, 0, 1, 12   # eval_vjp gradient layout
 
 c_float_p = C.POINTER(C.c_float)

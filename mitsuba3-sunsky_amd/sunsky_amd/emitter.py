@@ -245,26 +245,68 @@ class SunskyEmitter:
             t = t.unsqueeze(0)
         return t.contiguous()
 
+    def _plane(self, t, n, name):
+        """One fp32 plane of n values on the emitter's device (a 0-d value is broadcast)."""
+        t = self._f32(t)
+        if t.dim() == 0:
+            t = t.expand(n).contiguous()
+        if t.dim() != 1 or t.shape[0] != n:
+            raise ValueError(f"{name} must have {n} values (one per lane), got shape {tuple(t.shape)}")
+        return t
+
+    def _planes(self, t, rows, n, name):
+        """A (rows, n) SoA fp32 tensor on the emitter's device."""
+        t = self._f32(t)
+        if t.dim() != 2 or t.shape[0] != rows or t.shape[1] != n:
+            raise ValueError(f"{name} must be a ({rows}, {n}) tensor, got shape {tuple(t.shape)}")
+        return t
+
+    def _out(self, out, shape, row_stride_ok=False):
+        """Caller-provided output: float32 on the emitter's device, the given shape, planes
+        contiguous (rows may be strided when row_stride_ok)."""
+        if out is None:
+            return torch.empty(shape, dtype=torch.float32, device=self.device)
+        if (not isinstance(out, torch.Tensor) or out.dtype != torch.float32 or out.device != self.device
+                or tuple(out.shape) != tuple(shape)):
+            raise ValueError(f"out must be a float32 tensor of shape {tuple(shape)} on {self.device}")
+        if not (out.is_contiguous() or (row_stride_ok and out.stride(-1) == 1 and out.stride(0) >= shape[-1])):
+            raise ValueError("out planes must be contiguous")
+        return out
+
     def _mask(self, active, n):
         if active is None or active is True:
             return None
         a = torch.as_tensor(active, device=self.device)
         if a.dim() == 0:
             a = a.expand(n)
+        if a.dim() != 1 or a.shape[0] != n:
+            raise ValueError(f"active mask must have {n} entries, got shape {tuple(a.shape)}")
         return a.to(torch.uint8).contiguous()
 
-    def _vec_in(self, v):
+    def _vec_in(self, v, n=None, name="vectors"):
         v = self._f32(v)
         if v.dim() != 2 or v.shape[0] != 3:
-            raise ValueError("vectors are SoA tensors of shape (3, n)")
+            raise ValueError(f"{name} are SoA tensors of shape (3, n)")
+        if n is not None and v.shape[1] != n:
+            raise ValueError(f"{name} must have {n} lanes, got {v.shape[1]}")
         return v, Vec3In(v[0].data_ptr(), v[1].data_ptr(), v[2].data_ptr())
 
     def _wavelengths(self, wl, n):
+        """Per-lane wavelengths as a (k, n) plane set, 1 <= k <= 16 (Spectrum<Float, k>); a scalar
+        or a single value is broadcast to every lane."""
+        if wl is None:
+            raise ValueError("spectral variants need wavelengths")
         wl = torch.as_tensor(wl, dtype=torch.float32, device=self.device)
-        if wl.dim() == 0:
-            wl = wl.expand(1, n)
+        if wl.dim() == 0 or (wl.dim() == 1 and wl.numel() == 1):
+            wl = wl.reshape(1, 1).expand(1, n)
         elif wl.dim() == 1:
-            wl = wl.view(1, -1).expand(1, n) if wl.numel() == 1 else wl.view(1, n)
+            if wl.shape[0] != n:
+                raise ValueError(f"wavelengths: {wl.shape[0]} values for {n} lanes")
+            wl = wl.view(1, n)
+        elif wl.dim() != 2 or wl.shape[1] != n:
+            raise ValueError(f"wavelengths must be (k, {n}), got shape {tuple(wl.shape)}")
+        if not 1 <= wl.shape[0] <= _capi.MAX_LAMBDA_PER_RAY:
+            raise ValueError(f"1..{_capi.MAX_LAMBDA_PER_RAY} wavelengths per lane, got {wl.shape[0]}")
         return wl.contiguous()
 
     # ------------------------------------------------------------ hot path
@@ -330,6 +372,10 @@ class SunskyEmitter:
             raise ValueError(f"d_out must have shape ({k}, {n})")
         if grad is None:
             grad = torch.zeros(_capi.GRAD_COUNT, dtype=torch.float32, device=self.device)
+        elif (not isinstance(grad, torch.Tensor) or grad.dtype != torch.float32 or grad.device != self.device
+              or not grad.is_contiguous() or grad.numel() < _capi.GRAD_COUNT):
+            raise ValueError(f"grad must be a contiguous float32 tensor of >= {_capi.GRAD_COUNT} values on "
+                             f"{self.device}")
         check(lib().sunsky_eval_vjp(self._h, vin, _ptr(wl), k if self.is_spectral else 0, n, _ptr(m), n,
                                     _ptr(d_out), n, _ptr(grad), self._stream()))
         nch = 11 if self.is_spectral else 3
@@ -350,8 +396,7 @@ class SunskyEmitter:
             k, lam_p, m = len(lam), _fa(lam), len(lam)
         else:
             k, lam_p, m = 3, None, 0
-        if out is None:
-            out = torch.empty((k, height, width), dtype=torch.float32, device=self.device)
+        out = self._out(out, (k, height, width))
         check(lib().sunsky_bake_latlong(self._h, width, height, float(theta[0]), float(theta[1]), float(phi[0]),
                                         float(phi[1]), lam_p, m, _ptr(out), height * width, self._stream()))
         return out
@@ -366,15 +411,16 @@ class SunskyEmitter:
         if self.is_spectral:
             if wavelengths is None:
                 raise ValueError("spectral direct lighting needs per-point wavelengths")
-            wl = self._f32(wavelengths, rows=1)
-            if wl.dim() == 1:
-                wl = wl.view(1, -1)
+            wl = self._wavelengths(wavelengths, n)
+            if wl.shape[0] > 4:
+                raise ValueError("direct_diffuse takes up to 4 wavelengths per point")
             k, lam_p, lstride = wl.shape[0], _ptr(wl), wl.stride(0)
         else:
             wl, k, lam_p, lstride = None, 3, None, 0
-        rho = self._f32(reflectance)
-        if out is None:
-            out = torch.empty((k, n), dtype=torch.float32, device=self.device)
+        rho = None
+        if reflectance is not None:
+            rho = self._planes(reflectance, k, n, "reflectance")
+        out = self._out(out, (k, n))
         check(lib().sunsky_direct_diffuse(self._h, nin, _ptr(rho), lam_p, k if self.is_spectral else 0, lstride,
                                           int(seed) & 0xFFFFFFFF, int(spp), n, _ptr(out), out.stride(0),
                                           self._stream()))
@@ -385,8 +431,7 @@ class SunskyEmitter:
         wi, vin = self._vec_in(wi)
         n = wi.shape[1]
         lam = [float(x) for x in np.atleast_1d(np.asarray(wavelengths, dtype=np.float32))]
-        if out is None:
-            out = torch.empty((len(lam), n), dtype=torch.float32, device=self.device)
+        out = self._out(out, (len(lam), n), row_stride_ok=True)
         m = self._mask(active, n)
         check(lib().sunsky_eval_spectral_broadcast(self._h, vin, _fa(lam), len(lam), _ptr(m), n,
                                                    _ptr(out), out.stride(0), self._stream()))
@@ -404,7 +449,7 @@ class SunskyEmitter:
         m = self._mask(active, n)
         p = getattr(it, "p", None) if it is not None else None
         if p is not None:
-            p, pin = self._vec_in(p)
+            p, pin = self._vec_in(p, n, "it.p")
         else:
             pin = Vec3In(None, None, None)
         d = torch.empty((3, n), dtype=torch.float32, device=self.device)
@@ -441,11 +486,16 @@ class SunskyEmitter:
 
     def sample_ray(self, time, wavelength_sample, sample2, sample3, active=None):
         """sample_ray(time, wavelength_sample, sample2, sample3, active) -- sunsky.cpp:354-397."""
-        s2, s3 = self._f32(sample2), self._f32(sample3)
+        s2 = self._f32(sample2)
+        if s2.dim() != 2 or s2.shape[0] != 2:
+            raise ValueError("sample2 is a (2, n) tensor")
         n = s2.shape[1]
-        ws = self._f32(wavelength_sample)
-        if ws is not None and ws.dim() == 0:
-            ws = ws.expand(n).contiguous()
+        s3 = self._planes(sample3, 2, n, "sample3")
+        ws = None
+        if self.is_spectral or wavelength_sample is not None:
+            if wavelength_sample is None:
+                raise ValueError("spectral sample_ray needs a wavelength sample")
+            ws = self._plane(wavelength_sample, n, "wavelength_sample")
         m = self._mask(active, n)
         o = torch.empty((3, n), dtype=torch.float32, device=self.device)
         d = torch.empty((3, n), dtype=torch.float32, device=self.device)
@@ -461,9 +511,7 @@ class SunskyEmitter:
         """sample_wavelengths(si, sample, active) -- sunsky.cpp:463-480."""
         wi, vin = self._vec_in(si.wi)
         n = wi.shape[1]
-        s = self._f32(sample)
-        if s is not None and s.dim() == 0:
-            s = s.expand(n).contiguous()
+        s = self._plane(sample, n, "sample") if (sample is not None or self.is_spectral) else None
         m = self._mask(active, n)
         lam = torch.empty((4, n), dtype=torch.float32, device=self.device)
         w = torch.empty((4 if self.is_spectral else 3, n), dtype=torch.float32, device=self.device)

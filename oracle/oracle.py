@@ -260,6 +260,17 @@ class Oracle:
                                _ptr(lam), _ptr(w))
         return {"o": o.T.copy(), "d": d.T.copy(), "wavelengths": lam.T.copy(), "weight": w.T.copy()}
 
+    def sample_wavelengths(self, wi, sample):
+        """sample_wavelengths(si{wi}, sample) (sunsky.cpp:463-480) -> (lambda (n, 4), weight (n, k))."""
+        wi = np.asarray(wi, dtype=np.float32)
+        n = wi.shape[0]
+        s = _f(sample if sample is not None else np.zeros(n, np.float32))
+        lam = np.zeros((4, n), dtype=self.dtype)
+        w = np.zeros((4 if self.spectral else 3, n), dtype=self.dtype)
+        self._fn("sample_wavelengths")(self._h, _ptr(_f(wi[:, 0])), _ptr(_f(wi[:, 1])), _ptr(_f(wi[:, 2])),
+                                       _ptr(s), C.c_size_t(n), _ptr(lam), _ptr(w))
+        return lam.T.copy(), w.T.copy()
+
     def override_w_sky(self, w_sky):
         """Adopt the product's staged sampling weight so sampling parity isolates the kernels."""
         f = self._fn("override_w_sky")

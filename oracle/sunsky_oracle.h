@@ -97,6 +97,10 @@ void oracle_sun_coordinates(int year, int month, int day, float hour, float minu
                            const float *s2x, const float *s2y, const float *s3x,                 \
                            const float *s3y, size_t n, R *ox, R *oy, R *oz, R *dx, R *dy,        \
                            R *dz, R *lambda_out, R *weight);                                     \
+    /* sample_wavelengths(si, sample): spectral -> 4 shifted samples per ray; RGB -> eval */  \
+    void oracle_sample_wavelengths_##SFX(const oracle_##SFX *o, const float *wx, const float *wy,\
+                           const float *wz, const float *sample, size_t n, R *lambda_out,        \
+                           R *weight);                                                           \
     /* test hook: adopt another implementation's staged sky/sun sampling weight */             \
     void oracle_override_w_sky_##SFX(oracle_##SFX *o, double w_sky);                            \
     /* HW solar radiance (restates ArHosekSkyModel.c:686-784 on the packed tables) */          \

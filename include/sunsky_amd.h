@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define SUNSKY_AMD_ABI_VERSION 1
+#define SUNSKY_AMD_ABI_VERSION 2
 
 typedef enum sunsky_status {
     SUNSKY_OK = 0,
@@ -122,8 +122,10 @@ int sunsky_props_set_irregular_spectrum(sunsky_props *p, const char *name, const
                                         const float *values, int count);
 
 /* ------------------------------------------------------------ emitter
- * SunskyEmitter(const Properties&) -- sunsky.cpp:162-218.  Tables are staged on
- * the host and uploaded to the CURRENT HIP device.  dataset_path: NULL for the
+ * SunskyEmitter(const Properties&) -- sunsky.cpp:162-218.  The emitter lives on the
+ * CURRENT HIP device: its state (one SunskyKArgs block + tables) is allocated there,
+ * the radiance tables and the JIT sampling quadrature are staged there by kernels,
+ * and every later call on the emitter runs on that device whatever device is current.  dataset_path: NULL for the
  * bundled pack, a .pack file, or a directory holding the reference's
  * resources/sunsky/datasets/<table>.bin files (path_to_dataset, sunsky.h:124-141). */
 int sunsky_emitter_create(const sunsky_props *props, int variant, int semantics,
@@ -133,9 +135,22 @@ int sunsky_emitter_create(const sunsky_props *props, int variant, int semantics,
 int sunsky_emitter_create_host(const sunsky_props *props, int variant, int semantics,
                                const char *dataset_path, sunsky_emitter **out);
 void sunsky_emitter_destroy(sunsky_emitter *e);
-/* traverse() parameters, sunsky.cpp:220-240 (name, 1/3/11/16 floats) */
+/* traverse() parameters, sunsky.cpp:220-240 (name, 1/3/11/16 floats).  Values take
+ * effect at the next parameters_changed; a rejected update (e.g. turbidity 12) restores
+ * the last committed values. */
 int sunsky_emitter_set_param(sunsky_emitter *e, const char *name, const float *values, int count);
-/* parameters_changed(), sunsky.cpp:242-285 */
+/* Current value of a traverse() parameter: *count values written to out (<= capacity). */
+int sunsky_emitter_get_param(const sunsky_emitter *e, const char *name, float *out, int capacity,
+                             int *count);
+/* parameters_changed(), sunsky.cpp:242-285, stream-ordered: validation and the cheap
+ * geometry / TGMM staging run on the host; the radiance tables (sunsky.h:158-231,
+ * 404-419) and the JIT quadrature (estimate_sky_sun_ratio, sunsky.cpp:772-886) run as
+ * kernels on `stream`, writing the emitter's device state in place.  Batch calls on
+ * `stream` after this one see the new state; the call does not wait for the device.
+ * Work on other streams must be ordered by the caller (the reference's contract:
+ * parameters_changed is not concurrent with rendering).  Capturable in a hipGraph. */
+int sunsky_emitter_parameters_changed_async(sunsky_emitter *e, void *stream);
+/* Blocking form: _async on the default (null) stream, then waits for the staging. */
 int sunsky_emitter_parameters_changed(sunsky_emitter *e);
 /* set_scene(), sunsky.cpp:287-301: bounding sphere of the scene bbox */
 int sunsky_emitter_set_scene(sunsky_emitter *e, int bbox_valid, const float center[3], float radius);

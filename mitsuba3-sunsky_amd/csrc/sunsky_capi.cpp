@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -129,6 +130,7 @@ struct DeviceModule {
     hipFunction_t jvp_rgb = nullptr, jvp_spec = nullptr;   // eval_jvp (reference operation order)
     hipFunction_t vjp_rgb = nullptr, vjp_spec = nullptr, grad_reduce = nullptr;   // eval_vjp
     hipFunction_t latlong_tables = nullptr;                                     // bake_latlong
+    hipFunction_t stage_radiance = nullptr, quad_points = nullptr, quad_finish = nullptr;   // parameters_changed
     int cu_count = 256;
 };
 
@@ -158,6 +160,9 @@ DeviceModule* module_for_device(int dev) {
     hip_check(hipModuleGetFunction(&m->vjp_spec, m->module, "sunsky_eval_vjp_spec"), "sunsky_eval_vjp_spec");
     hip_check(hipModuleGetFunction(&m->grad_reduce, m->module, "sunsky_grad_reduce"), "sunsky_grad_reduce");
     hip_check(hipModuleGetFunction(&m->latlong_tables, m->module, "sunsky_latlong_tables"), "sunsky_latlong_tables");
+    hip_check(hipModuleGetFunction(&m->stage_radiance, m->module, "sunsky_stage_radiance"), "sunsky_stage_radiance");
+    hip_check(hipModuleGetFunction(&m->quad_points, m->module, "sunsky_stage_quad_points"), "sunsky_stage_quad_points");
+    hip_check(hipModuleGetFunction(&m->quad_finish, m->module, "sunsky_stage_quad_finish"), "sunsky_stage_quad_finish");
     hip_check(hipDeviceGetAttribute(&m->cu_count, hipDeviceAttributeMultiprocessorCount, dev),
               "hipDeviceGetAttribute");
     DeviceModule* raw = m.release();
@@ -232,6 +237,51 @@ LambdaSet make_lambda_set(const float* lam, int m) {
     return L;
 }
 
+// Makes the emitter's device current for the scope of an entry point: every
+// allocation, event and launch of an emitter happens on its own GPU whatever the
+// caller's current device is.
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int dev) {
+        if (dev < 0) return;
+        int cur = 0;
+        hip_check(hipGetDevice(&cur), "hipGetDevice");
+        if (cur != dev) {
+            hip_check(hipSetDevice(dev), "hipSetDevice");
+            prev = cur;
+        }
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
+struct StageArgs {   // mirrors the kernel-side struct (sunsky_kernels.hip)
+    SunskyKArgs* state;
+    float* sun_table;
+    const float* sky_params_ds;
+    const float* sky_rad_ds;
+    const float* sun_rad_ds;
+    RadianceStage rs;
+    float albedo[kNbWavelengths];
+    int nch, variant, sun_block;
+    float sky_scale;
+};
+
+constexpr int kQuadBlock = 256;   // sunsky_kernels.hip: one quadrature row per workgroup
+struct QuadArgs {    // mirrors the kernel-side struct (sunsky_kernels.hip)
+    SunskyKArgs* state;
+    const float* qx;
+    const float* qw;
+    float* rows;
+    int nq, nch;
+    float cie_y[kNbWavelengths];
+    float sky_scale, sun_scale;
+    int* status;
+};
+
 }  // namespace
 
 // ---------------------------------------------------------------- handles
@@ -241,45 +291,173 @@ struct sunsky_props {
 
 struct sunsky_emitter {
     std::unique_ptr<SunskyModel> model;
+    // Host mirror of the state: geometry, dispatch fields (variant, semantics, nch) and,
+    // once read back (sync_host), the device-staged radiance fields.
     SunskyKArgs kargs;
     DeviceModule* mod = nullptr;
     int device = 0;
     int precision = SUNSKY_PRECISION_FAST;
+    // ---- device state (one per emitter per GPU).  Every kernel reads the emitter
+    // through `d_state` (SunskyKArgs in device memory, s_load'ed by the kernels);
+    // parameters_changed rewrites it in place, ordered on the caller's stream.
+    SunskyKArgs* d_state = nullptr;
     float* d_sun_table = nullptr;
     float* d_sun_ld = nullptr;
+    float* d_datasets = nullptr;          // sky params | sky radiance | sun table | quadrature x | w
+    const float *d_sky_params_ds = nullptr, *d_sky_rad_ds = nullptr, *d_sun_rad_ds = nullptr;
+    const float *d_qx = nullptr, *d_qw = nullptr;
+    float* d_quad_part = nullptr;         // quadrature row sums [2][200][nch]
+    int* d_status = nullptr;              // device staging status (0 ok)
+    static constexpr int kRing = 4;       // pinned host images of the state for the async copy
+    SunskyKArgs* h_ring = nullptr;
+    hipEvent_t ring_ev[kRing] = {};
+    bool ring_used[kRing] = {};
+    int ring_i = 0;
+    mutable hipEvent_t stage_done = nullptr;   // recorded after the last device staging
     mutable float* d_jvp = nullptr;   // eval_jvp tangent tables (layout: sunsky_kernels.hip)
     mutable float* d_vjp = nullptr;   // eval_vjp basis-tangent tables
     mutable float* d_partials = nullptr;   // eval_vjp per-workgroup gradient partials
     mutable size_t partials_cap = 0;
+    mutable float* h_ad = nullptr;         // pinned staging of the AD tangent tables
     mutable float* d_bake = nullptr;       // bake_latlong angle tables
     mutable size_t bake_cap = 0;
     // AD tangent tables depend only on the emitter state: restaged when `rev` (bumped by
-    // every upload) or, for the JVP, the requested tangent changes.  `ad_done` is recorded
+    // every staging) or, for the JVP, the requested tangent changes.  `ad_done` is recorded
     // after each AD launch; the next AD call's stream waits on it, so a later call on
-    // another stream cannot overwrite d_jvp / d_partials under an in-flight kernel.
+    // another stream cannot overwrite d_jvp / d_partials under an in-flight kernel.  The
+    // bakes order their angle tables the same way (`bake_done`).
     uint64_t rev = 0;
     mutable uint64_t vjp_rev = ~0ull, jvp_rev = ~0ull;
     mutable std::vector<float> jvp_key;
-    mutable hipEvent_t ad_done = nullptr;
+    mutable hipEvent_t ad_done = nullptr, ad_copy_done = nullptr, bake_done = nullptr;
 
-    void upload() {
-        int cur = 0;
-        hip_check(hipGetDevice(&cur), "hipGetDevice");
-        if (cur != device) hip_check(hipSetDevice(device), "hipSetDevice");
-        const std::vector<float>& st = model->sun_table();
+    static constexpr size_t kAdFloats = 576 + kSunRgbTableSize;   // the larger (VJP) tangent block
+
+    // Allocations of a GPU emitter (once, at creation): state, tables, the raw datasets
+    // the staging kernels read, quadrature nodes, scratch, pinned ring, events.
+    void init_device() {
+        const bool spec = model->variant() == kSpectral;
+        hip_check(hipMalloc(&d_state, sizeof(SunskyKArgs)), "hipMalloc");
+        hip_check(hipMalloc(&d_sun_table, sizeof(float) * kSunRgbTableSize), "hipMalloc");
+        hip_check(hipMalloc(&d_sun_ld, sizeof(float) * kNbWavelengths * kNbSunLdParams), "hipMalloc");
+        const std::vector<float>& sp = model->sky_params_ds();
+        const std::vector<float>& sr = model->sky_rad_ds();
+        const std::vector<float>& su = model->sun_rad_ds();
+        std::vector<float> qx, qw;
+        SunskyModel::quadrature_nodes(&qx, &qw);
+        std::vector<float> all;
+        all.reserve(sp.size() + sr.size() + su.size() + qx.size() + qw.size());
+        all.insert(all.end(), sp.begin(), sp.end());
+        all.insert(all.end(), sr.begin(), sr.end());
+        all.insert(all.end(), su.begin(), su.end());
+        all.insert(all.end(), qx.begin(), qx.end());
+        all.insert(all.end(), qw.begin(), qw.end());
+        hip_check(hipMalloc(&d_datasets, sizeof(float) * all.size()), "hipMalloc");
+        hip_check(hipMemcpy(d_datasets, all.data(), sizeof(float) * all.size(), hipMemcpyHostToDevice), "hipMemcpy");
+        d_sky_params_ds = d_datasets;
+        d_sky_rad_ds = d_sky_params_ds + sp.size();
+        d_sun_rad_ds = d_sky_rad_ds + sr.size();
+        d_qx = d_sun_rad_ds + su.size();
+        d_qw = d_qx + qx.size();
         const std::vector<float>& ld = model->sun_ld();
-        if (!d_sun_table) hip_check(hipMalloc(&d_sun_table, sizeof(float) * kSunRgbTableSize), "hipMalloc");
-        if (!d_sun_ld) hip_check(hipMalloc(&d_sun_ld, sizeof(float) * kNbWavelengths * kNbSunLdParams), "hipMalloc");
-        // Tables may still be read by in-flight launches of a previous state.
-        hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-        hip_check(hipMemcpy(d_sun_table, st.data(), sizeof(float) * st.size(), hipMemcpyHostToDevice), "hipMemcpy");
-        hip_check(hipMemcpy(d_sun_ld, ld.data(), sizeof(float) * std::min<size_t>(ld.size(), kNbWavelengths * kNbSunLdParams),
-                            hipMemcpyHostToDevice), "hipMemcpy");
+        if (spec)
+            hip_check(hipMemcpy(d_sun_ld, ld.data(), sizeof(float) * std::min<size_t>(ld.size(), kNbWavelengths * kNbSunLdParams),
+                                hipMemcpyHostToDevice), "hipMemcpy");
+        const size_t nq = qx.size();
+        hip_check(hipMalloc(&d_quad_part, sizeof(float) * 2 * nq * model->nch()), "hipMalloc");
+        hip_check(hipMalloc(&d_status, sizeof(int)), "hipMalloc");
+        hip_check(hipMemset(d_status, 0, sizeof(int)), "hipMemset");
+        hip_check(hipHostMalloc((void**)&h_ring, sizeof(SunskyKArgs) * kRing, hipHostMallocDefault), "hipHostMalloc");
+        for (int i = 0; i < kRing; ++i)
+            hip_check(hipEventCreateWithFlags(&ring_ev[i], hipEventDisableTiming), "hipEventCreate");
+        hip_check(hipEventCreateWithFlags(&stage_done, hipEventDisableTiming), "hipEventCreate");
+    }
+
+    // parameters_changed on the device, ordered on `s`: the host-staged part of the
+    // state (geometry, TGMM, discrete distribution) by an async copy from a pinned image,
+    // then the staging kernels write the sky channels, the sun table and (JIT) the
+    // sampling weight and wavelength distribution.  Nothing here waits for the device,
+    // except for a pinned image still in flight kRing updates later.
+    void stage_async(hipStream_t s) {
         kargs = model->kargs();
-        ++rev;
         kargs.sun_table = d_sun_table;
         kargs.sun_ld = d_sun_ld;
-        if (cur != device) (void)hipSetDevice(cur);
+        const int slot = ring_i;
+        ring_i = (ring_i + 1) % kRing;
+        if (ring_used[slot]) hip_check(hipEventSynchronize(ring_ev[slot]), "hipEventSynchronize");
+        h_ring[slot] = kargs;
+        hip_check(hipMemcpyAsync(d_state, &h_ring[slot], sizeof(SunskyKArgs), hipMemcpyHostToDevice, s),
+                  "hipMemcpyAsync");
+        hip_check(hipEventRecord(ring_ev[slot], s), "hipEventRecord");
+        ring_used[slot] = true;
+        const bool spec = model->variant() == kSpectral;
+        StageArgs A;
+        std::memset(&A, 0, sizeof(A));
+        A.state = d_state;
+        A.sun_table = d_sun_table;
+        A.sky_params_ds = d_sky_params_ds;
+        A.sky_rad_ds = d_sky_rad_ds;
+        A.sun_rad_ds = d_sun_rad_ds;
+        A.rs = model->radiance_stage();
+        const std::vector<float>& alb = model->albedo();
+        for (int c = 0; c < model->nch(); ++c) A.albedo[c] = alb[c];
+        A.nch = model->nch();
+        A.variant = model->variant();
+        A.sun_block = spec ? kSunSpecTableSize : kSunRgbTableSize;
+        A.sky_scale = model->sky_scale();
+        void* sargs[] = {&A};
+        hip_check(hipModuleLaunchKernel(mod->stage_radiance, 1, 1, 1, 256, 1, 1, 0, s, sargs, nullptr),
+                  "hipModuleLaunchKernel(sunsky_stage_radiance)");
+        if (model->semantics() == kJit) {
+            QuadArgs Q;
+            std::memset(&Q, 0, sizeof(Q));
+            Q.state = d_state;
+            Q.qx = d_qx;
+            Q.qw = d_qw;
+            Q.rows = d_quad_part;
+            Q.nq = 200;
+            Q.nch = model->nch();
+            std::memcpy(Q.cie_y, model->cie_y(), sizeof(Q.cie_y));
+            Q.sky_scale = model->sky_scale();
+            Q.sun_scale = model->sun_scale();
+            Q.status = d_status;
+            void* qargs[] = {&Q};
+            static_assert(200 <= kQuadBlock, "one quadrature row per workgroup");
+            hip_check(hipModuleLaunchKernel(mod->quad_points, (unsigned)Q.nq, 1, 1, kQuadBlock, 1, 1, 0, s, qargs, nullptr),
+                      "hipModuleLaunchKernel(sunsky_stage_quad_points)");
+            hip_check(hipModuleLaunchKernel(mod->quad_finish, 1, 1, 1, 256, 1, 1, 0, s, qargs, nullptr),
+                      "hipModuleLaunchKernel(sunsky_stage_quad_finish)");
+        }
+        hip_check(hipEventRecord(stage_done, s), "hipEventRecord");
+        ++rev;
+    }
+
+    // Bring the device-staged fields back into the host model (get_info / get_table /
+    // to_string): waits for the last staging only.
+    void sync_host() const {
+        if (!model->radiance_stale() || !d_state) return;
+        DeviceScope g(device);
+        hip_check(hipEventSynchronize(stage_done), "hipEventSynchronize");
+        SunskyKArgs dk;
+        hip_check(hipMemcpy(&dk, d_state, sizeof(dk), hipMemcpyDeviceToHost), "hipMemcpy");
+        std::vector<float> st(kSunRgbTableSize);
+        hip_check(hipMemcpy(st.data(), d_sun_table, sizeof(float) * st.size(), hipMemcpyDeviceToHost), "hipMemcpy");
+        int status = 0;
+        hip_check(hipMemcpy(&status, d_status, sizeof(int), hipMemcpyDeviceToHost), "hipMemcpy");
+        model->adopt_device_stage(dk, st.data());
+        auto* self = const_cast<sunsky_emitter*>(this);
+        const SunskyKArgs& hk = model->kargs();
+        std::memcpy(self->kargs.sky, hk.sky, sizeof(hk.sky));
+        std::memcpy(self->kargs.fsky, hk.fsky, sizeof(hk.fsky));
+        self->kargs.w_sky = hk.w_sky;
+        self->kargs.spec_size = hk.spec_size;
+        std::memcpy(self->kargs.spec_pdf, hk.spec_pdf, sizeof(hk.spec_pdf));
+        std::memcpy(self->kargs.spec_cdf, hk.spec_cdf, sizeof(hk.spec_cdf));
+        self->kargs.spec_integral = hk.spec_integral;
+        self->kargs.spec_norm = hk.spec_norm;
+        self->kargs.spec_interval = hk.spec_interval;
+        self->kargs.spec_inv_interval = hk.spec_inv_interval;
+        if (status) throw std::runtime_error("ContinuousDistribution: entries must be non-negative!");
     }
 
     hipFunction_t fn(KernelId k) const {
@@ -293,13 +471,21 @@ struct sunsky_emitter {
     }
 
     ~sunsky_emitter() {
-        if (d_sun_table) (void)hipFree(d_sun_table);
-        if (d_sun_ld) (void)hipFree(d_sun_ld);
-        if (d_jvp) (void)hipFree(d_jvp);
-        if (d_vjp) (void)hipFree(d_vjp);
-        if (d_partials) (void)hipFree(d_partials);
-        if (d_bake) (void)hipFree(d_bake);
-        if (ad_done) (void)hipEventDestroy(ad_done);
+        if (device < 0) return;
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && cur != device) (void)hipSetDevice(device);
+        // a destroyed emitter may still be read by launches in flight on any stream
+        (void)hipDeviceSynchronize();
+        for (void* p : {(void*)d_state, (void*)d_sun_table, (void*)d_sun_ld, (void*)d_datasets, (void*)d_quad_part,
+                        (void*)d_status, (void*)d_jvp, (void*)d_vjp, (void*)d_partials, (void*)d_bake})
+            if (p) (void)hipFree(p);
+        if (h_ring) (void)hipHostFree(h_ring);
+        if (h_ad) (void)hipHostFree(h_ad);
+        for (hipEvent_t ev : ring_ev)
+            if (ev) (void)hipEventDestroy(ev);
+        for (hipEvent_t ev : {stage_done, ad_done, ad_copy_done, bake_done})
+            if (ev) (void)hipEventDestroy(ev);
+        if (cur >= 0 && cur != device) (void)hipSetDevice(cur);
     }
 
     // Order this AD call after the previous one (any stream), then mark its end.
@@ -308,6 +494,19 @@ struct sunsky_emitter {
         else hip_check(hipStreamWaitEvent(st, ad_done, 0), "hipStreamWaitEvent");
     }
     void ad_end(hipStream_t st) const { hip_check(hipEventRecord(ad_done, st), "hipEventRecord"); }
+    // Stream-ordered upload of host-computed AD tangent tables through a pinned buffer:
+    // the host rewrites the pinned buffer only once the previous copy out of it is done.
+    void ad_upload(float* dst, const std::vector<float>& buf, hipStream_t st) const {
+        if (!h_ad) {
+            hip_check(hipHostMalloc((void**)&h_ad, sizeof(float) * kAdFloats, hipHostMallocDefault), "hipHostMalloc");
+            hip_check(hipEventCreateWithFlags(&ad_copy_done, hipEventDisableTiming), "hipEventCreate");
+        } else {
+            hip_check(hipEventSynchronize(ad_copy_done), "hipEventSynchronize");
+        }
+        std::memcpy(h_ad, buf.data(), sizeof(float) * buf.size());
+        hip_check(hipMemcpyAsync(dst, h_ad, sizeof(float) * buf.size(), hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+        hip_check(hipEventRecord(ad_copy_done, st), "hipEventRecord");
+    }
 };
 
 extern "C" {
@@ -359,12 +558,16 @@ int sunsky_emitter_create(const sunsky_props* props, int variant, int semantics,
     return guarded([&] {
         std::unique_ptr<sunsky_emitter> e(new sunsky_emitter());
         std::string ds = dataset_path && *dataset_path ? std::string(dataset_path) : default_pack_path();
-        e->model.reset(new SunskyModel(props->props, variant, semantics, ds));
+        // radiance tables + quadrature are staged on the device (stage_async)
+        e->model.reset(new SunskyModel(props->props, variant, semantics, ds, /*radiance_on_host=*/false));
         hip_check(hipGetDevice(&e->device), "hipGetDevice");
         e->mod = module_for_device(e->device);
         if (const char* env = std::getenv("SUNSKY_AMD_PRECISION"))
             e->precision = std::strcmp(env, "reference") == 0 ? SUNSKY_PRECISION_REFERENCE : SUNSKY_PRECISION_FAST;
-        e->upload();
+        e->init_device();
+        e->stage_async(nullptr);
+        hip_check(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+        e->sync_host();
         for (const std::string& w : e->model->warnings) std::fprintf(stderr, "WARN sunsky: %s\n", w.c_str());
         *out = e.release();
     });
@@ -391,13 +594,34 @@ int sunsky_emitter_set_param(sunsky_emitter* e, const char* name, const float* v
     return guarded([&] { e->model->set_param(name, v, count); });
 }
 
-int sunsky_emitter_parameters_changed(sunsky_emitter* e) {
+int sunsky_emitter_parameters_changed_async(sunsky_emitter* e, void* stream) {
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     return guarded([&] {
-        e->model->parameters_changed();   // keeps the scene bounding sphere
-        if (e->device >= 0) e->upload();
-        else e->kargs = e->model->kargs();
+        const bool gpu = e->device >= 0;
+        e->model->parameters_changed(/*radiance_on_host=*/!gpu);   // keeps the scene bounding sphere
+        if (gpu) {
+            DeviceScope g(e->device);
+            e->stage_async((hipStream_t)stream);
+        } else {
+            e->kargs = e->model->kargs();
+        }
     });
+}
+
+int sunsky_emitter_parameters_changed(sunsky_emitter* e) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    int rc = sunsky_emitter_parameters_changed_async(e, nullptr);
+    if (rc != SUNSKY_OK || e->device < 0) return rc;
+    return guarded([&] {
+        DeviceScope g(e->device);
+        hip_check(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+        e->sync_host();
+    });
+}
+
+int sunsky_emitter_get_param(const sunsky_emitter* e, const char* name, float* out, int cap, int* count) {
+    if (!e || !name || !count) return fail(SUNSKY_ERROR_INVALID_VALUE, "null argument");
+    return guarded([&] { *count = e->model->get_param(name, out, out ? cap : 0); });
 }
 
 int sunsky_emitter_set_scene(sunsky_emitter* e, int bbox_valid, const float center[3], float radius) {
@@ -408,6 +632,14 @@ int sunsky_emitter_set_scene(sunsky_emitter* e, int bbox_valid, const float cent
         const SunskyKArgs& k = e->model->kargs();
         std::memcpy(e->kargs.bs_center, k.bs_center, sizeof(k.bs_center));
         e->kargs.bs_radius = k.bs_radius;
+        if (e->device >= 0) {   // the 4 bounding-sphere floats of the device state, in place
+            DeviceScope g(e->device);
+            static_assert(offsetof(SunskyKArgs, bs_radius) == offsetof(SunskyKArgs, bs_center) + 3 * sizeof(float),
+                          "bounding sphere layout");
+            float bs[4] = {k.bs_center[0], k.bs_center[1], k.bs_center[2], k.bs_radius};
+            hip_check(hipMemcpy((char*)e->d_state + offsetof(SunskyKArgs, bs_center), bs, sizeof(bs),
+                                hipMemcpyHostToDevice), "hipMemcpy");
+        }
     });
 }
 
@@ -420,6 +652,8 @@ int sunsky_emitter_set_precision(sunsky_emitter* e, int precision) {
 
 int sunsky_emitter_get_info(const sunsky_emitter* e, sunsky_info* out) {
     if (!e || !out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null argument");
+    int rc = guarded([&] { e->sync_host(); });
+    if (rc != SUNSKY_OK) return rc;
     const SunskyKArgs& k = e->kargs;
     std::memset(out, 0, sizeof(*out));
     out->variant = e->model->variant();
@@ -447,6 +681,8 @@ int sunsky_emitter_get_info(const sunsky_emitter* e, sunsky_info* out) {
 
 int sunsky_emitter_get_table(const sunsky_emitter* e, int id, float* out, size_t cap, size_t* count) {
     if (!e || !count) return fail(SUNSKY_ERROR_INVALID_VALUE, "null argument");
+    int rc = guarded([&] { e->sync_host(); });
+    if (rc != SUNSKY_OK) return rc;
     std::vector<float> v;
     const SunskyKArgs& k = e->kargs;
     switch (id) {
@@ -468,6 +704,8 @@ int sunsky_emitter_get_table(const sunsky_emitter* e, int id, float* out, size_t
 
 int sunsky_emitter_to_string(const sunsky_emitter* e, char* buf, size_t cap) {
     if (!e || !buf || !cap) return fail(SUNSKY_ERROR_INVALID_VALUE, "null argument");
+    int rc = guarded([&] { e->sync_host(); });
+    if (rc != SUNSKY_OK) return rc;
     std::string s = e->model->to_string();
     std::snprintf(buf, cap, "%s", s.c_str());
     return SUNSKY_OK;
@@ -493,7 +731,8 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
     if (spec && nlam > 1 && lstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "wl_stride < n");
     return guarded([&] {
         hipStream_t s = (hipStream_t)stream;
-        SunskyKArgs K = e->kargs;
+        DeviceScope dev_scope(e->device);
+        const SunskyKArgs* K = e->d_state;
         if (!spec) {
             bool vec = n >= 4 && aligned16(w.x) && aligned16(w.y) && aligned16(w.z) && aligned16(out) &&
                        (ostride % 4) == 0 && (!active || ((uintptr_t)active & 3u) == 0);
@@ -560,7 +799,8 @@ int sunsky_eval_spectral_broadcast(const sunsky_emitter* e, sunsky_vec3_in w, co
     for (int k = 0; nodes && k < m; ++k) nodes = L.lo[k] == k && L.f[k] == 0.f;
     return guarded([&] {
         hipStream_t s = (hipStream_t)stream;
-        SunskyKArgs K = e->kargs;
+        DeviceScope dev_scope(e->device);
+        const SunskyKArgs* K = e->d_state;
         float sign = -1.f;
         bool vec = n >= 4 && aligned16(w.x) && aligned16(w.y) && aligned16(w.z) && aligned16(out) &&
                    (ostride % 4) == 0 && (!active || ((uintptr_t)active & 3u) == 0);
@@ -598,7 +838,8 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
     if ((ds_p.x != nullptr) != (ds_p.y != nullptr) || (ds_p.x != nullptr) != (ds_p.z != nullptr))
         return fail(SUNSKY_ERROR_INVALID_VALUE, "ds_p must be all-NULL or all-set");
     return guarded([&] {
-        SunskyKArgs K = e->kargs;
+        DeviceScope dev_scope(e->device);
+        const SunskyKArgs* K = e->d_state;
         int nl = spec ? nlam : 0;
         void* args[] = {&K, &ux, &uy, (void*)&it_p.x, (void*)&it_p.y, (void*)&it_p.z, &lam, &lstride, &nl, &active, &n,
                         &ds_d.x, &ds_d.y, &ds_d.z, &ds_pdf, &ds_dist, &ds_p.x, &ds_p.y, &ds_p.z, &weight, &wstride};
@@ -617,7 +858,8 @@ int sunsky_pdf_direction(const sunsky_emitter* e, sunsky_vec3_in d, const uint8_
     if (n == 0) return SUNSKY_OK;
     if (!d.x || !d.y || !d.z || !pdf) return fail(SUNSKY_ERROR_INVALID_VALUE, "null direction / output pointer");
     return guarded([&] {
-        SunskyKArgs K = e->kargs;
+        DeviceScope dev_scope(e->device);
+        const SunskyKArgs* K = e->d_state;
         hipStream_t s = (hipStream_t)stream;
         bool vec = n >= 4 && aligned16(d.x) && aligned16(d.y) && aligned16(d.z) && aligned16(pdf) &&
                    (!active || ((uintptr_t)active & 3u) == 0);
@@ -647,7 +889,8 @@ int sunsky_sample_ray(const sunsky_emitter* e, const float* wls, const float* s2
     if (e->kargs.variant == kSpectral && !wls) return fail(SUNSKY_ERROR_INVALID_VALUE, "null wavelength sample");
     if (lstride < n || wstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "stride < n");
     return guarded([&] {
-        SunskyKArgs K = e->kargs;
+        DeviceScope dev_scope(e->device);
+        const SunskyKArgs* K = e->d_state;
         void* args[] = {&K, &wls, &s2x, &s2y, &s3x, &s3y, &active, &n, &o.x, &o.y, &o.z,
                         &d.x, &d.y, &d.z, &lam, &lstride, &weight, &wstride};
         const KernelId k = e->kargs.variant == kSpectral ? K_SAMPLE_RAY_SPEC : K_SAMPLE_RAY_RGB;
@@ -663,7 +906,8 @@ int sunsky_sample_wavelengths(const sunsky_emitter* e, sunsky_vec3_in w, const f
     if (e->kargs.variant == kSpectral && !sample) return fail(SUNSKY_ERROR_INVALID_VALUE, "null sample");
     if (lstride < n || wstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "stride < n");
     return guarded([&] {
-        SunskyKArgs K = e->kargs;
+        DeviceScope dev_scope(e->device);
+        const SunskyKArgs* K = e->d_state;
         void* args[] = {&K, (void*)&w.x, (void*)&w.y, (void*)&w.z, &sample, &active, &n, &lam, &lstride, &weight, &wstride};
         const KernelId k = e->kargs.variant == kSpectral ? K_SAMPLE_WAVELENGTHS_SPEC : K_SAMPLE_WAVELENGTHS_RGB;
         launch(e->fn(k), grid_for(e->mod, k, n), (hipStream_t)stream, args);
@@ -692,20 +936,19 @@ int sunsky_eval_jvp(const sunsky_emitter* e, int param, const float* tangent, in
         if (n == 0) return;
         if (!e->mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
         hipStream_t st = (hipStream_t)stream;
+        DeviceScope dev_scope(e->device);
+        e->ad_begin(st);   // ordered after the previous AD call (which may read d_jvp), any stream
         if (stage) {
             std::vector<float> buf(128 + kSunRgbTableSize, 0.f);
             std::memcpy(buf.data(), tan.dsky.data(), sizeof(float) * tan.dsky.size());
             std::memcpy(buf.data() + kNbWavelengths * 10, tan.dsun_local, 3 * sizeof(float));
             std::memcpy(buf.data() + 128, tan.dsun.data(), sizeof(float) * tan.dsun.size());
             if (!e->d_jvp) hip_check(hipMalloc(&e->d_jvp, sizeof(float) * buf.size()), "hipMalloc");
-            // a previous eval_jvp of this emitter may still read the buffer
-            hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
-            hip_check(hipMemcpy(e->d_jvp, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice), "hipMemcpy");
+            e->ad_upload(e->d_jvp, buf, st);
             e->jvp_key = key;
             e->jvp_rev = e->rev;
         }
-        e->ad_begin(st);
-        SunskyKArgs K = e->kargs;
+        const SunskyKArgs* K = e->d_state;
         const float* jvp = e->d_jvp;
         const float *x = wi.x, *y = wi.y, *z = wi.z;
         float sign = -1.f;
@@ -745,10 +988,13 @@ int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam
         const unsigned grid = (unsigned)std::max<size_t>(
             1, std::min<size_t>((n + kBlock - 1) / kBlock, (size_t)e->mod->cu_count * 6));
         hipStream_t st = (hipStream_t)stream;
+        DeviceScope dev_scope(e->device);
         const bool stage = !e->d_vjp || e->vjp_rev != e->rev;
-        if (stage || e->partials_cap < grid)
-            hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");   // in-flight readers of the old buffers
+        const bool had_ad = e->ad_done != nullptr;
+        e->ad_begin(st);   // ordered after the previous AD call (d_vjp / d_partials readers), any stream
         if (e->partials_cap < grid) {
+            // the host frees the old partials only once the previous AD call is done with them
+            if (had_ad) hip_check(hipEventSynchronize(e->ad_done), "hipEventSynchronize");
             if (e->d_partials) hip_check(hipFree(e->d_partials), "hipFree");
             e->d_partials = nullptr;
             hip_check(hipMalloc(&e->d_partials, sizeof(float) * 16 * grid), "hipMalloc");
@@ -772,11 +1018,10 @@ int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam
                     std::memcpy(buf.data() + 5 * blk + 3 * k, tS.dsun_local, 3 * sizeof(float));
                 }
             if (!e->d_vjp) hip_check(hipMalloc(&e->d_vjp, sizeof(float) * buf.size()), "hipMalloc");
-            hip_check(hipMemcpy(e->d_vjp, buf.data(), sizeof(float) * buf.size(), hipMemcpyHostToDevice), "hipMemcpy");
+            e->ad_upload(e->d_vjp, buf, st);
             e->vjp_rev = e->rev;
         }
-        e->ad_begin(st);
-        SunskyKArgs K = e->kargs;
+        const SunskyKArgs* K = e->d_state;
         const float* vjp = e->d_vjp;
         float* partials = e->d_partials;
         const float *x = wi.x, *y = wi.y, *z = wi.z;
@@ -814,12 +1059,18 @@ int sunsky_bake_latlong(const sunsky_emitter* e, int width, int height, float th
                  phi0, width > 1 ? (phi1 - phi0) / (float)(width - 1) : 0.f, nullptr};
     return guarded([&] {
         if (!e->mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
-        SunskyKArgs K = e->kargs;
+        DeviceScope dev_scope(e->device);
+        const SunskyKArgs* K = e->d_state;
         hipStream_t s = (hipStream_t)stream;
         const size_t need = 2 * (size_t)width + 2 * (size_t)height;
+        // the angle tables are per emitter: order this bake after the previous one (any
+        // stream), so a bake on another stream cannot rewrite them under a running kernel
+        const bool had_bake = e->bake_done != nullptr;
+        if (!had_bake) hip_check(hipEventCreateWithFlags(&e->bake_done, hipEventDisableTiming), "hipEventCreate");
+        else hip_check(hipStreamWaitEvent(s, e->bake_done, 0), "hipStreamWaitEvent");
         if (e->bake_cap < need) {
-            // the tables of a previous bake may still be in use
-            hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+            // the host frees the old tables only once the previous bake is done with them
+            if (had_bake) hip_check(hipEventSynchronize(e->bake_done), "hipEventSynchronize");
             if (e->d_bake) hip_check(hipFree(e->d_bake), "hipFree");
             e->d_bake = nullptr;
             hip_check(hipMalloc(&e->d_bake, sizeof(float) * need), "hipMalloc");
@@ -840,6 +1091,7 @@ int sunsky_bake_latlong(const sunsky_emitter* e, int width, int height, float th
             void* args[] = {&K, &G, &L, &out, &ostride};
             launch(e->fn(K_BAKE_SPEC), grid_for(e->mod, K_BAKE_SPEC, n), s, args);
         }
+        hip_check(hipEventRecord(e->bake_done, s), "hipEventRecord");
     });
 }
 
@@ -858,7 +1110,8 @@ int sunsky_direct_diffuse(const sunsky_emitter* e, sunsky_vec3_in nrm, const flo
     if (ostride < n || (spec && lstride < n)) return fail(SUNSKY_ERROR_INVALID_VALUE, "stride < n");
     return guarded([&] {
         if (!e->mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
-        SunskyKArgs K = e->kargs;
+        DeviceScope dev_scope(e->device);
+        const SunskyKArgs* K = e->d_state;
         int nl = spec ? nlam : 0;
         void* args[] = {&K, (void*)&nrm.x, (void*)&nrm.y, (void*)&nrm.z, &rho, &lam, &lstride, &nl, &seed, &spp, &n,
                         &out, &ostride};

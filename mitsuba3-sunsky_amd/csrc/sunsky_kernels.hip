@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include "sunsky_math.h"
+#include "sunsky_staging.h"
 #include "sunsky_types.h"
 
 using namespace sunsky;
@@ -2055,10 +2056,10 @@ __device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const f
 // ======================================================================
 #define SS_EVAL_RGB(NAME, VEC, FAST, NEG)                                                                          \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_RGB_ATTR void NAME(                                               \
-        SunskyKArgs K, const float* wx, const float* wy, const float* wz, const uint8_t* active, size_t n,     \
+        const SunskyKArgs* __restrict__ Kp, const float* wx, const float* wy, const float* wz, const uint8_t* active, size_t n,     \
         float* out, size_t ostride, float sign) {                                                              \
         (void)sign;                                                                                            \
-        eval_rgb_body<VEC, FAST, NEG>(K, wx, wy, wz, active, n, out, ostride);                                 \
+        eval_rgb_body<VEC, FAST, NEG>(*Kp, wx, wy, wz, active, n, out, ostride);                                 \
     }
 // eval(si): wo = -wi (NEG); eval_direction(ds): wo = ds.d (the _dir kernels)
 SS_EVAL_RGB(sunsky_eval_rgb_v4_fast, 4, true, true)
@@ -2072,10 +2073,10 @@ SS_EVAL_RGB(sunsky_eval_rgb_v1_dir_ref, 1, false, false)
 
 #define SS_EVAL_SPEC_BCAST(NAME, VEC, FAST)                                                                   \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_NODES_ATTR void NAME(                                               \
-        SunskyKArgs K, LambdaSet L, const float* wx, const float* wy, const float* wz, const uint8_t* active,  \
+        const SunskyKArgs* __restrict__ Kp, LambdaSet L, const float* wx, const float* wy, const float* wz, const uint8_t* active,  \
         size_t n, float* out, size_t ostride, float sign) {                                                    \
         (void)sign;   /* always eval(si): wo = -wi */                                                         \
-        eval_spec_bcast_body<VEC, FAST, true>(K, L, wx, wy, wz, active, n, out, ostride);                      \
+        eval_spec_bcast_body<VEC, FAST, true>(*Kp, L, wx, wy, wz, active, n, out, ostride);                      \
     }
 SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v4_fast, 4, true)
 SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v1_fast, 1, true)
@@ -2084,21 +2085,21 @@ SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v1_ref, 1, false)
 
 #define SS_EVAL_SPEC_NODES(NAME, VEC, FAST)                                                                   \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_NODES_ATTR void NAME(                                               \
-        SunskyKArgs K, LambdaSet L, const float* wx, const float* wy, const float* wz, const uint8_t* active,  \
+        const SunskyKArgs* __restrict__ Kp, LambdaSet L, const float* wx, const float* wy, const float* wz, const uint8_t* active,  \
         size_t n, float* out, size_t ostride, float sign) {                                                    \
         (void)L;                                                                                               \
         (void)sign;                                                                                            \
-        eval_spec_nodes_body<VEC, FAST, true>(K, wx, wy, wz, active, n, out, ostride);                         \
+        eval_spec_nodes_body<VEC, FAST, true>(*Kp, wx, wy, wz, active, n, out, ostride);                         \
     }
 SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v4_fast, 4, true)
 SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v4_ref, 4, false)
 
 #define SS_EVAL_SPEC_RAYS(NAME, VEC, FAST, NEG)                                                                    \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
-        SunskyKArgs K, const float* wx, const float* wy, const float* wz, const float* lam, size_t lstride,    \
+        const SunskyKArgs* __restrict__ Kp, const float* wx, const float* wy, const float* wz, const float* lam, size_t lstride,    \
         int nlam, const uint8_t* active, size_t n, float* out, size_t ostride, float sign) {                   \
         (void)sign;                                                                                            \
-        eval_spec_rays_body<VEC, FAST, NEG>(K, wx, wy, wz, lam, lstride, nlam, active, n, out, ostride);       \
+        eval_spec_rays_body<VEC, FAST, NEG>(*Kp, wx, wy, wz, lam, lstride, nlam, active, n, out, ostride);       \
     }
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_fast, 4, true, true)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_fast, 1, true, true)
@@ -2111,10 +2112,10 @@ SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_dir_ref, 1, false, false)
 
 #define SS_SAMPLE_DIRECTION(NAME, FAST, SPEC, LEAN)                                                           \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
-        SunskyKArgs K, const float* ux, const float* uy, const float* px, const float* py, const float* pz,   \
+        const SunskyKArgs* __restrict__ Kp, const float* ux, const float* uy, const float* px, const float* py, const float* pz,   \
         const float* lam, size_t lstride, int nlam, const uint8_t* active, size_t n, float* dx, float* dy,     \
         float* dz, float* pdf, float* dist, float* opx, float* opy, float* opz, float* weight, size_t wstride) { \
-        sample_direction_body<FAST, SPEC, LEAN>(K, ux, uy, px, py, pz, lam, lstride, nlam, active, n, dx, dy,  \
+        sample_direction_body<FAST, SPEC, LEAN>(*Kp, ux, uy, px, py, pz, lam, lstride, nlam, active, n, dx, dy,  \
                                                 dz, pdf, dist, opx, opy, opz, weight, wstride);                \
     }
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_fast, true, false, false)
@@ -2128,9 +2129,9 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_ref, false, true, true)
 
 #define SS_PDF_DIRECTION(NAME, VEC, FAST)                                                                     \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
-        SunskyKArgs K, const float* dx, const float* dy, const float* dz, const uint8_t* active, size_t n,     \
+        const SunskyKArgs* __restrict__ Kp, const float* dx, const float* dy, const float* dz, const uint8_t* active, size_t n,     \
         float* pdf) {                                                                                          \
-        pdf_direction_body<VEC, FAST>(K, dx, dy, dz, active, n, pdf);                                          \
+        pdf_direction_body<VEC, FAST>(*Kp, dx, dy, dz, active, n, pdf);                                          \
     }
 SS_PDF_DIRECTION(sunsky_pdf_direction_v4_fast, 4, true)
 SS_PDF_DIRECTION(sunsky_pdf_direction_v1_fast, 1, true)
@@ -2139,9 +2140,9 @@ SS_PDF_DIRECTION(sunsky_pdf_direction_v1_ref, 1, false)
 
 #define SS_SAMPLE_WAVELENGTHS(NAME, FAST, SPEC)                                                               \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
-        SunskyKArgs K, const float* wx, const float* wy, const float* wz, const float* sample,                 \
+        const SunskyKArgs* __restrict__ Kp, const float* wx, const float* wy, const float* wz, const float* sample,                 \
         const uint8_t* active, size_t n, float* lam, size_t lstride, float* weight, size_t wstride) {          \
-        sample_wavelengths_body<FAST, SPEC>(K, wx, wy, wz, sample, active, n, lam, lstride, weight, wstride);  \
+        sample_wavelengths_body<FAST, SPEC>(*Kp, wx, wy, wz, sample, active, n, lam, lstride, weight, wstride);  \
     }
 SS_SAMPLE_WAVELENGTHS(sunsky_sample_wavelengths_rgb_fast, true, false)
 SS_SAMPLE_WAVELENGTHS(sunsky_sample_wavelengths_rgb_ref, false, false)
@@ -2150,10 +2151,10 @@ SS_SAMPLE_WAVELENGTHS(sunsky_sample_wavelengths_spec_ref, false, true)
 
 #define SS_SAMPLE_RAY(NAME, FAST, SPEC)                                                                       \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
-        SunskyKArgs K, const float* wls, const float* s2x, const float* s2y, const float* s3x,                 \
+        const SunskyKArgs* __restrict__ Kp, const float* wls, const float* s2x, const float* s2y, const float* s3x,                 \
         const float* s3y, const uint8_t* active, size_t n, float* ox, float* oy, float* oz, float* dx,         \
         float* dy, float* dz, float* lam, size_t lstride, float* weight, size_t wstride) {                     \
-        sample_ray_body<FAST, SPEC>(K, wls, s2x, s2y, s3x, s3y, active, n, ox, oy, oz, dx, dy, dz, lam,        \
+        sample_ray_body<FAST, SPEC>(*Kp, wls, s2x, s2y, s3x, s3y, active, n, ox, oy, oz, dx, dy, dz, lam,        \
                                     lstride, weight, wstride);                                                 \
     }
 SS_SAMPLE_RAY(sunsky_sample_ray_rgb_fast, true, false)
@@ -2163,9 +2164,9 @@ SS_SAMPLE_RAY(sunsky_sample_ray_spec_ref, false, true)
 
 #define SS_DIRECT_DIFFUSE(NAME, FAST, SPEC)                                                                   \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                              \
-        SunskyKArgs K, const float* nx, const float* ny, const float* nz, const float* rho, const float* lam, \
+        const SunskyKArgs* __restrict__ Kp, const float* nx, const float* ny, const float* nz, const float* rho, const float* lam, \
         size_t lstride, int nlam, uint32_t seed, uint32_t spp, size_t n, float* out, size_t ostride) {          \
-        direct_diffuse_body<FAST, SPEC>(K, nx, ny, nz, rho, lam, lstride, nlam, seed, spp, n, out, ostride);   \
+        direct_diffuse_body<FAST, SPEC>(*Kp, nx, ny, nz, rho, lam, lstride, nlam, seed, spp, n, out, ostride);   \
     }
 SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_rgb_fast, true, false)
 SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_rgb_ref, false, false)
@@ -2173,26 +2174,26 @@ SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_spec_fast, true, true)
 SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_spec_ref, false, true)
 
 extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_jvp_rgb(
-    SunskyKArgs K, const float* jvp, const float* wx, const float* wy, const float* wz, const uint8_t* active,
+    const SunskyKArgs* __restrict__ Kp, const float* jvp, const float* wx, const float* wy, const float* wz, const uint8_t* active,
     size_t n, float* out, float* dout, size_t ostride, float sign) {
-    eval_jvp_rgb_body(K, jvp, wx, wy, wz, active, n, out, dout, ostride, sign);
+    eval_jvp_rgb_body(*Kp, jvp, wx, wy, wz, active, n, out, dout, ostride, sign);
 }
 extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_jvp_spec(
-    SunskyKArgs K, const float* jvp, const float* wx, const float* wy, const float* wz, const float* lam,
+    const SunskyKArgs* __restrict__ Kp, const float* jvp, const float* wx, const float* wy, const float* wz, const float* lam,
     size_t lstride, int nlam, const uint8_t* active, size_t n, float* out, float* dout, size_t ostride, float sign) {
-    eval_jvp_spec_body(K, jvp, wx, wy, wz, lam, lstride, nlam, active, n, out, dout, ostride, sign);
+    eval_jvp_spec_body(*Kp, jvp, wx, wy, wz, lam, lstride, nlam, active, n, out, dout, ostride, sign);
 }
 
 extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_vjp_rgb(
-    SunskyKArgs K, const float* vjp, const float* wx, const float* wy, const float* wz, const uint8_t* active,
+    const SunskyKArgs* __restrict__ Kp, const float* vjp, const float* wx, const float* wy, const float* wz, const uint8_t* active,
     size_t n, const float* dout, size_t ostride, float sign, float* partials) {
-    eval_vjp_rgb_body(K, vjp, wx, wy, wz, active, n, dout, ostride, sign, partials);
+    eval_vjp_rgb_body(*Kp, vjp, wx, wy, wz, active, n, dout, ostride, sign, partials);
 }
 extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_vjp_spec(
-    SunskyKArgs K, const float* vjp, const float* wx, const float* wy, const float* wz, const float* lam,
+    const SunskyKArgs* __restrict__ Kp, const float* vjp, const float* wx, const float* wy, const float* wz, const float* lam,
     size_t lstride, int nlam, const uint8_t* active, size_t n, const float* dout, size_t ostride, float sign,
     float* partials) {
-    eval_vjp_spec_body(K, vjp, wx, wy, wz, lam, lstride, nlam, active, n, dout, ostride, sign, partials);
+    eval_vjp_spec_body(*Kp, vjp, wx, wy, wz, lam, lstride, nlam, active, n, dout, ostride, sign, partials);
 }
 // grad[p] += sum over blocks (in block order) of partials[block][p]; one wave.
 // grad[p] += sum over blocks of partials[b][p], one 256-thread workgroup: thread (s, p)
@@ -2216,13 +2217,127 @@ extern "C" __global__ __launch_bounds__(256) void sunsky_grad_reduce(const float
 }
 
 #define SS_BAKE(NAME_RGB, NAME_SPEC, FAST)                                                                    \
-    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME_RGB(SunskyKArgs K, LatLong G, float* out,      \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME_RGB(const SunskyKArgs* __restrict__ Kp, LatLong G, float* out,      \
                                                                     size_t ostride) {                          \
-        bake_rgb_body<FAST>(K, G, out, ostride);                                                               \
+        bake_rgb_body<FAST>(*Kp, G, out, ostride);                                                               \
     }                                                                                                          \
-    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME_SPEC(SunskyKArgs K, LatLong G, LambdaSet L,    \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME_SPEC(const SunskyKArgs* __restrict__ Kp, LatLong G, LambdaSet L,    \
                                                                      float* out, size_t ostride) {             \
-        bake_spec_body<FAST>(K, G, L, out, ostride);                                                           \
+        bake_spec_body<FAST>(*Kp, G, L, out, ostride);                                                           \
     }
 SS_BAKE(sunsky_bake_latlong_rgb_fast, sunsky_bake_latlong_spec_fast, true)
 SS_BAKE(sunsky_bake_latlong_rgb_ref, sunsky_bake_latlong_spec_ref, false)
+
+// ======================================================================
+// Device staging of parameters_changed (sunsky.cpp:242-285): the radiance tables
+// (compute_radiance_params, sunsky.h:158-231; compute_sun_params, :404-419) and the
+// JIT sampling weight / wavelength distribution (estimate_sky_sun_ratio,
+// sunsky.cpp:772-886) written straight into the emitter's device state, on the
+// caller's stream.  The host writes the rest of the state (geometry, TGMM) with an
+// async copy just before; launches that follow on the stream see the new state.
+// ======================================================================
+struct StageArgs {                 // mirrors the host-side struct (sunsky_capi.cpp)
+    SunskyKArgs* state;            // the emitter's device state (sky[], fsky[] written)
+    float* sun_table;              // its turbidity-lerped sun table (written)
+    const float* sky_params_ds;    // (10 T, 2 albedo, 6 ctrl, nch, 9)
+    const float* sky_rad_ds;       // (10, 2, 6, nch)
+    const float* sun_rad_ds;       // (10, sun_block)
+    RadianceStage rs;
+    float albedo[kNbWavelengths];
+    int nch, variant, sun_block;
+    float sky_scale;
+};
+
+// One workgroup: every sky coefficient / radiance entry, every sun-table entry, then
+// one thread per channel folds it (sunsky_staging.h: the host model's arithmetic).
+extern "C" __global__ __launch_bounds__(256) void sunsky_stage_radiance(StageArgs A) {
+    __shared__ float p[kNbWavelengths * kNbSkyParams];
+    __shared__ float r[kNbWavelengths];
+    const int t = threadIdx.x;
+    const int np = A.nch * kNbSkyParams;
+    for (int e = t; e < np; e += blockDim.x)
+        p[e] = radiance_param(A.sky_params_ds, np, e, A.rs, A.albedo[e / kNbSkyParams]);
+    for (int e = t; e < A.nch; e += blockDim.x) r[e] = radiance_param(A.sky_rad_ds, A.nch, e, A.rs, A.albedo[e]);
+    for (int i = t; i < A.sun_block; i += blockDim.x) A.sun_table[i] = sun_param(A.sun_rad_ds, A.sun_block, i, A.rs);
+    __syncthreads();
+    if (t < A.nch) {
+        SkyChannel ch;
+        FastChannel f;
+        fold_channel(&p[t * kNbSkyParams], r[t], A.variant, A.sky_scale, &ch, &f);
+        A.state->sky[t] = ch;
+        A.state->fsky[t] = f;
+    }
+}
+
+constexpr int kQuadBlock = 256;    // one quadrature row per workgroup, one point per thread
+
+struct QuadArgs {                  // mirrors the host-side struct (sunsky_capi.cpp)
+    SunskyKArgs* state;
+    const float* qx;               // 200 Gauss-Legendre nodes / weights (fp32)
+    const float* qw;
+    float* rows;                   // [2][nq][nch] row sums (sky, sun)
+    int nq, nch;
+    float cie_y[kNbWavelengths];
+    float sky_scale, sun_scale;
+    int* status;                   // 0 ok, 1 negative wavelength-distribution entry
+};
+
+// Workgroup j = quadrature row j, thread i = point (i, j): its direction terms once,
+// every channel's sky and sun terms, then a fixed-shape tree reduction over the row's
+// points in LDS (deterministic: the same order on every run).
+extern "C" __global__ __launch_bounds__(kQuadBlock) void sunsky_stage_quad_points(QuadArgs A) {
+    __shared__ float red[2 * kNbWavelengths][kQuadBlock];
+    const int j = blockIdx.x, i = threadIdx.x;
+    const SunskyKArgs& K = *A.state;
+    float as[kNbWavelengths], au[kNbWavelengths];
+#pragma unroll
+    for (int c = 0; c < kNbWavelengths; ++c) as[c] = au[c] = 0.f;
+    if (i < A.nq) {
+        const QuadDir d = quad_dir(K, A.qx, A.qw, i, j);
+        const float wj = A.qw[j];
+#pragma unroll
+        for (int c = 0; c < kNbWavelengths; ++c)
+            if (c < A.nch) quad_channel(K, K.sun_table, K.sun_ld, d, wj, c, &as[c], &au[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < kNbWavelengths; ++c) {
+        red[c][i] = as[c];
+        red[kNbWavelengths + c][i] = au[c];
+    }
+    __syncthreads();
+    for (int h = kQuadBlock / 2; h > 0; h >>= 1) {
+        if (i < h)
+#pragma unroll
+            for (int c = 0; c < 2 * kNbWavelengths; ++c) red[c][i] += red[c][i + h];
+        __syncthreads();
+    }
+    if (i < A.nch) {
+        A.rows[(size_t)j * A.nch + i] = red[i][0];
+        A.rows[(size_t)(A.nq + j) * A.nch + i] = red[kNbWavelengths + i][0];
+    }
+}
+
+// One workgroup: the row sums to LDS, thread c adds channel c's rows in row order, then
+// one thread derives the sampling weight and the wavelength distribution (quad_finish).
+extern "C" __global__ __launch_bounds__(256) void sunsky_stage_quad_finish(QuadArgs A) {
+    __shared__ float rows[2 * 200 * kNbWavelengths];
+    __shared__ float sky[kNbWavelengths], sun[kNbWavelengths];
+    const int total = 2 * A.nq * A.nch;
+    for (int i = threadIdx.x; i < total; i += blockDim.x) rows[i] = A.rows[i];
+    __syncthreads();
+    const int c = threadIdx.x;
+    if (c < A.nch) {
+        float s = 0.f, u = 0.f;
+        for (int j = 0; j < A.nq; ++j) {
+            s += rows[j * A.nch + c];
+            u += rows[(A.nq + j) * A.nch + c];
+        }
+        sky[c] = s;
+        sun[c] = u;
+    }
+    __syncthreads();
+    if (c == 0) {
+        const bool ok = quad_finish(A.state, sky, sun, A.cie_y, A.sky_scale, A.sun_scale);
+        *A.status = ok ? 0 : 1;
+    }
+}

@@ -12,6 +12,7 @@
 #include <sys/stat.h>
 
 #include "sunsky_math.h"
+#include "sunsky_staging.h"
 
 namespace sunsky {
 
@@ -34,38 +35,13 @@ std::vector<float> to_f32(const Table& t) {
     return r;
 }
 
-// bezier_interpolate + compute_radiance_params, sunsky.h:158-231
+// bezier_interpolate + compute_radiance_params, sunsky.h:158-231 (per-entry
+// arithmetic shared with the device staging kernel: sunsky_staging.h)
 void compute_radiance_params(const std::vector<float>& ds, int nch, int npar, const std::vector<float>& albedo,
-                             float turbidity, float eta, std::vector<float>* out) {
-    static const float coefs[kNbSkyCtrlPts] = {1, 5, 10, 10, 5, 1};
-    const int result_size = nch * npar, a_block = kNbSkyCtrlPts * result_size, t_block = kNbAlbedo * a_block;
-    float x = cbrtf(2.f * kInvPi * eta);
-    int t_high = (int)floorf(turbidity), t_low = t_high - 1;
-    float t_rem = turbidity - (float)t_high;
-    bool in_range = (0.f <= eta) && (eta <= 0.5f * kPi);
+                             const RadianceStage& rs, std::vector<float>* out) {
+    const int result_size = nch * npar;
     out->assign(result_size, 0.f);
-    for (int e = 0; e < result_size; ++e) {
-        float bez[2][2];
-        for (int ti = 0; ti < 2; ++ti) {
-            int t = ti ? t_high : t_low;
-            for (int a = 0; a < 2; ++a) {
-                float res = 0.f;
-                if (t >= 0 && t < kNbTurbidity)   // gather mask "t < NB_TURBIDITY"
-                    for (int k = 0; k < kNbSkyCtrlPts; ++k) {
-                        float data = ds[(size_t)t * t_block + a * a_block + k * result_size + e];
-                        float term = coefs[k] * powif_(x, k);
-                        term = term * powif_(1.f - x, kNbSkyCtrlPts - 1 - k);
-                        term = term * data;
-                        res = res + term;
-                    }
-                bez[ti][a] = res;
-            }
-        }
-        float ra_low = lerpf_(bez[0][0], bez[1][0], t_rem);
-        float ra_high = lerpf_(bez[0][1], bez[1][1], t_rem);
-        float v = lerpf_(ra_low, ra_high, albedo[e / npar]);
-        (*out)[e] = in_range ? v : 0.f;
-    }
+    for (int e = 0; e < result_size; ++e) (*out)[e] = radiance_param(ds.data(), result_size, e, rs, albedo[e / npar]);
 }
 
 // Forward-mode derivative of compute_radiance_params (sunsky.h:158-231) along
@@ -114,15 +90,9 @@ void radiance_params_jvp(const std::vector<float>& ds, int nch, int npar, const 
 }
 
 // compute_sun_params, sunsky.h:404-419
-void compute_sun_params(const std::vector<float>& ds, int block, float turbidity, std::vector<float>* out) {
-    int t_high = (int)floorf(turbidity), t_low = t_high - 1;
-    float t_rem = turbidity - (float)t_high;
+void compute_sun_params(const std::vector<float>& ds, int block, const RadianceStage& rs, std::vector<float>* out) {
     out->assign(block, 0.f);
-    for (int i = 0; i < block; ++i) {
-        float lo = (t_low >= 0 && t_low < kNbTurbidity) ? ds[(size_t)t_low * block + i] : 0.f;
-        float hi = (t_high >= 0 && t_high < kNbTurbidity) ? ds[(size_t)t_high * block + i] : 0.f;
-        (*out)[i] = lerpf_(lo, hi, t_rem);
-    }
+    for (int i = 0; i < block; ++i) (*out)[i] = sun_param(ds.data(), block, i, rs);
 }
 
 float clipf_(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
@@ -224,7 +194,8 @@ void gauss_legendre(int n, std::vector<double>* nodes, std::vector<double>* weig
 }
 
 // ------------------------------------------------------------ SunskyModel
-SunskyModel::SunskyModel(const Properties& props, int variant, int semantics, const std::string& datasets)
+SunskyModel::SunskyModel(const Properties& props, int variant, int semantics, const std::string& datasets,
+                         bool radiance_on_host)
     : variant_(variant), semantics_(semantics) {
     if (variant != kRGB && variant != kSpectral)
         throw std::invalid_argument("Unsupported spectrum type, can only render in Spectral or RGB modes!");
@@ -295,9 +266,12 @@ SunskyModel::SunskyModel(const Properties& props, int variant, int semantics, co
     float lv[3] = {local.x, local.y, local.z};
     update_angles(lv);
     load_datasets(datasets);
-    stage();
+    sky_params_.assign((size_t)nch_ * kNbSkyParams, 0.f);
+    sky_rad_.assign(nch_, 0.f);
+    stage(radiance_on_host);
     k_.bs_center[0] = k_.bs_center[1] = k_.bs_center[2] = 0.f;   // unit bounding sphere until set_scene
     k_.bs_radius = 1.f;
+    commit();
 
     std::vector<std::string> unq = props.unqueried();
     if (!unq.empty()) {
@@ -397,8 +371,69 @@ void SunskyModel::update_angles(const float l[3]) {
     k_.sun_t[0] = t.x; k_.sun_t[1] = t.y; k_.sun_t[2] = t.z;
 }
 
-void SunskyModel::stage() {
+// Scalars of the radiance / sun-table staging for the current (turbidity, eta)
+RadianceStage SunskyModel::radiance_stage() const {
+    const float eta = 0.5f * kPi - k_.sun_theta;
+    RadianceStage r;
+    r.x = cbrtf(2.f * kInvPi * eta);
+    r.t_high = (int)floorf(turbidity_);
+    r.t_low = r.t_high - 1;
+    r.t_rem = turbidity_ - (float)r.t_high;
+    r.in_range = (0.f <= eta) && (eta <= 0.5f * kPi);
+    return r;
+}
+
+// compute_radiance_params x2 + compute_sun_params + channel folding (sunsky.h:158-231,
+// 404-419): the part of parameters_changed a GPU emitter runs on the device instead.
+void SunskyModel::stage_radiance() {
     const bool spec = variant_ == kSpectral;
+    const RadianceStage rs = radiance_stage();
+    compute_radiance_params(sky_params_ds_, nch_, kNbSkyParams, albedo_, rs, &sky_params_);
+    compute_radiance_params(sky_rad_ds_, nch_, 1, albedo_, rs, &sky_rad_);
+    for (int c = 0; c < nch_; ++c)
+        fold_channel(&sky_params_[c * kNbSkyParams], sky_rad_[c], variant_, sky_scale_, &k_.sky[c], &k_.fsky[c]);
+    compute_sun_params(sun_rad_ds_, spec ? kSunSpecTableSize : kSunRgbTableSize, rs, &sun_table_);
+}
+
+// Host staging.  radiance_on_host = false (GPU emitters): the sky channels, the sun
+// table and the JIT quadrature are left to the device staging kernels
+// (sunsky_stage_*), which write them into the emitter's device state; the host copy
+// of those fields is then stale until adopt_device_stage().
+void SunskyModel::stage(bool radiance_on_host) {
+    stage_geometry();
+    if (radiance_on_host) {
+        stage_radiance();
+        estimate_sky_sun_ratio();
+    } else if (semantics_ == kScalar) {
+        estimate_sky_sun_ratio();   // constants only (sunsky.cpp:778-783)
+    }
+    radiance_stale_ = !radiance_on_host;
+}
+
+void SunskyModel::adopt_device_stage(const SunskyKArgs& dk, const float* sun_table) {
+    for (int c = 0; c < nch_; ++c) {
+        k_.sky[c] = dk.sky[c];
+        k_.fsky[c] = dk.fsky[c];
+        const SkyChannel& ch = dk.sky[c];
+        const float p[kNbSkyParams] = {ch.A, ch.B, ch.C, ch.D, ch.E, ch.F, ch.G, ch.H, ch.I};
+        for (int q = 0; q < kNbSkyParams; ++q) sky_params_[(size_t)c * kNbSkyParams + q] = p[q];
+        sky_rad_[c] = ch.rad;
+    }
+    k_.w_sky = dk.w_sky;
+    k_.spec_size = dk.spec_size;
+    std::memcpy(k_.spec_pdf, dk.spec_pdf, sizeof(k_.spec_pdf));
+    std::memcpy(k_.spec_cdf, dk.spec_cdf, sizeof(k_.spec_cdf));
+    k_.spec_integral = dk.spec_integral;
+    k_.spec_norm = dk.spec_norm;
+    k_.spec_interval = dk.spec_interval;
+    k_.spec_inv_interval = dk.spec_inv_interval;
+    sun_table_.assign(sun_table, sun_table + (variant_ == kSpectral ? kSunSpecTableSize : kSunRgbTableSize));
+    radiance_stale_ = false;
+}
+
+// Everything of the staging that does not depend on the radiance tables: scales,
+// aperture, pdf constants, the sun-disc row bound and the TGMM / discrete distribution.
+void SunskyModel::stage_geometry() {
     const float eta = 0.5f * kPi - k_.sun_theta;
     k_.variant = variant_;
     k_.semantics = semantics_;
@@ -414,31 +449,9 @@ void SunskyModel::stage() {
                     (1.f - cosf(sun_half_aperture_));
     k_.sun_pdf = kInvTwoPi / (1.f - k_.cos_cutoff);   // square_to_uniform_cone_pdf, warp.h:568-577
 
-    // ---------------- sky radiance (compute_radiance_params x2)
-    compute_radiance_params(sky_params_ds_, nch_, kNbSkyParams, albedo_, turbidity_, eta, &sky_params_);
-    compute_radiance_params(sky_rad_ds_, nch_, 1, albedo_, turbidity_, eta, &sky_rad_);
-    for (int c = 0; c < nch_; ++c) {
-        const float* p = &sky_params_[c * kNbSkyParams];
-        SkyChannel& ch = k_.sky[c];
-        ch.A = p[0]; ch.B = p[1]; ch.C = p[2]; ch.D = p[3]; ch.E = p[4];
-        ch.F = p[5]; ch.G = p[6]; ch.H = p[7]; ch.I = p[8];
-        ch.P = 1.f + ch.I * ch.I;
-        ch.rad = sky_rad_[c];
-        ch.Bl2 = (float)((double)ch.B * 1.4426950408889634074);
-        ch.El2 = (float)((double)ch.E * 1.4426950408889634074);
-        ch.Q = -2.f * ch.I;
-        ch.pad[0] = ch.pad[1] = 0.f;
-        const float Rs = variant_ == kRGB ? ch.rad * sky_scale_ * (float)kCieYNormalization : ch.rad * sky_scale_;
-        FastChannel& f = k_.fsky[c];
-        f.A = ch.A; f.Bl2 = ch.Bl2; f.El2 = ch.El2; f.P = ch.P; f.Q = ch.Q;
-        f.Cs = ch.C * Rs; f.Ds = ch.D * Rs; f.Fs = ch.F * Rs; f.Gs = ch.G * Rs; f.Hs = ch.H * Rs;
-        f.pad[0] = f.pad[1] = 0.f;
-    }
     k_.sun_mul = variant_ == kRGB
                      ? sun_scale_ * k_.area_ratio * (float)kSpecToRgbSunConv * (float)kCieYNormalization
                      : sun_scale_ * k_.area_ratio;
-    // ---------------- sun radiance (compute_sun_params)
-    compute_sun_params(sun_rad_ds_, spec ? kSunSpecTableSize : kSunRgbTableSize, turbidity_, &sun_table_);
     {
         // Lowest segment of render_sun's search (sunsky.cpp:579-587) over the elevations of
         // directions inside the disc, [eta - aperture / 2, eta + aperture / 2], with a margin
@@ -519,7 +532,6 @@ void SunskyModel::stage() {
 
     k_.sun_table = nullptr;   // device pointers are patched in by the C-ABI layer
     k_.sun_ld = nullptr;
-    estimate_sky_sun_ratio();
 }
 
 // Index returned by the kernels' discrete_sample_reuse for s = value * sum:
@@ -577,98 +589,44 @@ void SunskyModel::estimate_sky_sun_ratio() {
         }
         return;
     }
-    constexpr int NQ = 200;
-    std::vector<double> xd, wd;
-    gauss_legendre(NQ, &xd, &wd);
-    float x[NQ], w[NQ];
-    for (int i = 0; i < NQ; ++i) { x[i] = (float)xd[i]; w[i] = (float)wd[i]; }
-    const float3_ sn = mk3(k_.sun_n[0], k_.sun_n[1], k_.sun_n[2]);
-    const float3_ ss = mk3(k_.sun_s[0], k_.sun_s[1], k_.sun_s[2]);
-    const float3_ st = mk3(k_.sun_t[0], k_.sun_t[1], k_.sun_t[2]);
-    float sky[kNbWavelengths] = {0}, sun[kNbWavelengths] = {0};
-    // Row partial sums in parallel, rows added in a fixed order: deterministic
-    // for any thread count.
+    std::vector<float> x, w;
+    quadrature_nodes(&x, &w);
+    const int NQ = (int)x.size();
+    // Row partial sums in parallel, rows added in a fixed order: deterministic for any
+    // thread count, and the same reduction the device staging kernels run.
     std::vector<float> row_sky((size_t)NQ * nch_), row_sun((size_t)NQ * nch_);
 #pragma omp parallel for schedule(static)
     for (int j = 0; j < NQ; ++j) {
-        // sky over the hemisphere: phi = pi (x+1), cos_theta = (x+1)/2
-        float cos_theta = 0.5f * (x[j] + 1.f);
-        float sin_theta = safe_sqrtf_(1.f - cos_theta * cos_theta);
-        // sun over its cone: cos_gamma = ((1-cc) x + (1+cc)) / 2
-        const float cc = k_.cos_cutoff;
-        float cos_gamma = 0.5f * ((1.f - cc) * x[j] + (1.f + cc));
-        float sin_gamma = safe_sqrtf_(1.f - cos_gamma * cos_gamma);
-        for (int c = 0; c < nch_; ++c) { row_sky[(size_t)j * nch_ + c] = 0.f; row_sun[(size_t)j * nch_ + c] = 0.f; }
+        float as[kNbWavelengths] = {0}, au[kNbWavelengths] = {0};
         for (int i = 0; i < NQ; ++i) {
-            float phi = kPi * (x[i] + 1.f);
-            float sp = sinf(phi), cp = cosf(phi);
-            float3_ wo = mk3(sin_theta * cp, sin_theta * sp, cos_theta);
-            float gamma = unit_angle(sn, wo);
-            for (int c = 0; c < nch_; ++c)
-                row_sky[(size_t)j * nch_ + c] += render_sky(k_.sky[c], cos_theta, gamma) * w[i] * w[j];
-            float3_ sw = mk3(sin_gamma * cp, sin_gamma * sp, cos_gamma);
-            float g2 = unit_angle_z(sw);
-            float3_ wl = frame_to_world(ss, st, sn, sw);
-            if (!(wl.z >= 0.f)) continue;
-            float xs;
-            int pos = sun_segment(wl.z, &xs);
-            float cpsi = cos_psi(g2, k_.inv_sin2_half_ap);
+            const QuadDir d = quad_dir(k_, x.data(), w.data(), i, j);
             for (int c = 0; c < nch_; ++c) {
-                float v;
-                if (spec) {
-                    v = render_sun_spec(sun_table_.data(), pos, c, xs) * w[i] * w[j];
-                    v *= sun_limb_darkening(sun_ld_.data(), c, c, 0.f, cpsi);
-                } else {
-                    v = render_sun_rgb(sun_table_.data(), pos, c, xs, cpsi) * w[i] * w[j];
-                }
-                row_sun[(size_t)j * nch_ + c] += v;
+                float vs, vu;
+                quad_channel(k_, sun_table_.data(), sun_ld_.data(), d, w[j], c, &vs, &vu);
+                as[c] += vs;
+                au[c] += vu;
             }
         }
+        for (int c = 0; c < nch_; ++c) {
+            row_sky[(size_t)j * nch_ + c] = as[c];
+            row_sun[(size_t)j * nch_ + c] = au[c];
+        }
     }
+    float sky[kNbWavelengths] = {0}, sun[kNbWavelengths] = {0};
     for (int j = 0; j < NQ; ++j)
         for (int c = 0; c < nch_; ++c) { sky[c] += row_sky[(size_t)j * nch_ + c]; sun[c] += row_sun[(size_t)j * nch_ + c]; }
-    const float J_sky = 0.5f * kPi, J_sun = 0.5f * kPi * (1.f - k_.cos_cutoff);
-    for (int c = 0; c < nch_; ++c) { sky[c] *= J_sky; sun[c] *= J_sun; }
+    if (!quad_finish(&k_, sky, sun, cie_y_, sky_scale_, sun_scale_))
+        throw std::runtime_error("ContinuousDistribution: entries must be non-negative!");
+}
 
-    float sky_lum = sky_scale_, sun_lum = sun_scale_;
-    if (!spec) {
-        auto lum = [](const float* c) { return c[0] * 0.212671f + c[1] * 0.715160f + c[2] * 0.072169f; };
-        sky_lum *= lum(sky);
-        sun_lum *= lum(sun) * k_.area_ratio * (float)kSpecToRgbSunConv;
-    } else {
-        float ls = 0.f, lu = 0.f;
-        for (int c = 0; c < kNbWavelengths; ++c) { ls += cie_y_[c] * sky[c]; lu += cie_y_[c] * sun[c]; }
-        sky_lum *= ls / (float)kNbWavelengths;
-        sun_lum *= lu / (float)kNbWavelengths * k_.area_ratio;
-    }
-    float res = sky_lum / (sky_lum + sun_lum);
-    if (std::isnan(res)) res = 0.f;
-    k_.w_sky = res;
-
-    if (spec) {
-        // ContinuousDistribution(range = [360, 720], avg_spec[1..10]), JIT compute_cdf (distr_1d.h:513-538)
-        const int size = kNbWavelengths - 1;
-        bool all_zero = true;
-        for (int i = 0; i < size; ++i) {
-            k_.spec_pdf[i] = sun[i + 1] + sky[i + 1];
-            all_zero &= k_.spec_pdf[i] == 0.f;
-        }
-        if (all_zero)
-            for (int i = 0; i < size; ++i) k_.spec_pdf[i] += 1.f;
-        for (int i = 0; i < size; ++i)
-            if (k_.spec_pdf[i] < 0.f) throw std::runtime_error("ContinuousDistribution: entries must be non-negative!");
-        k_.spec_size = size;
-        float interval = (720.f - 360.f) / (float)(size - 1), prefix = 0.f, pre[kNbWavelengths];
-        for (int i = 0; i < size; ++i) { prefix += k_.spec_pdf[i]; pre[i] = prefix; }
-        for (int i = 1; i < size; ++i)
-            k_.spec_cdf[i - 1] = interval * (pre[i] - 0.5f * k_.spec_pdf[0] - 0.5f * k_.spec_pdf[i]);
-        k_.spec_interval = interval;
-        k_.spec_integral = k_.spec_cdf[size - 2];
-        k_.spec_norm = 1.f / k_.spec_integral;
-        k_.spec_inv_interval = 1.f / interval;
-    } else {
-        k_.spec_size = 0;
-    }
+// quad::gauss_legendre<Float>(200) nodes and weights, fp64 -> fp32 (sunsky.cpp:789-790)
+void SunskyModel::quadrature_nodes(std::vector<float>* x, std::vector<float>* w) {
+    constexpr int NQ = 200;
+    std::vector<double> xd, wd;
+    gauss_legendre(NQ, &xd, &wd);
+    x->resize(NQ);
+    w->resize(NQ);
+    for (int i = 0; i < NQ; ++i) { (*x)[i] = (float)xd[i]; (*w)[i] = (float)wd[i]; }
 }
 
 void SunskyModel::validate() const {
@@ -784,19 +742,77 @@ void SunskyModel::set_param(const std::string& name, const float* v, int count) 
     else throw std::invalid_argument("unknown parameter '" + name + "'");
 }
 
-void SunskyModel::parameters_changed() {
-    validate();
-    float local[3];
-    if (active_record_) {
-        compute_sun_coordinates(time_, location_, local);
-        float3_ w = xform_vec(k_.to_world, mk3(local[0], local[1], local[2]));
-        sun_dir_[0] = w.x; sun_dir_[1] = w.y; sun_dir_[2] = w.z;
-    } else {
-        float3_ l = xform_vec(k_.to_local, mk3(sun_dir_[0], sun_dir_[1], sun_dir_[2]));
-        local[0] = l.x; local[1] = l.y; local[2] = l.z;
+void SunskyModel::parameters_changed(bool radiance_on_host) {
+    try {
+        validate();
+        float local[3];
+        if (active_record_) {
+            compute_sun_coordinates(time_, location_, local);
+            float3_ w = xform_vec(k_.to_world, mk3(local[0], local[1], local[2]));
+            sun_dir_[0] = w.x; sun_dir_[1] = w.y; sun_dir_[2] = w.z;
+        } else {
+            float3_ l = xform_vec(k_.to_local, mk3(sun_dir_[0], sun_dir_[1], sun_dir_[2]));
+            local[0] = l.x; local[1] = l.y; local[2] = l.z;
+        }
+        update_angles(local);
+        stage(radiance_on_host);
+    } catch (...) {
+        rollback();
+        throw;
     }
-    update_angles(local);
-    stage();
+    commit();
+}
+
+void SunskyModel::commit() {
+    Snapshot& c = committed_;
+    c.turbidity = turbidity_; c.sky_scale = sky_scale_; c.sun_scale = sun_scale_;
+    c.albedo = albedo_; c.time = time_; c.location = location_;
+    std::memcpy(c.sun_dir, sun_dir_, sizeof(sun_dir_));
+    std::memcpy(c.to_world, to_world_, sizeof(to_world_));
+    std::memcpy(c.to_world_d, to_world_d_, sizeof(to_world_d_));
+    std::memcpy(c.to_local_d, to_local_d_, sizeof(to_local_d_));
+    c.sky_params = sky_params_; c.sky_rad = sky_rad_; c.sun_table = sun_table_;
+    std::memcpy(c.gauss_raw, gauss_raw_, sizeof(gauss_raw_));
+    c.k = k_;
+    c.radiance_stale = radiance_stale_;
+}
+
+void SunskyModel::rollback() {
+    const Snapshot& c = committed_;
+    turbidity_ = c.turbidity; sky_scale_ = c.sky_scale; sun_scale_ = c.sun_scale;
+    albedo_ = c.albedo; time_ = c.time; location_ = c.location;
+    std::memcpy(sun_dir_, c.sun_dir, sizeof(sun_dir_));
+    std::memcpy(to_world_, c.to_world, sizeof(to_world_));
+    std::memcpy(to_world_d_, c.to_world_d, sizeof(to_world_d_));
+    std::memcpy(to_local_d_, c.to_local_d, sizeof(to_local_d_));
+    sky_params_ = c.sky_params; sky_rad_ = c.sky_rad; sun_table_ = c.sun_table;
+    std::memcpy(gauss_raw_, c.gauss_raw, sizeof(gauss_raw_));
+    const float bs[4] = {k_.bs_center[0], k_.bs_center[1], k_.bs_center[2], k_.bs_radius};
+    k_ = c.k;
+    k_.bs_center[0] = bs[0]; k_.bs_center[1] = bs[1]; k_.bs_center[2] = bs[2]; k_.bs_radius = bs[3];
+    radiance_stale_ = c.radiance_stale;
+}
+
+int SunskyModel::get_param(const std::string& name, float* out, int cap) const {
+    std::vector<float> v;
+    if (name == "turbidity") v = {turbidity_};
+    else if (name == "sky_scale") v = {sky_scale_};
+    else if (name == "sun_scale") v = {sun_scale_};
+    else if (name == "albedo") v = albedo_;
+    else if (name == "latitude") v = {location_.latitude};
+    else if (name == "longitude") v = {location_.longitude};
+    else if (name == "timezone") v = {location_.timezone};
+    else if (name == "year") v = {(float)time_.year};
+    else if (name == "month") v = {(float)time_.month};
+    else if (name == "day") v = {(float)time_.day};
+    else if (name == "hour") v = {time_.hour};
+    else if (name == "minute") v = {time_.minute};
+    else if (name == "second") v = {time_.second};
+    else if (name == "sun_direction") v.assign(sun_dir_, sun_dir_ + 3);
+    else if (name == "to_world") v.assign(to_world_, to_world_ + 16);
+    else throw std::invalid_argument("unknown parameter '" + name + "'");
+    for (int i = 0; i < (int)v.size() && i < cap; ++i) out[i] = v[i];
+    return (int)v.size();
 }
 
 void SunskyModel::set_scene(bool bbox_valid, const float center[3], float radius) {

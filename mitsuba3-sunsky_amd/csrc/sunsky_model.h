@@ -8,6 +8,7 @@
 
 #include "sunsky_dataset.h"
 #include "sunsky_props.h"
+#include "sunsky_staging.h"
 #include "sunsky_types.h"
 
 namespace sunsky {
@@ -33,15 +34,20 @@ struct EvalTangent {
 class SunskyModel {
 public:
     // SunskyEmitter(const Properties&), sunsky.cpp:162-218.  Throws std::invalid_argument /
-    // std::runtime_error with the reference's messages.
-    SunskyModel(const Properties& props, int variant, int semantics, const std::string& dataset_dir_or_pack);
+    // std::runtime_error with the reference's messages.  radiance_on_host = false leaves the
+    // radiance tables and the JIT quadrature to the device staging kernels (GPU emitters).
+    SunskyModel(const Properties& props, int variant, int semantics, const std::string& dataset_dir_or_pack,
+                bool radiance_on_host = true);
 
     // traverse() parameters (sunsky.cpp:220-240): turbidity, sky_scale, sun_scale,
     // albedo (1 or nch values), latitude, longitude, timezone, year, day, month,
     // hour, minute, second, sun_direction (3), to_world (16, row-major).
     void set_param(const std::string& name, const float* v, int count);
-    // parameters_changed, sunsky.cpp:242-285
-    void parameters_changed();
+    // parameters_changed, sunsky.cpp:242-285.  A rejected update (validation or staging
+    // error) restores the last committed state before rethrowing.
+    void parameters_changed(bool radiance_on_host = true);
+    // Current value of a traverse() parameter (set_param's names) -> count values.
+    int get_param(const std::string& name, float* out, int cap) const;
     // set_scene, sunsky.cpp:287-301
     void set_scene(bool bbox_valid, const float center[3], float radius);
 
@@ -58,6 +64,20 @@ public:
     const std::vector<float>& sky_radiance() const { return sky_rad_; }
     const float* gaussians_raw() const { return gauss_raw_; }
     std::string to_string() const;
+    // device staging: the libm scalars of compute_radiance_params for the current state,
+    // the raw datasets the staging kernels read, the quadrature nodes, and the adoption of
+    // the device-staged fields (sky channels, sun table, w_sky, wavelength distribution)
+    RadianceStage radiance_stage() const;
+    const std::vector<float>& sky_params_ds() const { return sky_params_ds_; }
+    const std::vector<float>& sky_rad_ds() const { return sky_rad_ds_; }
+    const std::vector<float>& sun_rad_ds() const { return sun_rad_ds_; }
+    const float* cie_y() const { return cie_y_; }
+    float sky_scale() const { return sky_scale_; }
+    float sun_scale() const { return sun_scale_; }
+    int semantics() const { return semantics_; }
+    bool radiance_stale() const { return radiance_stale_; }
+    void adopt_device_stage(const SunskyKArgs& device_kargs, const float* sun_table);
+    static void quadrature_nodes(std::vector<float>* x, std::vector<float>* w);
     // Tangent of the eval tables for param (JvpParam) along `tangent`
     // (turbidity: 1 value; albedo: 1 or nch; sun_direction: 3, world space).
     EvalTangent eval_tangent(int param, const float* tangent, int count) const;
@@ -67,7 +87,9 @@ private:
     void load_datasets(const std::string& where);
     void extract_albedo(const Properties& props);
     void update_angles(const float local_sun[3]);
-    void stage();                 // radiance + sun + TGMM + sampling weight
+    void stage(bool radiance_on_host);   // geometry (+ radiance + sampling weight)
+    void stage_geometry();               // scales, aperture, TGMM, discrete distribution
+    void stage_radiance();               // sky channels + sun table (host-only emitters)
     int gauss_search(float s) const;
     void build_gauss_guide();
     void estimate_sky_sun_ratio();
@@ -90,6 +112,23 @@ private:
     std::vector<float> sky_params_, sky_rad_, sun_table_;
     float gauss_raw_[kNbMixture * kNbGaussianParams];
     SunskyKArgs k_;
+    bool radiance_stale_ = false;   // sky channels / sun table / w_sky live on the device only
+    // last committed state (rollback of a rejected parameters_changed)
+    struct Snapshot {
+        float turbidity, sky_scale, sun_scale;
+        std::vector<float> albedo;
+        DateTime time;
+        Location location;
+        float sun_dir[3], to_world[16];
+        double to_world_d[9], to_local_d[9];
+        std::vector<float> sky_params, sky_rad, sun_table;
+        float gauss_raw[kNbMixture * kNbGaussianParams];
+        SunskyKArgs k;
+        bool radiance_stale;
+    };
+    Snapshot committed_;
+    void commit();
+    void rollback();
 };
 
 }  // namespace sunsky

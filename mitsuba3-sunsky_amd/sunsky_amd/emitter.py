@@ -104,12 +104,26 @@ class Parameters(dict):
         if args or kw:
             for k, v in dict(*args, **kw).items():
                 self[k] = v
-        for key in sorted(self._dirty):
-            v = np.atleast_1d(np.asarray(self[key], dtype=np.float32)).reshape(-1)
-            check(lib().sunsky_emitter_set_param(self._emitter._h, key.encode(), _fa(v.tolist()), v.size))
-        self._dirty.clear()
-        check(lib().sunsky_emitter_parameters_changed(self._emitter._h))
-        self._emitter._refresh_info()
+        em = self._emitter
+        try:
+            for key in sorted(self._dirty):
+                v = np.atleast_1d(np.asarray(self[key], dtype=np.float32)).reshape(-1)
+                check(lib().sunsky_emitter_set_param(em._h, key.encode(), _fa(v.tolist()), v.size))
+            if em.device is None:
+                check(lib().sunsky_emitter_parameters_changed(em._h))
+            else:
+                # stream-ordered on the current torch stream: evals queued after this see the
+                # new state; nothing waits for the device (sunsky_emitter_parameters_changed_async)
+                with torch.cuda.device(em.device):
+                    check(lib().sunsky_emitter_parameters_changed_async(em._h, em._stream()))
+        except Exception:
+            # a rejected update leaves the emitter at its last committed values: show them
+            for key in self._dirty:
+                super().__setitem__(key, em.get_param(key))
+            raise
+        finally:
+            self._dirty.clear()
+            em._info = None   # read back lazily (info(), sky_sampling_w, ...)
 
 
 class SunskyEmitter:
@@ -129,6 +143,7 @@ class SunskyEmitter:
         self.is_spectral = variant == "spectral"
         self._props = dict(props)
         self._h = None
+        self._info = None
         host = device == "host"
         self.device = None if host else torch.device(device if device is not None else "cuda")
         if not host and self.device.index is None:
@@ -164,12 +179,31 @@ class SunskyEmitter:
         check(lib().sunsky_emitter_get_info(self._h, C.byref(inf)))
         self._info = inf
 
+    @property
+    def _inf(self):
+        """The emitter's info, read back (once per state) after a stream-ordered update."""
+        if self._info is None:
+            self._refresh_info()
+        return self._info
+
+    def get_param(self, name):
+        """Current value of a traverse() parameter (sunsky_emitter_get_param)."""
+        buf = (C.c_float * 16)()
+        cnt = C.c_int()
+        check(lib().sunsky_emitter_get_param(self._h, name.encode(), buf, 16, C.byref(cnt)))
+        vals = np.frombuffer(buf, dtype=np.float32, count=cnt.value).copy()
+        if name == "to_world":
+            return vals.reshape(4, 4)
+        if name in ("year", "month", "day"):
+            return int(vals[0])
+        return float(vals[0]) if cnt.value == 1 and name != "albedo" else vals
+
     def set_precision(self, precision):
         check(lib().sunsky_emitter_set_precision(self._h, _PRECISION[precision]))
         self._refresh_info()
 
     def info(self):
-        i = self._info
+        i = self._inf
         return {
             "variant": i.variant, "semantics": i.semantics, "nb_channels": i.nb_channels,
             "active_record": bool(i.active_record), "turbidity": i.turbidity, "sky_scale": i.sky_scale,
@@ -191,11 +225,11 @@ class SunskyEmitter:
 
     @property
     def flags(self):
-        return self._info.flags
+        return self._inf.flags
 
     @property
     def sky_sampling_w(self):
-        return self._info.sky_sampling_w
+        return self._inf.sky_sampling_w
 
     def bbox(self):
         mn, mx = (C.c_float * 3)(), (C.c_float * 3)()
@@ -214,19 +248,14 @@ class SunskyEmitter:
         self._refresh_info()
 
     def traverse(self):
-        """Parameters exposed by traverse() (sunsky.cpp:220-240)."""
-        inf = self.info()
-        vals = {"turbidity": inf["turbidity"], "sky_scale": inf["sky_scale"], "sun_scale": inf["sun_scale"],
-                "albedo": self.table("albedo")}
-        if inf["active_record"]:
-            for k in ("latitude", "longitude", "timezone", "year", "day", "month", "hour", "minute", "second"):
-                vals[k] = self._props.get(k, {"latitude": 35.6894, "longitude": 139.6917, "timezone": 9.0,
-                                              "year": 2010, "month": 7, "day": 10, "hour": 15.0, "minute": 0.0,
-                                              "second": 0.0}[k])
+        """Parameters exposed by traverse() (sunsky.cpp:220-240), read back from the emitter."""
+        keys = ["turbidity", "sky_scale", "sun_scale", "albedo"]
+        if self.info()["active_record"]:
+            keys += ["latitude", "longitude", "timezone", "year", "day", "month", "hour", "minute", "second"]
         else:
-            vals["sun_direction"] = inf["sun_dir_world"]
-        vals["to_world"] = np.asarray(self._props.get("to_world", np.eye(4)), dtype=np.float32).reshape(4, 4)
-        return Parameters(self, vals)
+            keys += ["sun_direction"]
+        keys += ["to_world"]
+        return Parameters(self, {k: self.get_param(k) for k in keys})
 
     def __repr__(self):
         buf = C.create_string_buffer(4096)
@@ -418,8 +447,8 @@ class SunskyEmitter:
         else:
             wl, k, lam_p, lstride = None, 3, None, 0
         rho = None
-        if reflectance is not None:
-            rho = self._planes(reflectance, k, n, "reflectance")
+        if reflectance is not None:   # gray albedo per point (include/sunsky_amd.h)
+            rho = self._plane(reflectance, n, "reflectance")
         out = self._out(out, (k, n))
         check(lib().sunsky_direct_diffuse(self._h, nin, _ptr(rho), lam_p, k if self.is_spectral else 0, lstride,
                                           int(seed) & 0xFFFFFFFF, int(spp), n, _ptr(out), out.stride(0),

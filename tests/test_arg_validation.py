@@ -82,7 +82,7 @@ def test_outputs_checked(rgb, spec):
     with pytest.raises(ValueError, match="out"):
         spec.eval_spectral_broadcast(wi(8), [400.0, 500.0], out=torch.zeros((2, 7)))
     with pytest.raises(ValueError, match="reflectance"):
-        rgb.direct_diffuse(wi(8), reflectance=torch.zeros((3, 4)))
+        rgb.direct_diffuse(wi(8), reflectance=torch.zeros(4))
 
 
 def test_numpy_inputs_are_accepted_up_to_the_launch(rgb):

@@ -1,0 +1,150 @@
+"""On-device staging of parameters_changed.
+
+A GPU emitter stages its radiance tables (compute_radiance_params, sunsky.h:158-231;
+compute_sun_params, :404-419) and the JIT sampling quadrature (estimate_sky_sun_ratio,
+sunsky.cpp:772-886) with kernels on the caller's stream.  Checked against the host
+staging of a host-only emitter (itself pinned to the oracle by tests/test_capi_cpu.py):
+
+* the polynomial staging (sky coefficients, sky radiance, sun table) is the same
+  arithmetic in the same order (csrc/sunsky_staging.h): bit for bit;
+* the quadrature (200 x 200 Gauss-Legendre, libm sin/cos/exp/pow on both sides, device
+  partial sums in a different fixed order): w_sky and the wavelength distribution
+  within 2e-6 relative;
+* an update is stream-ordered: eval queued right after params.update() on the same
+  stream, with no synchronisation, equals a freshly built emitter bit for bit.
+"""
+import time
+
+import numpy as np
+import pytest
+import torch
+
+import sunsky_amd as ss
+from helpers import SPECIAL_ALBEDO, angles_dict, hemisphere_wo, hour_dict
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ("rgb", "jit", hour_dict(3, 11.7753, 0.1, 1.0, 1.0)),
+    ("rgb", "jit", angles_dict(2.0, 0.3, np.deg2rad(45), 0.1, 1.0, 1.0)),
+    ("rgb", "scalar", angles_dict(6.0, -1.2, np.deg2rad(70), 0.5, 1.0, 1.0)),
+    ("rgb", "jit", angles_dict(10.0, 2.0, np.deg2rad(20), [0.1, 0.5, 0.9], 0.7, 1.3)),
+    ("spectral", "jit", angles_dict(3.0, 0.0, np.deg2rad(30), 0.3, 1.0, 1.0)),
+    ("spectral", "jit", angles_dict(4.2, 0.0, np.deg2rad(30), SPECIAL_ALBEDO, 1.0, 1.0)),
+    ("spectral", "scalar", hour_dict(5.2, 9.5, 0.2, 1.0, 1.0)),
+    ("rgb", "jit", dict(angles_dict(3.0, 0.5, np.deg2rad(40), 0.3, 1.0, 1.0), sun_aperture=30.0)),
+    ("rgb", "jit", angles_dict(1.0, 0.5, np.deg2rad(95), 0.3, 1.0, 1.0)),   # sun below the horizon
+]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+
+
+def _bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+def assert_staged_equal(gpu, host):
+    for t in ("sky_params", "sky_radiance", "sun_radiance"):
+        a, b = gpu.table(t), host.table(t)
+        assert np.array_equal(_bits(a), _bits(b)), f"{t}: max diff {np.abs(a - b).max():.3e}"
+    wg, wh = gpu.sky_sampling_w, host.sky_sampling_w
+    assert abs(wg - wh) <= 2e-6 * max(abs(wh), 1e-30), (wg, wh)
+    pg, ph = gpu.table("spectral_pdf"), host.table("spectral_pdf")
+    assert pg.shape == ph.shape
+    if ph.size:
+        np.testing.assert_allclose(pg, ph, rtol=2e-6)
+        np.testing.assert_allclose(gpu.table("spectral_cdf"), host.table("spectral_cdf"), rtol=2e-6)
+    for t in ("gaussians", "gaussian_cdf", "albedo"):
+        assert np.array_equal(_bits(gpu.table(t)), _bits(host.table(t))), t
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}-{c[1]}-{i}" for i, c in enumerate(CASES)])
+def test_device_staging_matches_host_staging(case):
+    variant, sem, d = case
+    gpu = ss.SunskyEmitter(d, variant, sem)
+    host = ss.SunskyEmitter(d, variant, sem, device="host")
+    assert_staged_equal(gpu, host)
+
+
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+def test_update_is_stream_ordered(variant):
+    """params.update() then eval on the same (non-default) stream, no sync in between."""
+    d = angles_dict(3.0, 0.2, np.deg2rad(50), 0.3, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, variant)
+    n = 1 << 16
+    wi = torch.from_numpy(np.ascontiguousarray(-hemisphere_wo(n, seed=3).T)).cuda()
+    lam = torch.full((4, n), 500.0, device="cuda") + 50 * torch.arange(4, device="cuda").view(4, 1)
+    si = ss.SurfaceInteraction3f(wi=wi, wavelengths=lam if variant == "spectral" else None)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    outs = []
+    seq = [(6.5, 0.7), (2.25, 0.1), (9.0, 0.45)]
+    with torch.cuda.stream(side):
+        p = em.traverse()
+        for turb, alb in seq:
+            p["turbidity"] = turb
+            p["albedo"] = alb
+            p.update()
+            outs.append(em.eval(si))          # queued behind the staging kernels
+    torch.cuda.synchronize()
+    for (turb, alb), got in zip(seq, outs):
+        fresh = ss.SunskyEmitter(dict(d, turbidity=turb, albedo=alb), variant)
+        ref = fresh.eval(si)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref), (turb, alb)
+    host = ss.SunskyEmitter(dict(d, turbidity=seq[-1][0], albedo=seq[-1][1]), variant, device="host")
+    assert_staged_equal(em, host)
+
+
+def test_update_latency_report():
+    """params.update() host time and device staging time (printed; bounded loosely)."""
+    d = angles_dict(3.0, 0.2, np.deg2rad(50), 0.3, 1.0, 1.0)
+    for variant in ("rgb", "spectral"):
+        em = ss.SunskyEmitter(d, variant)
+        p = em.traverse()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 50
+        t0 = time.perf_counter()
+        e0.record()
+        for k in range(reps):
+            p["turbidity"] = 3.0 + 0.01 * k
+            p.update()
+        e1.record()
+        host_ms = (time.perf_counter() - t0) / reps * 1e3
+        torch.cuda.synchronize()
+        dev_ms = e0.elapsed_time(e1) / reps
+        hs = ss.SunskyEmitter(d, variant, device="host")
+        hp = hs.traverse()
+        t0 = time.perf_counter()
+        for k in range(5):
+            hp["turbidity"] = 3.0 + 0.01 * k
+            hp.update()
+        cpu_ms = (time.perf_counter() - t0) / 5 * 1e3
+        print(f"{variant}: update() host {host_ms:.3f} ms/call, device staging {dev_ms:.3f} ms/update; "
+              f"host-only staging {cpu_ms:.2f} ms/update")
+        assert host_ms < 5.0 and dev_ms < 5.0
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs 2 GPUs")
+def test_emitter_on_non_current_device():
+    """every call runs on the emitter's own device, whatever device is current."""
+    d = angles_dict(3.0, 0.2, np.deg2rad(50), 0.3, 1.0, 1.0)
+    em1 = ss.SunskyEmitter(d, "rgb", device="cuda:1")
+    em0 = ss.SunskyEmitter(d, "rgb", device="cuda:0")
+    n = 4096
+    wi = torch.from_numpy(np.ascontiguousarray(-hemisphere_wo(n, seed=3).T))
+    torch.cuda.set_device(0)
+    out1 = em1.eval(ss.SurfaceInteraction3f(wi=wi.to("cuda:1")))
+    grad = em1.eval_vjp(ss.SurfaceInteraction3f(wi=wi.to("cuda:1")), torch.ones((3, n), device="cuda:1"))[0]
+    bake = em1.bake_latlong(64, 32)
+    out0 = em0.eval(ss.SurfaceInteraction3f(wi=wi.to("cuda:0")))
+    torch.cuda.synchronize(0)
+    torch.cuda.synchronize(1)
+    assert out1.device.index == 1 and grad.device.index == 1 and bake.device.index == 1
+    assert torch.equal(out1.cpu(), out0.cpu())

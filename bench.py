@@ -301,6 +301,87 @@ def parity_c4(em, d_scene, u, d, pdf_s, wgt, pdf_q, n_check=1 << 19):
             "bounds": "dir p99.9 < 2e-6, max < 1e-4; pdf 1e-5 rel; weights 2e-5 (sky vs o32, sun vs o64)"}
 
 
+def run_c5(args, world, rank, dev, coll_dev, rehearsal):
+    """configs[4]: a --c5-dirs spectral batch per GPU (11 model
+    wavelengths, the C3 node kernel), then the gather of every rank's (11, n) radiance
+    planes into rank 0's (11, N) planes.  Per-GPU eval time (max over ranks), whole-job
+    evals/s, gather time and GB/s; rank 0's own shard checked bitwise after the gather.
+    Returns the report on rank 0, None elsewhere."""
+    n5 = args.c5_dirs
+    wi5 = -hemisphere_dirs(n5, seed=4321 + rank, device=dev)
+    spec5 = ss.SunskyEmitter(dict(sun_dict(3.0), albedo=0.3), "spectral", precision=args.precision, device=dev)
+    lams = [float(x) for x in range(320, 721, 40)]
+    out5 = torch.empty((11, n5), dtype=torch.float32, device=dev)
+    for _ in range(2):
+        spec5.eval_spectral_broadcast(wi5, lams, out=out5)
+    reps = max(3, args.steps // 10)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        spec5.eval_spectral_broadcast(wi5, lams, out=out5)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    te = (time.perf_counter() - t0) / reps
+    tg, tcat, own_ok, gpath = 0.0, 0.0, True, None
+    if world > 1:
+        from sunsky_amd.sharding import RadianceComm, gather_shards, shard_sizes
+        t = torch.tensor([te], device=coll_dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        te = float(t.item())
+        tgs = []
+        if not rehearsal:
+            # C ABI gather (grouped RCCL send/recv) straight into rank 0's final planes
+            gpath = "sunsky_gather_radiance: RCCL send/recv into rank 0's (11, N) planes, no padding / concat"
+            comm = RadianceComm(device=dev)
+            full = torch.empty((11, n5 * world), dtype=torch.float32, device=dev) if rank == 0 else None
+            comm.gather(out5, n5 * world, out=full)         # untimed: connection setup
+            for _ in range(3):
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                comm.gather(out5, n5 * world, out=full)
+                torch.cuda.synchronize()
+                tgs.append(time.perf_counter() - t0)
+            if rank == 0:
+                own_ok = bool(torch.equal(full[:, :n5], out5))
+            comm.close()
+            del full
+        else:
+            gpath = "torch.distributed.gather of padded shards + torch.cat (gloo rehearsal)"
+            send = out5.to(coll_dev)
+            bufs = gather_shards(send, n5 * world)           # untimed: connection setup
+            for _ in range(3):                                 # the collective alone, preallocated
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                gather_shards(send, n5 * world, bufs=bufs)
+                torch.cuda.synchronize()
+                tgs.append(time.perf_counter() - t0)
+            if rank == 0:
+                t0 = time.perf_counter()
+                full = torch.cat([b[:, :s] for b, s in zip(bufs, shard_sizes(n5 * world, world))], dim=1)
+                torch.cuda.synchronize()
+                tcat = time.perf_counter() - t0
+                own_ok = bool(torch.equal(full[:, :n5].to(dev), out5))
+                del full
+            del bufs, send
+        tg = sorted(tgs)[1]
+    if rank == 0:
+        nbytes = 11 * n5 * 4 * (world - 1)
+        return {
+            "dirs_per_gpu": n5, "lambdas": 11, "eval_s": te,
+            "evals_per_s_whole_job": 11 * n5 * world / te,
+            "gather_s": tg, "gather_bytes_to_root": nbytes, "gather_GBps": nbytes / tg / 1e9 if tg else None,
+            "gather_path": gpath,
+            "gather_timing": "median of 3 gathers into preallocated buffers after one untimed call",
+            "reassemble_planes_s": tcat, "end_to_end_s": te + tg + tcat, "bitwise_own_shard": own_ok,
+            "note": "configs[4]: per-GPU spectral eval (weak scaling) then gather of the radiance to rank 0"}
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -313,7 +394,9 @@ def main():
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather of the radiance to rank 0")
     ap.add_argument("--no-pmc", action="store_true", help="do not read the committed PMC traffic summary")
     ap.add_argument("--c5", action="store_true",
-                    help="also run configs[4]: spectral 11-lambda eval of --c5-dirs per GPU + gather to rank 0")
+                    help="also run configs[4]: spectral 11-lambda eval of --c5-dirs per GPU + gather to rank 0 "
+                         "(default on when more than one rank runs; --no-c5 turns it off)")
+    ap.add_argument("--no-c5", action="store_true")
     ap.add_argument("--c5-dirs", type=int, default=1 << 26, help="directions per GPU for --c5 (default 64M)")
     args = ap.parse_args()
 
@@ -600,78 +683,32 @@ def main():
 
     # ----------------------------------------------------------- optional gather
     if args.gather and world > 1:
-        # configs[4]'s final step: the radiance shards gathered to rank 0 over RCCL
-        # (sunsky_amd.sharding.gather_radiance); reported beside `value`, never in it.
+        # configs[4]'s final step: the radiance shards gathered to rank 0 through the C ABI's
+        # RCCL gather (sunsky_gather_radiance); reported beside `value`, never in it.
         from sunsky_amd.sharding import gather_radiance
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        full = gather_radiance(outs[0].to(coll_dev), n * world)
+        full = gather_radiance(outs[0] if not rehearsal else outs[0].cpu(), n * world)
         torch.cuda.synchronize()
         gt = time.perf_counter() - t0
         if rank == 0:
             nbytes = outs[0].numel() * 4 * (world - 1)
             result["gather"] = {"seconds": gt, "bytes_to_root": nbytes, "GBps": nbytes / gt / 1e9,
+                                "path": "torch.distributed.gather (gloo rehearsal)" if rehearsal
+                                        else "sunsky_gather_radiance (RCCL send/recv)",
                                 "bitwise_own_shard": bool(torch.equal(full[:, :n].to(dev), outs[0]))}
         del full
 
     # ------------------------------------------- configs[4]: spectral shard + gather
-    if args.c5:
-        from sunsky_amd.sharding import gather_radiance
-        n5 = args.c5_dirs
+    if (args.c5 or world > 1) and not args.no_c5:
         del outs
-        wi5 = -hemisphere_dirs(n5, seed=4321 + rank, device=dev)
-        spec5 = ss.SunskyEmitter(dict(sun_dict(3.0), albedo=0.3), "spectral", precision=args.precision, device=dev)
-        lams = [float(x) for x in range(320, 721, 40)]
-        out5 = torch.empty((11, n5), dtype=torch.float32, device=dev)
-        for _ in range(2):
-            spec5.eval_spectral_broadcast(wi5, lams, out=out5)
-        reps = max(3, args.steps // 10)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            spec5.eval_spectral_broadcast(wi5, lams, out=out5)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        te = (time.perf_counter() - t0) / reps
-        tg, tcat, own_ok = 0.0, 0.0, True
-        if world > 1:
-            from sunsky_amd.sharding import gather_shards, shard_sizes
-            t = torch.tensor([te], device=coll_dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            te = float(t.item())
-            send = out5.to(coll_dev)
-            bufs = gather_shards(send, n5 * world)           # untimed: connection setup
-            tgs = []
-            for _ in range(3):                                 # the collective alone, preallocated
-                torch.cuda.synchronize()
-                dist.barrier()
-                t0 = time.perf_counter()
-                gather_shards(send, n5 * world, bufs=bufs)
-                torch.cuda.synchronize()
-                tgs.append(time.perf_counter() - t0)
-            tg = sorted(tgs)[1]
-            if rank == 0:
-                t0 = time.perf_counter()
-                full = torch.cat([b[:, :s] for b, s in zip(bufs, shard_sizes(n5 * world, world))], dim=1)
-                torch.cuda.synchronize()
-                tcat = time.perf_counter() - t0
-                own_ok = bool(torch.equal(full[:, :n5].to(dev), out5))
-                del full
-            del bufs, send
+        try:
+            c5 = run_c5(args, world, rank, dev, coll_dev, rehearsal)
+        except Exception as exc:   # reported beside `value`; never fail the bench line
+            c5 = {"error": f"{type(exc).__name__}: {exc}"}
         if rank == 0:
-            nbytes = 11 * n5 * 4 * (world - 1)
-            result["c5_spectral_shard_gather"] = {
-                "dirs_per_gpu": n5, "lambdas": 11, "eval_s": te,
-                "evals_per_s_whole_job": 11 * n5 * world / te,
-                "gather_s": tg, "gather_bytes_to_root": nbytes, "gather_GBps": nbytes / tg / 1e9 if tg else None,
-                "gather_timing": "median of 3 dist.gather into preallocated per-rank buffers after one untimed call",
-                "reassemble_planes_s": tcat, "end_to_end_s": te + tg + tcat, "bitwise_own_shard": own_ok,
-                "note": "configs[4]: per-GPU spectral eval (weak scaling) then gather of the radiance to rank 0"}
-        del wi5, out5
+            result["c5_spectral_shard_gather"] = c5
 
     if rank == 0:
         if not args.no_cpu and world == 1:   # the CPU baseline: rank 0 at N=1 only

@@ -47,7 +47,8 @@ typedef enum sunsky_status {
     SUNSKY_ERROR_FORMAT = 3,          /* dataset header / size mismatch (sunsky.h:531)   */
     SUNSKY_ERROR_HIP = 4,             /* HIP runtime / code object failure               */
     SUNSKY_ERROR_NOT_IMPLEMENTED = 5, /* sample_position (sunsky.cpp:483-495)            */
-    SUNSKY_ERROR_INTERNAL = 6
+    SUNSKY_ERROR_INTERNAL = 6,
+    SUNSKY_ERROR_COMM = 7             /* RCCL unavailable / communicator failure         */
 } sunsky_status;
 
 typedef enum sunsky_variant {     /* mitsuba.conf variants: *_rgb / *_spectral */
@@ -286,6 +287,27 @@ const char *plugin_descr(void);
 
 /* Path of the bundled dataset pack the library resolves by default. */
 int sunsky_default_dataset_path(char *buf, size_t capacity);
+
+/* ------------------------------------------------------------ multi-GPU gather
+ * configs[4]: one process per GPU, each evaluating its contiguous
+ * slice of the ray batch; the only exchange is the gather of the radiance planes to
+ * one rank (the reference's ncclGather, rccl.h:745-746).  RCCL is loaded on first use
+ * (dlopen librccl.so.1); without it these calls return SUNSKY_ERROR_COMM. */
+#define SUNSKY_COMM_ID_BYTES 128
+typedef struct sunsky_comm sunsky_comm;
+/* ncclGetUniqueId: rank 0 makes the id, the caller hands it to every rank (any channel). */
+int sunsky_comm_get_unique_id(unsigned char id[SUNSKY_COMM_ID_BYTES]);
+/* ncclCommInitRank on the CURRENT HIP device (collective over the nranks processes). */
+int sunsky_comm_create(const unsigned char id[SUNSKY_COMM_ID_BYTES], int nranks, int rank, sunsky_comm **out);
+void sunsky_comm_destroy(sunsky_comm *comm);
+int sunsky_comm_info(const sunsky_comm *comm, int *rank, int *nranks, int *device);
+/* Gather every rank's shard into root's final planes, stream-ordered: rank r sends nplanes
+ * planes of counts[r] floats (plane p at send + p * send_stride); on root they land at
+ * recv + p * recv_stride + sum(counts[0..r)).  counts[] (nranks entries) is the same on
+ * every rank; recv is only read on root.  Grouped ncclSend / ncclRecv: no padding and no
+ * re-layout copy; root's own shard is a device copy (none when already in place). */
+int sunsky_gather_radiance(sunsky_comm *comm, int root, const float *send, size_t send_stride, int nplanes,
+                           const size_t *counts, float *recv, size_t recv_stride, void *stream);
 
 #ifdef __cplusplus
 }

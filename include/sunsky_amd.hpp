@@ -251,7 +251,18 @@ public:
     void set_parameter(const char* name, const std::vector<float>& values) {
         check(sunsky_emitter_set_param(e_, name, values.data(), (int)values.size()));
     }
+    // Blocking restage on the default stream (state read back to the host).
     void parameters_changed() { check(sunsky_emitter_parameters_changed(e_)); }
+    // Stream-ordered restage: the staging kernels run on `stream`; launches queued on it
+    // afterwards see the new state (sunsky_emitter_parameters_changed_async).
+    void parameters_changed(void* stream) { check(sunsky_emitter_parameters_changed_async(e_, stream)); }
+    // Current value of a traverse() parameter (sunsky_emitter_get_param).
+    std::vector<float> parameter(const char* name) const {
+        float buf[16];
+        int n = 0;
+        check(sunsky_emitter_get_param(e_, name, buf, 16, &n));
+        return std::vector<float>(buf, buf + n);
+    }
     void set_precision(Precision p) { check(sunsky_emitter_set_precision(e_, (int)p)); }
 
     sunsky_info info() const {

@@ -20,6 +20,7 @@
 #include <sys/stat.h>
 
 #include "sunsky_dataset.h"
+#include "sunsky_errors.h"
 #include "sunsky_model.h"
 #include "sunsky_props.h"
 #include "sunsky_types.h"
@@ -32,43 +33,17 @@ double hosek_solar_radiance(const std::string& datasets, double turbidity, doubl
                             double gamma);
 }
 
+namespace sunsky {
+namespace capi {
+std::string& last_error() {
+    thread_local std::string g_error;
+    return g_error;
+}
+}  // namespace capi
+}  // namespace sunsky
+
 namespace {
-thread_local std::string g_error;
-
-int fail(int code, const std::string& msg) {
-    g_error = msg;
-    return code;
-}
-
-struct HipError : std::runtime_error {
-    using std::runtime_error::runtime_error;
-};
-
-void hip_check(hipError_t e, const char* what) {
-    if (e != hipSuccess) throw HipError(std::string(what) + ": " + hipGetErrorString(e));
-}
-
-template <typename F>
-int guarded(F&& f) {
-    try {
-        f();
-        return SUNSKY_OK;
-    } catch (const HipError& e) {
-        return fail(SUNSKY_ERROR_HIP, e.what());
-    } catch (const std::invalid_argument& e) {
-        return fail(SUNSKY_ERROR_INVALID_VALUE, e.what());
-    } catch (const std::runtime_error& e) {
-        std::string m = e.what();
-        int code = (m.find("does not exist") != std::string::npos || m.find("cannot open") != std::string::npos)
-                       ? SUNSKY_ERROR_FILE
-                       : SUNSKY_ERROR_FORMAT;
-        return fail(code, m);
-    } catch (const std::exception& e) {
-        return fail(SUNSKY_ERROR_INTERNAL, e.what());
-    } catch (...) {
-        return fail(SUNSKY_ERROR_INTERNAL, "unknown error");
-    }
-}
+using namespace sunsky::capi;
 
 // ---------------------------------------------------------------- paths
 std::string library_dir() {
@@ -512,7 +487,7 @@ struct sunsky_emitter {
 extern "C" {
 
 int sunsky_abi_version(void) { return SUNSKY_AMD_ABI_VERSION; }
-const char* sunsky_last_error(void) { return g_error.c_str(); }
+const char* sunsky_last_error(void) { return last_error().c_str(); }
 
 int sunsky_props_create(sunsky_props** out) {
     if (!out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null output pointer");

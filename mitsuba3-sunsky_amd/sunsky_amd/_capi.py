@@ -14,7 +14,8 @@ CODE_OBJECT = os.path.join(BUILD_DIR, "sunsky_kernels.hsaco")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "sunsky_amd.h")
 
 OK = 0
-ERRORS = {1: ValueError, 2: FileNotFoundError, 3: ValueError, 4: RuntimeError, 5: NotImplementedError, 6: RuntimeError}
+ERRORS = {1: ValueError, 2: FileNotFoundError, 3: ValueError, 4: RuntimeError, 5: NotImplementedError, 6: RuntimeError,
+          7: RuntimeError}
 
 VARIANT_RGB, VARIANT_SPECTRAL = 0, 1
 SEMANTICS_JIT, SEMANTICS_SCALAR = 0, 1
@@ -98,6 +99,12 @@ _SIGS = {
                                          C.POINTER(C.c_size_t), C.POINTER(C.c_uint64), C.POINTER(C.c_int)]),
     "sunsky_array_to_file": (C.c_int, [C.c_char_p, c_float_p, C.c_size_t, C.POINTER(C.c_uint64), C.c_int]),
     "sunsky_default_dataset_path": (C.c_int, [C.c_char_p, C.c_size_t]),
+    "sunsky_comm_get_unique_id": (C.c_int, [C.c_char_p]),
+    "sunsky_comm_create": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.POINTER(vp)]),
+    "sunsky_comm_destroy": (None, [vp]),
+    "sunsky_comm_info": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "sunsky_gather_radiance": (C.c_int, [vp, C.c_int, vp, C.c_size_t, C.c_int, C.POINTER(C.c_size_t), vp,
+                                         C.c_size_t, vp]),
 }
 
 _lib = None

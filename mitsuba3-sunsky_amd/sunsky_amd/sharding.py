@@ -4,14 +4,21 @@ Directions / samples are independent and the per-emitter tables (<= 16 KB) are
 staged identically on every rank, so a batch of N rays splits into contiguous
 per-rank slices with no data-path collective; the only exchange is the
 optional gather of the radiance buffer to one rank (the reference's
-ncclGather of configs[4]), done here with torch.distributed (backend "nccl" =
-RCCL over xGMI on MI355X, "gloo" for the CPU tests).
+ncclGather of configs[4]).  On GPUs that gather is the C ABI's
+sunsky_gather_radiance (grouped RCCL send/recv over xGMI straight into the
+root's final [C][N] planes, csrc/sunsky_comm.cpp); torch.distributed only hands
+the RCCL unique id to the ranks.  CPU tensors (the gloo tests) take a
+torch.distributed.gather fallback with the same partitioning.
 
 Slice starts are multiples of 4 rays so every rank's SoA planes keep the
 16-byte alignment the VEC=4 eval kernel needs.
 """
+import ctypes as C
+
 import torch
 import torch.distributed as dist
+
+from ._capi import check, lib
 
 ALIGN = 4
 
@@ -53,11 +60,76 @@ def gather_shards(local, n_total, dst=0, group=None, bufs=None):
     return bufs if rank == dst else None
 
 
-def gather_radiance(local, n_total, dst=0, group=None):
+def gather_radiance(local, n_total, dst=0, group=None, comm=None):
     """Gather every rank's (C, n_r) radiance shard into the (C, n_total) buffer on `dst`
-    (None elsewhere).  Shards are padded to the largest size for the collective."""
+    (None elsewhere).  GPU shards go through the C ABI's RCCL gather (`comm`, a
+    RadianceComm, made on first use if None); CPU shards (gloo) through
+    torch.distributed.gather of padded shards."""
+    if local.is_cuda:
+        comm = comm if comm is not None else RadianceComm(group, local.device)
+        return comm.gather(local, n_total, root=dst)
     bufs = gather_shards(local, n_total, dst, group)
     if bufs is None:
         return None
     sizes = shard_sizes(n_total, dist.get_world_size(group))
     return torch.cat([b[:, :s] for b, s in zip(bufs, sizes)], dim=1)
+
+
+class RadianceComm:
+    """An RCCL communicator of the C ABI (sunsky_comm_create) over the ranks of a
+    torch.distributed group, on `device` (default: the current one).  Collective:
+    every rank of the group constructs it."""
+
+    def __init__(self, group=None, device=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        uid = C.create_string_buffer(128)
+        if self.rank == 0:
+            check(lib().sunsky_comm_get_unique_id(uid))
+        box = [bytes(uid.raw)]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib().sunsky_comm_create(box[0], self.world, self.rank, C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().sunsky_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def gather(self, local, n_total, root=0, out=None, stream=None):
+        """Every rank's (C, n_r) shard (n_r = shard_sizes(n_total)[rank]) into root's (C,
+        n_total) planes; returns them on root, None elsewhere.  Stream-ordered on the
+        current stream (or `stream`)."""
+        sizes = shard_sizes(n_total, self.world)
+        if local.dim() != 2 or local.shape[1] != sizes[self.rank] or local.dtype != torch.float32:
+            raise ValueError(f"rank {self.rank}: shard must be float32 (C, {sizes[self.rank]})")
+        if local.shape[1] and local.stride(1) != 1:
+            raise ValueError("shard planes must be contiguous")
+        c = local.shape[0]
+        if self.rank == root and out is None:
+            out = torch.empty((c, n_total), dtype=torch.float32, device=self.device)
+        if self.rank == root and (tuple(out.shape) != (c, n_total) or out.stride(1) != 1):
+            raise ValueError(f"out must be a (C, {n_total}) tensor with contiguous planes")
+        counts = (C.c_size_t * self.world)(*sizes)
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        send = C.c_void_p(local.data_ptr()) if local.numel() else C.c_void_p()
+        recv = C.c_void_p(out.data_ptr()) if self.rank == root else C.c_void_p()
+        check(lib().sunsky_gather_radiance(self._h, root, send, local.stride(0) if c > 1 else sizes[self.rank], c,
+                                           counts, recv, out.stride(0) if self.rank == root else 0,
+                                           C.c_void_p(st.cuda_stream)))
+        return out if self.rank == root else None
+
+
+def gather_radiance_rccl(comm, local, n_total, dst=0, out=None):
+    """sunsky_gather_radiance through a RadianceComm: no padding, no concatenation."""
+    return comm.gather(local, n_total, root=dst, out=out)

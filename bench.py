@@ -99,6 +99,27 @@ def pmc_traffic(kernel):
     return rec["traffic_bytes"], os.path.relpath(files[-1], ROOT)
 
 
+def valu_floor(kernel):
+    """VALU-issue floor of one launch of `kernel` from the newest committed
+    profiles/rNN_*valu_roofline.json (tools/gpu_valu.sh + tools/valu_summary.py: PMC
+    SQ_INSTS_VALU / SQ_INSTS_VALU_TRANS_F32 per dispatch; 2 cycles per plain and 8 per
+    transcendental wave64 instruction, 1024 SIMDs at 2.4 GHz).  None when absent."""
+    import glob
+    import re
+
+    def version(path):
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_valu_roofline.json")), key=version)
+    if not files:
+        return None
+    with open(files[-1]) as fh:
+        rec = json.load(fh).get(kernel)
+    if not rec:
+        return None
+    return {"valu_wave_insts": rec["valu_wave_insts"], "trans_wave_insts": rec["trans_wave_insts"],
+            "issue_floor_ms": rec["valu_issue_floor_ms"], "source": os.path.relpath(files[-1], ROOT)}
+
+
 def host_cpu_topology():
     """lscpu-style facts of the host plus the CPU quota this process may use (cgroup v2
     cpu.max: quota / period CPUs; on the GPU box 1600000 / 100000 = 16 of 256 CPUs)."""
@@ -601,6 +622,7 @@ def main():
         del lam4, rays_out
         # C4: sample_direction + pdf_direction, 64M samples (per GPU)
         ns = 4 * n
+        kfx = "ref" if args.precision == "reference" else "fast"
         smp = ss.SunskyEmitter(dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), "rgb", precision=args.precision,
                                device=dev)
         g = torch.Generator(device=dev)
@@ -646,6 +668,14 @@ def main():
                               "achieved_GBps": BYTES_SAMPLE * ns / (ms * 1e-3) / 1e9,
                               "note": "sample_direction (reads u; writes d, pdf, RGB weight) + pdf_direction "
                                       "(reads d; writes pdf)"}
+        vs, vp = valu_floor("sunsky_sample_direction_rgb_lean_" + kfx), valu_floor("sunsky_pdf_direction_v4_" + kfx)
+        if vs and vp:
+            sec["sampling_C4"]["valu_roofline"] = {
+                "bound": "valu", "unit": "ms",
+                "sample_direction": dict(vs, achieved_ms=ms_s, frac=vs["issue_floor_ms"] / ms_s),
+                "pdf_direction": dict(vp, achieved_ms=ms_p, frac=vp["issue_floor_ms"] / ms_p),
+                "note": "frac = VALU-issue floor (PMC instruction counts x issue cycles / (1024 SIMDs x 2.4 GHz)) "
+                        "/ measured launch time; HBM frac of the same launches is achieved_GBps / 8000"}
         if rank == 0:
             sec["sampling_C4"]["parity"] = parity_c4(smp, dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), u, d,
                                                      pdf_s, wgt, pdf_q)

@@ -2127,6 +2127,7 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_ref, false, false, true)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_fast, true, true, true)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_ref, false, true, true)
 
+
 #define SS_PDF_DIRECTION(NAME, VEC, FAST)                                                                     \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
         const SunskyKArgs* __restrict__ Kp, const float* dx, const float* dy, const float* dz, const uint8_t* active, size_t n,     \

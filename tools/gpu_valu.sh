@@ -1,0 +1,20 @@
+#!/bin/bash
+# VALU-roofline counters (one rocprofv3 --pmc pass per kernel; 8 SQ + 1 GRBM counters):
+# VALU / transcendental wave-instructions, VALU-active and wave cycles, waves, GPU-active cycles.
+# Summary: tools/valu_summary.py gpurun_out/valu/*/*counter_collection.csv
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out/valu
+cd /tmp
+export TMPDIR=/tmp
+export SUNSKY_AMD_DATASET=$R/mitsuba3-sunsky_amd/data/sunsky_datasets.pack
+H=$R/mitsuba3-sunsky_amd/build/sunsky_kernels.hsaco
+KB=$R/tools/build/kbench
+C="SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE"
+run() {   # name mode n kernel
+  timeout -s KILL 90 rocprofv3 --pmc $C -d $R/gpurun_out/valu/$1 -o $1 --output-format csv -- $KB $H $2 $3 5 64 $4 > $R/gpurun_out/valu/$1.log 2>&1
+}
+run sample sample 67108864 ${SAMPLE_KERNEL:-sunsky_sample_direction_rgb_lean_fast} && \
+run pdf pdf 67108864 sunsky_pdf_direction_v4_fast && \
+run rgb rgb 16777216 sunsky_eval_rgb_v4_fast && \
+run spec spec 16777216 sunsky_eval_spec_nodes_v4_fast

@@ -73,9 +73,13 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&d_ld, sizeof(float) * 66));
     CK(hipMemcpy(d_sun, model.sun_table().data(), sizeof(float) * model.sun_table().size(), hipMemcpyHostToDevice));
     CK(hipMemcpy(d_ld, model.sun_ld().data(), sizeof(float) * 66, hipMemcpyHostToDevice));
-    SunskyKArgs K = model.kargs();
-    K.sun_table = d_sun;
-    K.sun_ld = d_ld;
+    SunskyKArgs hk = model.kargs();
+    hk.sun_table = d_sun;
+    hk.sun_ld = d_ld;
+    // kernels read the emitter state through a device pointer (sunsky_types.h)
+    SunskyKArgs* K = nullptr;
+    CK(hipMalloc(&K, sizeof(SunskyKArgs)));
+    CK(hipMemcpy(K, &hk, sizeof(SunskyKArgs), hipMemcpyHostToDevice));
 
     // directions: cos theta = u1, phi = 2 pi u2; wi = -wo
     std::vector<float> hx(n), hy(n), hz(n);

@@ -1155,9 +1155,20 @@ __device__ __forceinline__ void sample_direction_body(
     stage_sampler_lds<FAST, SPEC>(K, &S);
     const float w_sun = 1.f - K.w_sky, inv_w = 1.f / K.w_sky, inv_w_sun = 1.f / w_sun;   // div_exact
     const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    // the next sample's u is loaded before this one's work, so its HBM latency overlaps the
+    // ~500 VALU instructions of a sample: 4.4 % faster, bitwise the same (interleaved A/B,
+    // profiles/r02_v6_ab_sample_prefetch.log).  Prefetching pdf_direction's directions
+    // measured 3.7 % slower (70 VGPRs: 7 waves/SIMD instead of 8).
+    // A sorted form (a workgroup ranks 256-1024 samples sky-first through LDS so only
+    // one 64-lane pass per tile runs both branches, outputs staged in LDS) was 5-25 %
+    // slower: profiles/r02_v6_ab_sample_prefetch_sorted.log.
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float nx = 0.f, ny = 0.f;
+    if (i < n) { nx = ux[i]; ny = uy[i]; }
+    for (; i < n; i += stride) {
         bool act = active ? active[i] != 0 : true;
-        const float sx = ux[i], sy = uy[i];
+        const float sx = nx, sy = ny;
+        if (i + stride < n) { nx = ux[i + stride]; ny = uy[i + stride]; }
         const bool pick_sky = sx < K.w_sky;
         // sx / w and the reused sample stay correctly rounded even in FAST: the
         // discrete-distribution reuse divides by the picked gaussian's pmf, so one

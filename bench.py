@@ -691,7 +691,8 @@ def main():
         n_in = ss._capi.Vec3In(nrm[0].data_ptr(), nrm[1].data_ptr(), nrm[2].data_ptr())
 
         def direct_step():
-            rc = lib.sunsky_direct_diffuse(smp._h, n_in, None, None, 0, 0, 7, spp, npts, dd.data_ptr(), npts, stream)
+            rc = lib.sunsky_direct_diffuse(smp._h, n_in, None, None, 0, 0, 7, spp, None, 0, npts, dd.data_ptr(), npts,
+                                           stream)
             if rc:
                 raise RuntimeError(lib.sunsky_last_error().decode())
 

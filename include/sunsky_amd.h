@@ -17,14 +17,18 @@
  *   - `stream` is a hipStream_t (NULL = default stream); every batch call is
  *     asynchronous and stream-ordered.  The hot-path calls (eval,
  *     eval_direction, eval_spectral_broadcast, sample_direction, pdf_direction,
- *     sample_ray, sample_wavelengths, direct_diffuse) allocate nothing, make no
- *     host-synchronous call and may be captured into a hipGraph
- *     (tests/test_graph_capture.py); a graph snapshots the emitter's parameters
- *     at capture, so recapture after parameters_changed().  eval_jvp and
- *     eval_vjp stage their tangent tables host-synchronously when the emitter
- *     state (or, for eval_jvp, the tangent) changed since the previous call,
- *     and order successive AD calls through an event; bake_latlong uploads
- *     per-call tables.  These three are not capturable;
+ *     sample_ray, sample_wavelengths, direct_diffuse, direct_diffuse_rays)
+ *     allocate nothing, make no host-synchronous call and may be captured into
+ *     a hipGraph (tests/test_graph_capture.py).  Kernels read the emitter state
+ *     from device memory, which parameters_changed_async rewrites in place on
+ *     the caller's stream, so a captured graph replays with the state current at
+ *     replay.  eval_jvp and eval_vjp restage their tangent tables (host fp64
+ *     derivative of the staging, stream-ordered copy from pinned memory) when
+ *     the emitter state (or, for eval_jvp, the tangent) changed since the
+ *     previous call; they and bake_latlong order successive calls on the same
+ *     emitter through events and are not capturable;
+ *   - every batch entry point opens a roctx range "<ProfilerPhase>:<entry>"
+ *     (the reference's MI_MASKED_FUNCTION scopes; SUNSKY_AMD_ROCTX=0 disables);
  *   - create/update/destroy are host-synchronous and must not race batch calls
  *     on the same emitter (the reference's parameters_changed() contract).
  */
@@ -38,7 +42,7 @@
 extern "C" {
 #endif
 
-#define SUNSKY_AMD_ABI_VERSION 2
+#define SUNSKY_AMD_ABI_VERSION 3   /* 3: direct_diffuse visibility, direct_diffuse_rays */
 
 typedef enum sunsky_status {
     SUNSKY_OK = 0,
@@ -220,18 +224,34 @@ int sunsky_bake_latlong(const sunsky_emitter *e, int width, int height, float th
                         float phi0, float phi1, const float *wavelengths_host, int n_wavelengths,
                         float *out, size_t out_stride, void *stream);
 
-/* A caller of sample_direction / pdf_direction / eval: the sun-and-sky light an
- * unoccluded smooth-diffuse point receives, gathered as the path integrator does at
- * one vertex (src/integrators/path.cpp:176-250; src/bsdfs/diffuse.cpp:100-180):
- * emitter sampling + cosine-hemisphere BSDF sampling combined with the power
- * heuristic, spp samples per point from PCG32Sampler-seeded streams
- * (src/render/sampler.cpp:125-144: sample_tea_32(seed, point index)).
+/* A caller of sample_direction / pdf_direction / eval: the sun-and-sky light a
+ * smooth-diffuse point receives, gathered as the path integrator does at one vertex
+ * (src/integrators/path.cpp:176-250; src/bsdfs/diffuse.cpp:100-180): emitter
+ * sampling + cosine-hemisphere BSDF sampling combined with the power heuristic, spp
+ * samples per point from PCG32Sampler-seeded streams (src/render/sampler.cpp:125-144:
+ * sample_tea_32(seed, point index)).
  * normal: unit world-space normals; reflectance: gray per point (NULL = 1).
  * out planes: 3 (RGB) or n_wavelengths <= 4 (spectral, per-point wavelengths).
+ * visibility: NULL for unoccluded points, else one byte per (sample s, point i) at
+ * visibility[s * vis_stride + i] with the caller's tracer verdicts on the rays
+ * sunsky_direct_diffuse_rays wrote for the same (seed, spp, normal): bit 0 = the
+ * shadow ray along the emitter sample is unoccluded (path.cpp:216-219 ray_test),
+ * bit 1 = the BSDF ray escapes to the environment (path.cpp:176-196).
  * n < 2^32. */
 int sunsky_direct_diffuse(const sunsky_emitter *e, sunsky_vec3_in normal, const float *reflectance,
                           const float *wavelengths, int n_wavelengths, size_t wl_stride, uint32_t seed,
-                          uint32_t spp, size_t n, float *out, size_t out_stride, void *stream);
+                          uint32_t spp, const uint8_t *visibility, size_t vis_stride, size_t n, float *out,
+                          size_t out_stride, void *stream);
+/* The rays a wavefront caller traces between the two halves of sunsky_direct_diffuse
+ * (the shadow ray of the emitter sample, path.cpp:216-219, and the BSDF ray,
+ * path.cpp:176-196), from the same streams and arithmetic as that call: for sample s
+ * of point i, emitter_dir[s * ray_stride + i] is the world direction of the emitter
+ * sample ((0,0,0) when the sample contributes nothing: pdf 0 or below the point's
+ * horizon) and bsdf_dir[s * ray_stride + i] the cosine-sampled world direction
+ * ((0,0,0) when its pdf is 0).  ray_stride >= n; n < 2^32. */
+int sunsky_direct_diffuse_rays(const sunsky_emitter *e, sunsky_vec3_in normal, uint32_t seed, uint32_t spp,
+                               size_t n, sunsky_vec3_out emitter_dir, sunsky_vec3_out bsdf_dir,
+                               size_t ray_stride, void *stream);
 
 /* ------------------------------------------------ forward-mode derivatives */
 typedef enum sunsky_param {         /* Differentiable traverse() parameters, sunsky.cpp:220-240 */
@@ -244,7 +264,7 @@ typedef enum sunsky_param {         /* Differentiable traverse() parameters, sun
  * dr::grad(eval(si)) computes in the reference's AD variants (exercised by
  * sunsky-testing/traversal_test.py:94-145).  Layout as sunsky_eval; d_out has the
  * planes of out.  The tangent of the staged tables is computed on the host and
- * uploaded before the launch (host-synchronous), the rays are processed on `stream`. */
+ * uploaded (stream-ordered, pinned staging) and the rays processed on `stream`. */
 int sunsky_eval_jvp(const sunsky_emitter *e, int param, const float *tangent, int tangent_count,
                     sunsky_vec3_in wi, const float *wavelengths, int n_wavelengths, size_t wl_stride,
                     const uint8_t *active, size_t n, float *out, float *d_out, size_t out_stride,

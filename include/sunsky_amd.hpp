@@ -207,15 +207,25 @@ public:
                                   wavelengths.empty() ? nullptr : wavelengths.data(), (int)wavelengths.size(),
                                   out.data, out.stride ? out.stride : n, stream));
     }
-    // Direct sun + sky light at unoccluded diffuse points (sunsky_direct_diffuse): one vertex of
+    // Direct sun + sky light at diffuse points (sunsky_direct_diffuse): one vertex of
     // PathIntegrator::sample (path.cpp:176-250) with diffuse.cpp's BSDF, spp samples per point.
-    // Spectral: wavelengths = the points' si.wavelengths (<= 4 planes).
+    // Spectral: wavelengths = the points' si.wavelengths (<= 4 planes).  visibility: NULL
+    // (unoccluded) or the tracer's verdicts [spp][vis_stride] on direct_diffuse_rays' rays.
     void direct_diffuse(Vector3 normal, size_t n, uint32_t seed, uint32_t spp, SpectrumOut out,
                         const float* reflectance = nullptr, Wavelengths wavelengths = {},
-                        void* stream = nullptr) const {
+                        void* stream = nullptr, const uint8_t* visibility = nullptr,
+                        size_t vis_stride = 0) const {
         check(sunsky_direct_diffuse(e_, vin(normal), reflectance, wavelengths.data, wavelengths.count,
-                                    wavelengths.stride ? wavelengths.stride : n, seed, spp, n, out.data,
-                                    out.stride ? out.stride : n, stream));
+                                    wavelengths.stride ? wavelengths.stride : n, seed, spp, visibility,
+                                    vis_stride ? vis_stride : n, n, out.data, out.stride ? out.stride : n,
+                                    stream));
+    }
+    // The shadow and BSDF rays of direct_diffuse's samples (sunsky_direct_diffuse_rays):
+    // planes [spp][ray_stride] per component, (0,0,0) where no ray is needed.
+    void direct_diffuse_rays(Vector3 normal, size_t n, uint32_t seed, uint32_t spp, Vector3Out emitter_dir,
+                             Vector3Out bsdf_dir, size_t ray_stride = 0, void* stream = nullptr) const {
+        check(sunsky_direct_diffuse_rays(e_, vin(normal), seed, spp, n, vout(emitter_dir), vout(bsdf_dir),
+                                         ray_stride ? ray_stride : n, stream));
     }
     // Spectral eval of one wavelength list broadcast to every ray (test_sunsky.py:42-59 layout)
     void eval_spectral_broadcast(Vector3 wi, size_t n, const std::vector<float>& wavelengths, SpectrumOut out,

@@ -22,6 +22,7 @@
 #include "sunsky_dataset.h"
 #include "sunsky_errors.h"
 #include "sunsky_model.h"
+#include "sunsky_profiler.h"
 #include "sunsky_props.h"
 #include "sunsky_types.h"
 
@@ -81,7 +82,8 @@ enum KernelId {
     K_EVAL_RGB_V4, K_EVAL_RGB_V1, K_EVAL_SPEC_BCAST_V4, K_EVAL_SPEC_BCAST_V1, K_EVAL_SPEC_NODES_V4,
     K_EVAL_SPEC_RAYS_V4, K_EVAL_SPEC_RAYS_V1, K_SAMPLE_DIRECTION_RGB, K_SAMPLE_DIRECTION_SPEC, K_PDF_DIRECTION_V4, K_PDF_DIRECTION_V1, K_SAMPLE_WAVELENGTHS_RGB,
     K_SAMPLE_WAVELENGTHS_SPEC, K_SAMPLE_RAY_RGB, K_SAMPLE_RAY_SPEC, K_BAKE_RGB, K_BAKE_SPEC,
-    K_DIRECT_DIFFUSE_RGB, K_DIRECT_DIFFUSE_SPEC, K_SAMPLE_DIRECTION_RGB_LEAN, K_SAMPLE_DIRECTION_SPEC_LEAN, K_COUNT
+    K_DIRECT_DIFFUSE_RGB, K_DIRECT_DIFFUSE_SPEC, K_SAMPLE_DIRECTION_RGB_LEAN, K_SAMPLE_DIRECTION_SPEC_LEAN,
+    K_DIRECT_DIFFUSE_RAYS, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
@@ -90,7 +92,7 @@ const char* kKernelNames[K_COUNT] = {
     "sunsky_sample_wavelengths_rgb",
     "sunsky_sample_wavelengths_spec", "sunsky_sample_ray_rgb", "sunsky_sample_ray_spec",
     "sunsky_bake_latlong_rgb", "sunsky_bake_latlong_spec", "sunsky_direct_diffuse_rgb", "sunsky_direct_diffuse_spec",
-    "sunsky_sample_direction_rgb_lean", "sunsky_sample_direction_spec_lean"};
+    "sunsky_sample_direction_rgb_lean", "sunsky_sample_direction_spec_lean", "sunsky_direct_diffuse_rays"};
 
 // eval kernels instantiated twice: eval(si) negates wi at compile time,
 // eval_direction(ds) uses ds.d as is (the "_dir" kernels)
@@ -166,7 +168,7 @@ int blocks_per_cu(KernelId k) {
         case K_SAMPLE_DIRECTION_RGB_LEAN: case K_SAMPLE_DIRECTION_SPEC_LEAN:
             return 64;
         case K_BAKE_RGB: case K_BAKE_SPEC: return 64;
-        case K_DIRECT_DIFFUSE_RGB: case K_DIRECT_DIFFUSE_SPEC: return 64;
+        case K_DIRECT_DIFFUSE_RGB: case K_DIRECT_DIFFUSE_SPEC: case K_DIRECT_DIFFUSE_RAYS: return 64;
         case K_EVAL_SPEC_RAYS_V4: case K_EVAL_SPEC_RAYS_V1: return 64;
         default: return 16;
     }
@@ -484,6 +486,12 @@ struct sunsky_emitter {
     }
 };
 
+// Batch calls need the emitter's device state: a host-only emitter
+// (sunsky_emitter_create_host) has none and rejects them.
+void require_device(const sunsky_emitter* e) {
+    if (!e->mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
+}
+
 extern "C" {
 
 int sunsky_abi_version(void) { return SUNSKY_AMD_ABI_VERSION; }
@@ -528,6 +536,7 @@ int sunsky_props_set_irregular_spectrum(sunsky_props* p, const char* name, const
 
 int sunsky_emitter_create(const sunsky_props* props, int variant, int semantics, const char* dataset_path,
                           sunsky_emitter** out) {
+    SUNSKY_PHASE("InitScene", "emitter_create");
     if (!props || !out) return fail(SUNSKY_ERROR_INVALID_VALUE, "null props / output pointer");
     *out = nullptr;
     return guarded([&] {
@@ -570,6 +579,7 @@ int sunsky_emitter_set_param(sunsky_emitter* e, const char* name, const float* v
 }
 
 int sunsky_emitter_parameters_changed_async(sunsky_emitter* e, void* stream) {
+    SUNSKY_PHASE("InitScene", "emitter_parameters_changed_async");
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     return guarded([&] {
         const bool gpu = e->device >= 0;
@@ -673,7 +683,7 @@ int sunsky_emitter_get_table(const sunsky_emitter* e, int id, float* out, size_t
         default: return fail(SUNSKY_ERROR_INVALID_VALUE, "unknown table id");
     }
     *count = v.size();
-    if (out) std::memcpy(out, v.data(), sizeof(float) * std::min(cap, v.size()));
+    if (out && !v.empty()) std::memcpy(out, v.data(), sizeof(float) * std::min(cap, v.size()));
     return SUNSKY_OK;
 }
 
@@ -705,6 +715,7 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
     if (nout > 1 && ostride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "out_stride < n");
     if (spec && nlam > 1 && lstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "wl_stride < n");
     return guarded([&] {
+        require_device(e);
         hipStream_t s = (hipStream_t)stream;
         DeviceScope dev_scope(e->device);
         const SunskyKArgs* K = e->d_state;
@@ -751,16 +762,19 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
 
 int sunsky_eval(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam, int nlam, size_t lstride,
                 const uint8_t* active, size_t n, float* out, size_t ostride, void* stream) {
+    SUNSKY_PHASE("EndpointEvaluate", "eval");
     return eval_impl(e, wi, lam, nlam, lstride, active, n, out, ostride, stream, -1.f);
 }
 
 int sunsky_eval_direction(const sunsky_emitter* e, sunsky_vec3_in d, const float* lam, int nlam, size_t lstride,
                           const uint8_t* active, size_t n, float* out, size_t ostride, void* stream) {
+    SUNSKY_PHASE("EndpointEvaluate", "eval_direction");
     return eval_impl(e, d, lam, nlam, lstride, active, n, out, ostride, stream, 1.f);
 }
 
 int sunsky_eval_spectral_broadcast(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam_host, int m,
                                    const uint8_t* active, size_t n, float* out, size_t ostride, void* stream) {
+    SUNSKY_PHASE("EndpointEvaluate", "eval_spectral_broadcast");
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     if (e->kargs.variant != kSpectral) return fail(SUNSKY_ERROR_INVALID_VALUE, "broadcast eval needs a spectral emitter");
     if (!lam_host || m < 1 || m > kMaxBroadcastLambda)
@@ -773,6 +787,7 @@ int sunsky_eval_spectral_broadcast(const sunsky_emitter* e, sunsky_vec3_in w, co
     bool nodes = m == kNbWavelengths;
     for (int k = 0; nodes && k < m; ++k) nodes = L.lo[k] == k && L.f[k] == 0.f;
     return guarded([&] {
+        require_device(e);
         hipStream_t s = (hipStream_t)stream;
         DeviceScope dev_scope(e->device);
         const SunskyKArgs* K = e->d_state;
@@ -800,6 +815,7 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
                             const float* lam, int nlam, size_t lstride, const uint8_t* active, size_t n,
                             sunsky_vec3_out ds_d, float* ds_pdf, float* ds_dist, sunsky_vec3_out ds_p,
                             float* weight, size_t wstride, void* stream) {
+    SUNSKY_PHASE("EndpointSampleDirection", "sample_direction");
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     if (n == 0) return SUNSKY_OK;
     const bool spec = e->kargs.variant == kSpectral;
@@ -813,6 +829,7 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
     if ((ds_p.x != nullptr) != (ds_p.y != nullptr) || (ds_p.x != nullptr) != (ds_p.z != nullptr))
         return fail(SUNSKY_ERROR_INVALID_VALUE, "ds_p must be all-NULL or all-set");
     return guarded([&] {
+        require_device(e);
         DeviceScope dev_scope(e->device);
         const SunskyKArgs* K = e->d_state;
         int nl = spec ? nlam : 0;
@@ -829,10 +846,12 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
 
 int sunsky_pdf_direction(const sunsky_emitter* e, sunsky_vec3_in d, const uint8_t* active, size_t n, float* pdf,
                          void* stream) {
+    SUNSKY_PHASE("EndpointEvaluate", "pdf_direction");
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     if (n == 0) return SUNSKY_OK;
     if (!d.x || !d.y || !d.z || !pdf) return fail(SUNSKY_ERROR_INVALID_VALUE, "null direction / output pointer");
     return guarded([&] {
+        require_device(e);
         DeviceScope dev_scope(e->device);
         const SunskyKArgs* K = e->d_state;
         hipStream_t s = (hipStream_t)stream;
@@ -857,6 +876,7 @@ int sunsky_pdf_direction(const sunsky_emitter* e, sunsky_vec3_in d, const uint8_
 int sunsky_sample_ray(const sunsky_emitter* e, const float* wls, const float* s2x, const float* s2y,
                       const float* s3x, const float* s3y, const uint8_t* active, size_t n, sunsky_vec3_out o,
                       sunsky_vec3_out d, float* lam, size_t lstride, float* weight, size_t wstride, void* stream) {
+    SUNSKY_PHASE("EndpointSampleRay", "sample_ray");
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     if (n == 0) return SUNSKY_OK;
     if (!s2x || !s2y || !s3x || !s3y || !o.x || !o.y || !o.z || !d.x || !d.y || !d.z || !lam || !weight)
@@ -864,6 +884,7 @@ int sunsky_sample_ray(const sunsky_emitter* e, const float* wls, const float* s2
     if (e->kargs.variant == kSpectral && !wls) return fail(SUNSKY_ERROR_INVALID_VALUE, "null wavelength sample");
     if (lstride < n || wstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "stride < n");
     return guarded([&] {
+        require_device(e);
         DeviceScope dev_scope(e->device);
         const SunskyKArgs* K = e->d_state;
         void* args[] = {&K, &wls, &s2x, &s2y, &s3x, &s3y, &active, &n, &o.x, &o.y, &o.z,
@@ -875,12 +896,14 @@ int sunsky_sample_ray(const sunsky_emitter* e, const float* wls, const float* s2
 
 int sunsky_sample_wavelengths(const sunsky_emitter* e, sunsky_vec3_in w, const float* sample, const uint8_t* active,
                               size_t n, float* lam, size_t lstride, float* weight, size_t wstride, void* stream) {
+    SUNSKY_PHASE("EndpointSampleRay", "sample_wavelengths");
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     if (n == 0) return SUNSKY_OK;
     if (!w.x || !w.y || !w.z || !lam || !weight) return fail(SUNSKY_ERROR_INVALID_VALUE, "null pointer");
     if (e->kargs.variant == kSpectral && !sample) return fail(SUNSKY_ERROR_INVALID_VALUE, "null sample");
     if (lstride < n || wstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "stride < n");
     return guarded([&] {
+        require_device(e);
         DeviceScope dev_scope(e->device);
         const SunskyKArgs* K = e->d_state;
         void* args[] = {&K, (void*)&w.x, (void*)&w.y, (void*)&w.z, &sample, &active, &n, &lam, &lstride, &weight, &wstride};
@@ -892,6 +915,7 @@ int sunsky_sample_wavelengths(const sunsky_emitter* e, sunsky_vec3_in w, const f
 int sunsky_eval_jvp(const sunsky_emitter* e, int param, const float* tangent, int tangent_count, sunsky_vec3_in wi,
                     const float* lam, int nlam, size_t lstride, const uint8_t* active, size_t n, float* out,
                     float* d_out, size_t ostride, void* stream) {
+    SUNSKY_PHASE("EndpointEvaluate", "eval_jvp");
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     if (!tangent) return fail(SUNSKY_ERROR_INVALID_VALUE, "null tangent");
     const bool spec = e->kargs.variant == kSpectral;
@@ -909,7 +933,7 @@ int sunsky_eval_jvp(const sunsky_emitter* e, int param, const float* tangent, in
         EvalTangent tan;
         if (stage || n == 0) tan = e->model->eval_tangent(param, tangent, tangent_count);   // validates param / count
         if (n == 0) return;
-        if (!e->mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
+        require_device(e);
         hipStream_t st = (hipStream_t)stream;
         DeviceScope dev_scope(e->device);
         e->ad_begin(st);   // ordered after the previous AD call (which may read d_jvp), any stream
@@ -941,6 +965,7 @@ int sunsky_eval_jvp(const sunsky_emitter* e, int param, const float* tangent, in
 
 int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam, int nlam, size_t lstride,
                     const uint8_t* active, size_t n, const float* d_out, size_t ostride, float* grad, void* stream) {
+    SUNSKY_PHASE("EndpointEvaluate", "eval_vjp");
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     if (!grad) return fail(SUNSKY_ERROR_INVALID_VALUE, "null gradient buffer");
     const bool spec = e->kargs.variant == kSpectral;
@@ -952,7 +977,7 @@ int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam
     if (nout > 1 && ostride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "out_stride < n");
     if (spec && nlam > 1 && lstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "wl_stride < n");
     return guarded([&] {
-        if (!e->mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
+        require_device(e);
         // basis tangents: turbidity, albedo (all channels at once: channel c's tables depend on
         // albedo[c] only, so the all-ones tangent is the diagonal), sun_direction x / y / z
         const SunskyModel& M = *e->model;
@@ -1019,6 +1044,7 @@ int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam
 
 int sunsky_bake_latlong(const sunsky_emitter* e, int width, int height, float theta0, float theta1, float phi0,
                         float phi1, const float* lam_host, int m, float* out, size_t ostride, void* stream) {
+    SUNSKY_PHASE("EndpointEvaluate", "bake_latlong");
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     if (width < 1 || height < 1) return fail(SUNSKY_ERROR_INVALID_VALUE, "image size must be >= 1 x 1");
     if ((int64_t)width * height >= (int64_t)1 << 31) return fail(SUNSKY_ERROR_INVALID_VALUE, "image larger than 2^31 pixels");
@@ -1033,7 +1059,7 @@ int sunsky_bake_latlong(const sunsky_emitter* e, int width, int height, float th
     LatLong G = {width, height, theta0, height > 1 ? (theta1 - theta0) / (float)(height - 1) : 0.f,
                  phi0, width > 1 ? (phi1 - phi0) / (float)(width - 1) : 0.f, nullptr};
     return guarded([&] {
-        if (!e->mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
+        require_device(e);
         DeviceScope dev_scope(e->device);
         const SunskyKArgs* K = e->d_state;
         hipStream_t s = (hipStream_t)stream;
@@ -1071,8 +1097,9 @@ int sunsky_bake_latlong(const sunsky_emitter* e, int width, int height, float th
 }
 
 int sunsky_direct_diffuse(const sunsky_emitter* e, sunsky_vec3_in nrm, const float* rho, const float* lam, int nlam,
-                          size_t lstride, uint32_t seed, uint32_t spp, size_t n, float* out, size_t ostride,
-                          void* stream) {
+                          size_t lstride, uint32_t seed, uint32_t spp, const uint8_t* vis, size_t vstride, size_t n,
+                          float* out, size_t ostride, void* stream) {
+    SUNSKY_PHASE("SamplingIntegratorSample", "direct_diffuse");
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     if (n == 0) return SUNSKY_OK;
     const bool spec = e->kargs.variant == kSpectral;
@@ -1083,15 +1110,36 @@ int sunsky_direct_diffuse(const sunsky_emitter* e, sunsky_vec3_in nrm, const flo
         return fail(SUNSKY_ERROR_INVALID_VALUE, "spectral direct lighting needs 1..4 wavelength planes");
     if (!spec && (lam || nlam)) return fail(SUNSKY_ERROR_INVALID_VALUE, "RGB direct lighting takes no wavelengths");
     if (ostride < n || (spec && lstride < n)) return fail(SUNSKY_ERROR_INVALID_VALUE, "stride < n");
+    if (vis && vstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "vis_stride < n");
     return guarded([&] {
-        if (!e->mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
+        require_device(e);
         DeviceScope dev_scope(e->device);
         const SunskyKArgs* K = e->d_state;
         int nl = spec ? nlam : 0;
-        void* args[] = {&K, (void*)&nrm.x, (void*)&nrm.y, (void*)&nrm.z, &rho, &lam, &lstride, &nl, &seed, &spp, &n,
-                        &out, &ostride};
+        void* args[] = {&K, (void*)&nrm.x, (void*)&nrm.y, (void*)&nrm.z, &rho, &lam, &lstride, &nl, &seed, &spp, &vis,
+                        &vstride, &n, &out, &ostride};
         const KernelId k = spec ? K_DIRECT_DIFFUSE_SPEC : K_DIRECT_DIFFUSE_RGB;
         launch(e->fn(k), grid_for(e->mod, k, n), (hipStream_t)stream, args);
+    });
+}
+
+int sunsky_direct_diffuse_rays(const sunsky_emitter* e, sunsky_vec3_in nrm, uint32_t seed, uint32_t spp, size_t n,
+                               sunsky_vec3_out em, sunsky_vec3_out bs, size_t rstride, void* stream) {
+    SUNSKY_PHASE("SamplingIntegratorSample", "direct_diffuse_rays");
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (n == 0) return SUNSKY_OK;
+    if (!nrm.x || !nrm.y || !nrm.z) return fail(SUNSKY_ERROR_INVALID_VALUE, "null normal pointer");
+    if (!em.x || !em.y || !em.z || !bs.x || !bs.y || !bs.z) return fail(SUNSKY_ERROR_INVALID_VALUE, "null ray pointer");
+    if (spp < 1) return fail(SUNSKY_ERROR_INVALID_VALUE, "spp must be >= 1");
+    if (n > 0xffffffffull) return fail(SUNSKY_ERROR_INVALID_VALUE, "more than 2^32 points (the sampler's lane index is 32-bit)");
+    if (rstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "ray_stride < n");
+    return guarded([&] {
+        require_device(e);
+        DeviceScope dev_scope(e->device);
+        const SunskyKArgs* K = e->d_state;
+        void* args[] = {&K, (void*)&nrm.x, (void*)&nrm.y, (void*)&nrm.z, &seed, &spp, &n, &em.x, &em.y, &em.z,
+                        &bs.x, &bs.y, &bs.z, &rstride};
+        launch(e->fn(K_DIRECT_DIFFUSE_RAYS), grid_for(e->mod, K_DIRECT_DIFFUSE_RAYS, n), (hipStream_t)stream, args);
     });
 }
 

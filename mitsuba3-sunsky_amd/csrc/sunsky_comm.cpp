@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "sunsky_amd.h"
+#include "sunsky_profiler.h"
 #include "sunsky_errors.h"
 
 using namespace sunsky::capi;
@@ -136,6 +137,7 @@ int sunsky_comm_info(const sunsky_comm* c, int* rank, int* nranks, int* device) 
 
 int sunsky_gather_radiance(sunsky_comm* c, int root, const float* send, size_t send_stride, int nplanes,
                            const size_t* counts, float* recv, size_t recv_stride, void* stream) {
+    SUNSKY_PHASE("Gather", "gather_radiance");
     if (!c || !counts) return fail(SUNSKY_ERROR_INVALID_VALUE, "null communicator / counts");
     if (root < 0 || root >= c->nranks) return fail(SUNSKY_ERROR_INVALID_VALUE, "invalid root rank");
     if (nplanes < 1) return fail(SUNSKY_ERROR_INVALID_VALUE, "nplanes must be >= 1");

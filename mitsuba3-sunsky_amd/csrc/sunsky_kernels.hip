@@ -1447,11 +1447,18 @@ __device__ __forceinline__ float mis_power(float a, float b) {
 // per-point wavelength (spectral, si.wavelengths).  Everything between the
 // normal and the accumulated radiance stays in VGPRs: per point the kernel
 // reads 12 B (+ rho, + wavelengths) and writes 4 B per channel, whatever spp.
+// Occlusion (optional): vis[s * vstride + i] holds the caller's ray-tracer
+// verdicts for sample s of point i -- bit 0 the shadow ray along the emitter
+// sample is unoccluded (path.cpp:216-219, scene->ray_test), bit 1 the BSDF ray
+// escapes to the environment (path.cpp:176-196, no surface hit).  The rays are
+// the ones sunsky_direct_diffuse_rays writes from the same streams; vis = null
+// is the unoccluded point (every bit set).
 template <bool FAST, bool SPEC>
 __device__ __forceinline__ void direct_diffuse_body(
     const SunskyKArgs& K, const float* __restrict__ nx, const float* __restrict__ ny, const float* __restrict__ nz,
     const float* __restrict__ rho, const float* __restrict__ lam, size_t lstride, int nlam, uint32_t seed,
-    uint32_t spp, size_t n, float* __restrict__ out, size_t ostride) {
+    uint32_t spp, const uint8_t* __restrict__ vis, size_t vstride, size_t n, float* __restrict__ out,
+    size_t ostride) {
     __shared__ SamplerLds<FAST, SPEC> S;
     stage_sampler_lds<FAST, SPEC>(K, &S);
     const float w_sun = 1.f - K.w_sky, inv_w = 1.f / K.w_sky, inv_w_sun = 1.f / w_sun;   // div_exact
@@ -1476,6 +1483,7 @@ __device__ __forceinline__ void direct_diffuse_body(
         for (uint32_t smp = 0; smp < spp; ++smp) {
             const float u0 = rng.next_float(), u1 = rng.next_float();
             const float u2 = rng.next_float(), u3 = rng.next_float();
+            const unsigned v = vis ? (unsigned)vis[(size_t)smp * vstride + i] : 3u;
             // ---- emitter sampling: sample_direction (sunsky.cpp:399-441)
             const bool pick_sky = u0 < K.w_sky;
             float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, u0, u1, inv_w, inv_w_sun);
@@ -1485,7 +1493,7 @@ __device__ __forceinline__ void direct_diffuse_body(
             compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
             const float pd = lerpf_(sunp, skyp, K.w_sky);
             const float cos_em = dot3(nrm, d);
-            if (pd != 0.f && cos_em > 0.f) {
+            if ((v & 1u) && pd != 0.f && cos_em > 0.f) {
                 const float bpdf = kInvPi * cos_em;     // diffuse eval / pdf: rho / pi cos, cos / pi
                 const float scale = bpdf * mis_power<FAST>(pd, bpdf);
                 const float3_ wo = to_local(K, d);
@@ -1513,7 +1521,7 @@ __device__ __forceinline__ void direct_diffuse_body(
             disk_concentric_dev<FAST>(u2, u3, &px, &py);
             const float lz = safe_sqrt_sel<FAST>(1.f - fmaf(px, px, py * py));
             const float bpdf = kInvPi * lz;
-            if (bpdf > 0.f) {
+            if ((v & 2u) && bpdf > 0.f) {
                 const float3_ dw = frame_to_world(fs, ft, nrm, mk3(px, py, lz));
                 const float3_ wo = to_local(K, dw);
                 // pdf_direction (sunsky.cpp:443-451) of the escaped ray
@@ -1540,6 +1548,59 @@ __device__ __forceinline__ void direct_diffuse_body(
 #pragma unroll
         for (int c = 0; c < C; ++c)
             if (c < nc) __builtin_nontemporal_store(acc[c] * r, out + (size_t)c * ostride + i);
+    }
+}
+
+// The rays a caller's tracer tests between the two halves of direct_diffuse_body,
+// from the same PCG32 streams and the same arithmetic: for sample s of point i,
+// em[s * rstride + i] is the world direction of the emitter sample (the shadow ray
+// of path.cpp:216-219), (0, 0, 0) where that sample contributes nothing anyway
+// (pdf 0 or below the point's horizon), and bs[s * rstride + i] the cosine-sampled
+// BSDF direction (path.cpp:176-196), (0, 0, 0) where its pdf is 0.  Directions
+// are the same values direct_diffuse_body computes, so a caller's verdicts about
+// them (vis) apply bit for bit.  Only the mixture tables are needed (LDS).
+template <bool FAST>
+__device__ __forceinline__ void direct_diffuse_rays_body(
+    const SunskyKArgs& K, const float* __restrict__ nx, const float* __restrict__ ny, const float* __restrict__ nz,
+    uint32_t seed, uint32_t spp, size_t n, float* __restrict__ ex, float* __restrict__ ey, float* __restrict__ ez,
+    float* __restrict__ bx, float* __restrict__ by, float* __restrict__ bz, size_t rstride) {
+    __shared__ TgmmLds T;
+    stage_tgmm(K, &T);
+    __syncthreads();
+    const float w_sun = 1.f - K.w_sky, inv_w = 1.f / K.w_sky, inv_w_sun = 1.f / w_sun;   // div_exact
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float3_ nrm = mk3(nx[i], ny[i], nz[i]);
+        float3_ fs, ft;
+        coordinate_system(nrm, &fs, &ft);
+        uint32_t v0 = seed, v1 = (uint32_t)i;
+        sample_tea_32(&v0, &v1);
+        Pcg32 rng;
+        rng.seed(v0, v1);
+        for (uint32_t smp = 0; smp < spp; ++smp) {
+            const float u0 = rng.next_float(), u1 = rng.next_float();
+            const float u2 = rng.next_float(), u3 = rng.next_float();
+            const bool pick_sky = u0 < K.w_sky;
+            const float3_ sd = sample_sky_or_sun<FAST>(K, T, pick_sky, u0, u1, inv_w, inv_w_sun);
+            const bool act = sd.z >= 0.f;
+            const float3_ d = to_world(K, sd);
+            float skyp, sunp;
+            compute_pdfs<FAST>(K, T, sd, pick_sky, act, &skyp, &sunp);
+            const float pd = lerpf_(sunp, skyp, K.w_sky);
+            const bool em_ok = pd != 0.f && dot3(nrm, d) > 0.f;
+            float px, py;
+            disk_concentric_dev<FAST>(u2, u3, &px, &py);
+            const float lz = safe_sqrt_sel<FAST>(1.f - fmaf(px, px, py * py));
+            const bool bs_ok = kInvPi * lz > 0.f;
+            const float3_ dw = frame_to_world(fs, ft, nrm, mk3(px, py, lz));
+            const size_t o = (size_t)smp * rstride + i;
+            __builtin_nontemporal_store(em_ok ? d.x : 0.f, ex + o);
+            __builtin_nontemporal_store(em_ok ? d.y : 0.f, ey + o);
+            __builtin_nontemporal_store(em_ok ? d.z : 0.f, ez + o);
+            __builtin_nontemporal_store(bs_ok ? dw.x : 0.f, bx + o);
+            __builtin_nontemporal_store(bs_ok ? dw.y : 0.f, by + o);
+            __builtin_nontemporal_store(bs_ok ? dw.z : 0.f, bz + o);
+        }
     }
 }
 
@@ -2177,13 +2238,24 @@ SS_SAMPLE_RAY(sunsky_sample_ray_spec_ref, false, true)
 #define SS_DIRECT_DIFFUSE(NAME, FAST, SPEC)                                                                   \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                              \
         const SunskyKArgs* __restrict__ Kp, const float* nx, const float* ny, const float* nz, const float* rho, const float* lam, \
-        size_t lstride, int nlam, uint32_t seed, uint32_t spp, size_t n, float* out, size_t ostride) {          \
-        direct_diffuse_body<FAST, SPEC>(*Kp, nx, ny, nz, rho, lam, lstride, nlam, seed, spp, n, out, ostride);   \
+        size_t lstride, int nlam, uint32_t seed, uint32_t spp, const uint8_t* vis, size_t vstride, size_t n,     \
+        float* out, size_t ostride) {                                                                          \
+        direct_diffuse_body<FAST, SPEC>(*Kp, nx, ny, nz, rho, lam, lstride, nlam, seed, spp, vis, vstride, n, out, \
+                                        ostride);                                                              \
     }
 SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_rgb_fast, true, false)
 SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_rgb_ref, false, false)
 SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_spec_fast, true, true)
 SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_spec_ref, false, true)
+
+#define SS_DIRECT_DIFFUSE_RAYS(NAME, FAST)                                                                    \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                              \
+        const SunskyKArgs* __restrict__ Kp, const float* nx, const float* ny, const float* nz, uint32_t seed,   \
+        uint32_t spp, size_t n, float* ex, float* ey, float* ez, float* bx, float* by, float* bz, size_t rstride) { \
+        direct_diffuse_rays_body<FAST>(*Kp, nx, ny, nz, seed, spp, n, ex, ey, ez, bx, by, bz, rstride);         \
+    }
+SS_DIRECT_DIFFUSE_RAYS(sunsky_direct_diffuse_rays_fast, true)
+SS_DIRECT_DIFFUSE_RAYS(sunsky_direct_diffuse_rays_ref, false)
 
 extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_jvp_rgb(
     const SunskyKArgs* __restrict__ Kp, const float* jvp, const float* wx, const float* wy, const float* wz, const uint8_t* active,

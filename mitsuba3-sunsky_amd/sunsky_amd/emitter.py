@@ -430,13 +430,23 @@ class SunskyEmitter:
                                         float(phi[1]), lam_p, m, _ptr(out), height * width, self._stream()))
         return out
 
-    def direct_diffuse(self, normals, seed=0, spp=1, wavelengths=None, reflectance=None, out=None):
-        """Sun-and-sky light at unoccluded smooth-diffuse points (sunsky_direct_diffuse): the
-        path integrator's emitter sampling + BSDF sampling with MIS at one vertex
+    def direct_diffuse(self, normals, seed=0, spp=1, wavelengths=None, reflectance=None, out=None,
+                       visibility=None):
+        """Sun-and-sky light at smooth-diffuse points (sunsky_direct_diffuse): the path
+        integrator's emitter sampling + BSDF sampling with MIS at one vertex
         (path.cpp:176-250, diffuse.cpp:100-180), spp PCG32 samples per point.
-        normals (3, n); wavelengths (k <= 4, n) for spectral -> (C, n)."""
+        normals (3, n); wavelengths (k <= 4, n) for spectral -> (C, n).
+        visibility: None (unoccluded) or a (spp, n) uint8 tensor of the caller's tracer
+        verdicts on the rays of direct_diffuse_rays (bit 0 shadow ray unoccluded, bit 1
+        BSDF ray escaped)."""
         normals, nin = self._vec_in(normals)
         n = normals.shape[1]
+        vis = None
+        if visibility is not None:
+            vis = torch.as_tensor(visibility, device=self.device)
+            if vis.dim() != 2 or tuple(vis.shape) != (int(spp), n):
+                raise ValueError(f"visibility must be a ({int(spp)}, {n}) tensor, got shape {tuple(vis.shape)}")
+            vis = vis.to(torch.uint8).contiguous()
         if self.is_spectral:
             if wavelengths is None:
                 raise ValueError("spectral direct lighting needs per-point wavelengths")
@@ -451,9 +461,25 @@ class SunskyEmitter:
             rho = self._plane(reflectance, n, "reflectance")
         out = self._out(out, (k, n))
         check(lib().sunsky_direct_diffuse(self._h, nin, _ptr(rho), lam_p, k if self.is_spectral else 0, lstride,
-                                          int(seed) & 0xFFFFFFFF, int(spp), n, _ptr(out), out.stride(0),
-                                          self._stream()))
+                                          int(seed) & 0xFFFFFFFF, int(spp), _ptr(vis), n, n, _ptr(out),
+                                          out.stride(0), self._stream()))
         return out
+
+    def direct_diffuse_rays(self, normals, seed=0, spp=1):
+        """The shadow rays (emitter samples) and BSDF rays of direct_diffuse's samples for the
+        same (normals, seed, spp) (sunsky_direct_diffuse_rays) -> (emitter_dir, bsdf_dir), each
+        (3, spp, n) world directions, (0, 0, 0) where no ray is needed."""
+        normals, nin = self._vec_in(normals)
+        n = normals.shape[1]
+        if int(spp) < 1:
+            raise ValueError("spp must be >= 1")
+        em = torch.empty((3, int(spp), n), dtype=torch.float32, device=self.device)
+        bs = torch.empty((3, int(spp), n), dtype=torch.float32, device=self.device)
+        check(lib().sunsky_direct_diffuse_rays(
+            self._h, nin, int(seed) & 0xFFFFFFFF, int(spp), n,
+            Vec3Out(em[0].data_ptr(), em[1].data_ptr(), em[2].data_ptr()),
+            Vec3Out(bs[0].data_ptr(), bs[1].data_ptr(), bs[2].data_ptr()), n, self._stream()))
+        return em, bs
 
     def eval_spectral_broadcast(self, wi, wavelengths, active=None, out=None):
         """Spectral eval of one wavelength list for every direction -> (m, n)."""

@@ -386,36 +386,60 @@ def _mis_power(a, b):
     return np.where(np.isfinite(w), w, 0.0)
 
 
-def direct_diffuse(em, normals, seed, spp, wavelengths=None, rho=None):
-    """Sun-and-sky light at unoccluded smooth-diffuse points, gathered as the path
-    integrator does at one vertex (src/integrators/path.cpp:176-250; diffuse BSDF
-    src/bsdfs/diffuse.cpp:100-180): emitter sampling + cosine BSDF sampling with the
-    power heuristic, spp samples per point (u_em = next_2d, u_bsdf = next_2d).
-    em: an Oracle.  normals (n, 3); wavelengths (k, n) for spectral.  Returns (C, n) fp64."""
+def _direct_diffuse_samples(em, normals, seed, spp, lam):
+    """Per sample of direct_diffuse: the emitter sample (sample_direction result, the
+    cosine at the point, whether it contributes) and the cosine-sampled BSDF direction
+    with its pdf, from the PCG32Sampler streams (u_em = next_2d, u_bsdf = next_2d)."""
     normals = np.asarray(normals, dtype=np.float32)
     n = normals.shape[0]
     rng = Pcg32(seed, n)
     s, t = _coordinate_system(normals)
-    c = wavelengths.shape[0] if em.spectral else 3
-    acc = np.zeros((c, n), dtype=np.float64)
-    lam = None if not em.spectral else np.asarray(wavelengths, dtype=np.float32)
     for _ in range(spp):
         u0, u1, u2, u3 = rng.next_float(), rng.next_float(), rng.next_float(), rng.next_float()
         # emitter sampling (path.cpp:208-250)
         r = em.sample_direction(np.stack([u0, u1], axis=1), wavelengths=lam)
-        d, pd, w = r["d"], r["pdf"], r["weight"]
-        cos_em = (normals.astype(np.float64) * d).sum(axis=1)
-        ok = (pd != 0) & (cos_em > 0)
-        bpdf = np.where(ok, cos_em / np.pi, 0.0)
-        scale = np.where(ok, bpdf * _mis_power(pd, bpdf), 0.0)
-        acc += scale[None, :] * w.T
-        # BSDF sampling + the escaped ray (path.cpp:176-196)
+        cos_em = (normals.astype(np.float64) * r["d"]).sum(axis=1)
+        ok = (r["pdf"] != 0) & (cos_em > 0)
+        # BSDF sampling (path.cpp:176-196): square_to_cosine_hemisphere in the normal's frame
         px, py = _disk_concentric(u2, u3)
         lz = np.sqrt(np.maximum(0.0, 1.0 - (px.astype(np.float64) ** 2 + py.astype(np.float64) ** 2)))
         dw = (s * px[:, None] + t * py[:, None] + normals * lz[:, None]).astype(np.float32)
-        bp = lz / np.pi
-        mis = np.where(bp > 0, _mis_power(bp, em.pdf_direction(dw)), 0.0)
+        yield r, cos_em, ok, dw, lz / np.pi
+
+
+def direct_diffuse(em, normals, seed, spp, wavelengths=None, rho=None, vis=None):
+    """Sun-and-sky light at smooth-diffuse points, gathered as the path integrator does at
+    one vertex (src/integrators/path.cpp:176-250; diffuse BSDF src/bsdfs/diffuse.cpp:100-180):
+    emitter sampling + cosine BSDF sampling with the power heuristic, spp samples per point.
+    em: an Oracle.  normals (n, 3); wavelengths (k, n) for spectral.  vis: None or (spp, n)
+    uint8 tracer verdicts (bit 0 the shadow ray is unoccluded, path.cpp:216-219; bit 1 the
+    BSDF ray escapes, path.cpp:176-196).  Returns (C, n) fp64."""
+    normals = np.asarray(normals, dtype=np.float32)
+    n = normals.shape[0]
+    c = wavelengths.shape[0] if em.spectral else 3
+    acc = np.zeros((c, n), dtype=np.float64)
+    lam = None if not em.spectral else np.asarray(wavelengths, dtype=np.float32)
+    for k, (r, cos_em, ok, dw, bp) in enumerate(_direct_diffuse_samples(em, normals, seed, spp, lam)):
+        v = np.full(n, 3, np.uint8) if vis is None else np.asarray(vis[k], dtype=np.uint8)
+        ok = ok & ((v & 1) != 0)
+        bpdf = np.where(ok, cos_em / np.pi, 0.0)
+        scale = np.where(ok, bpdf * _mis_power(r["pdf"], bpdf), 0.0)
+        acc += scale[None, :] * r["weight"].T
+        # the escaped ray: eval weighted by MIS against pdf_direction
+        esc = (bp > 0) & ((v & 2) != 0)
+        mis = np.where(esc, _mis_power(bp, em.pdf_direction(dw)), 0.0)
         e = em.eval(-dw, lam) if em.spectral else em.eval(-dw).T
         acc += mis[None, :] * e
     r = np.ones(n) if rho is None else np.asarray(rho, dtype=np.float64)
     return acc * (r / spp)[None, :]
+
+
+def direct_diffuse_rays(em, normals, seed, spp):
+    """The rays a tracer tests for direct_diffuse (sunsky_direct_diffuse_rays): emitter-sample
+    directions and BSDF directions, each (spp, n, 3) fp32, zero where no ray is needed."""
+    em_d, bs_d = [], []
+    for r, cos_em, ok, dw, bp in _direct_diffuse_samples(em, normals, seed, spp, None if not em.spectral else
+                                                         np.full((1, len(normals)), 500.0, np.float32)):
+        em_d.append(np.where(ok[:, None], r["d"], 0.0).astype(np.float32))
+        bs_d.append(np.where((bp > 0)[:, None], dw, 0.0).astype(np.float32))
+    return np.stack(em_d), np.stack(bs_d)

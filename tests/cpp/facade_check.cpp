@@ -62,10 +62,11 @@ static int host_mode() {
     return 0;
 }
 
-static bool write_file(const std::string& path, const std::vector<float>& v) {
+template <typename T>
+static bool write_file(const std::string& path, const std::vector<T>& v) {
     FILE* f = std::fopen(path.c_str(), "wb");
     if (!f) return false;
-    std::fwrite(v.data(), sizeof(float), v.size(), f);
+    std::fwrite(v.data(), sizeof(T), v.size(), f);
     std::fclose(f);
     return true;
 }
@@ -119,7 +120,24 @@ static int gpu_mode(const std::string& dir) {
     HIPCK(hipDeviceSynchronize());
     std::vector<float> direct(3 * n);
     HIPCK(hipMemcpy(direct.data(), d_dd, 3 * n * 4, hipMemcpyDeviceToHost));
-    (void)hipFree(d_nrm); (void)hipFree(d_dd);
+    // the occluded form: the rays of the same samples, a tracer that blocks every shadow ray
+    // below 30 deg elevation and lets every BSDF ray escape, then the shading call
+    float *d_er, *d_br;
+    uint8_t* d_vis;
+    HIPCK(hipMalloc(&d_er, 3 * 2 * n * 4)); HIPCK(hipMalloc(&d_br, 3 * 2 * n * 4)); HIPCK(hipMalloc(&d_vis, 2 * n));
+    em.direct_diffuse_rays({d_nrm, d_nrm + n, d_nrm + 2 * n}, n, 3, 2, {d_er, d_er + 2 * n, d_er + 4 * n},
+                           {d_br, d_br + 2 * n, d_br + 4 * n});
+    HIPCK(hipDeviceSynchronize());
+    std::vector<float> er(3 * 2 * n);
+    HIPCK(hipMemcpy(er.data(), d_er, er.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<uint8_t> vis(2 * n);
+    for (size_t k = 0; k < 2 * n; ++k) vis[k] = (uint8_t)((er[4 * n + k] >= 0.5f ? 1 : 0) | 2);
+    HIPCK(hipMemcpy(d_vis, vis.data(), vis.size(), hipMemcpyHostToDevice));
+    em.direct_diffuse({d_nrm, d_nrm + n, d_nrm + 2 * n}, n, 3, 2, {d_dd, n}, nullptr, {}, nullptr, d_vis, n);
+    HIPCK(hipDeviceSynchronize());
+    std::vector<float> occluded(3 * n);
+    HIPCK(hipMemcpy(occluded.data(), d_dd, 3 * n * 4, hipMemcpyDeviceToHost));
+    (void)hipFree(d_nrm); (void)hipFree(d_dd); (void)hipFree(d_er); (void)hipFree(d_br); (void)hipFree(d_vis);
 
     std::vector<float> rgb(3 * n), dd(3 * n), pdf(n), w(3 * n), pdf2(n), djv(3 * n);
     HIPCK(hipMemcpy(djv.data(), d_djv, 3 * n * 4, hipMemcpyDeviceToHost));
@@ -131,7 +149,8 @@ static int gpu_mode(const std::string& dir) {
     bool ok = write_file(dir + "/wi.f32", wi) && write_file(dir + "/u.f32", u) && write_file(dir + "/rgb.f32", rgb) &&
               write_file(dir + "/d.f32", dd) && write_file(dir + "/pdf.f32", pdf) && write_file(dir + "/w.f32", w) &&
               write_file(dir + "/pdf2.f32", pdf2) && write_file(dir + "/drgb_dturbidity.f32", djv) &&
-              write_file(dir + "/direct.f32", direct);
+              write_file(dir + "/direct.f32", direct) && write_file(dir + "/occluded.f32", occluded) &&
+              write_file(dir + "/emitter_rays.f32", er) && write_file(dir + "/vis.u8", vis);
     for (float* ptr : {d_wi, d_u, d_rgb, d_d, d_pdf, d_w, d_pdf2, d_jv, d_djv}) (void)hipFree(ptr);
     if (!ok) { std::puts("FAIL writing outputs"); return 1; }
     std::printf("gpu ok w_sky=%.9g\n", em.info().sky_sampling_w);

@@ -71,6 +71,18 @@ def test_facade_gpu_mode(exe, tmp_path):
     ref = O.direct_diffuse(o32, np.tile(np.array([[0, 0, 1]], np.float32), (n, 1)), 3, 2)
     rel = (np.abs(dd - ref) / np.maximum(np.abs(ref), 1e-3 * np.abs(ref).max())).max(axis=0)
     assert np.quantile(rel, 0.995) < 2e-4
+    # the occluded form: rays from direct_diffuse_rays, the program's tracer verdicts, shading
+    e_o, _ = O.direct_diffuse_rays(o32, np.tile(np.array([[0, 0, 1]], np.float32), (n, 1)), 3, 2)
+    er = np.fromfile(tmp_path / "emitter_rays.f32", dtype=np.float32).reshape(3, 2, n).transpose(1, 2, 0)
+    both = er.any(axis=2) & e_o.any(axis=2)
+    assert np.quantile(np.abs(er[both] - e_o[both]).max(axis=1), 0.999) < 2e-6
+    vis = np.fromfile(tmp_path / "vis.u8", dtype=np.uint8).reshape(2, n)
+    assert 0.05 < (vis == 2).mean() < 0.95
+    occ = load("occluded.f32", 3).T
+    ref = O.direct_diffuse(o32, np.tile(np.array([[0, 0, 1]], np.float32), (n, 1)), 3, 2, vis=vis)
+    rel = (np.abs(occ - ref) / np.maximum(np.abs(ref), 1e-3 * np.abs(ref).max())).max(axis=0)
+    assert np.quantile(rel, 0.995) < 2e-4
+    assert occ.mean() < dd.mean()
     # eval_jvp through the facade: d eval / d turbidity vs fp64 central differences
     djv = load("drgb_dturbidity.f32", 3)
     h = 1e-3

@@ -120,6 +120,50 @@ def test_oracle_estimator_unbiased(variant):
     assert np.all(np.abs(est.mean(axis=1) - q) < 5 * se + 2e-4 * q), (est.mean(axis=1), q, se)
 
 
+# A synthetic occluder standing in for the caller's ray tracer: a ring of terrain that hides
+# every direction below elevation asin(MU0) of the emitter's frame.  "horizon" leaves the sun
+# (50 deg) visible, "wall" hides it (sin 50.27 deg < 0.8).  Aligned with the quadrature's
+# cap, so the occluded integral is exact: the sky over {mu >= MU0} (+ the sun disc if visible).
+OCCLUDERS = {"horizon": 0.4, "wall": 0.8}
+
+
+def occluded_quadrature(scene, variant, normal, mu0, lam=WL):
+    sky = O.Oracle(dict(scene, sun_scale=0.0), variant, "jit", "f64")
+    sun = O.Oracle(dict(scene, sky_scale=0.0), variant, "jit", "f64")
+    info = sun.info()
+    up = np.array([0.0, 0.0, 1.0])
+    e = _cap_integral(sky, up, mu0, normal, lam, 768, 1536)
+    if info["sun_dir_world"][2] > mu0 + 0.01:   # the whole disc above the terrain
+        e = e + _cap_integral(sun, info["sun_dir_world"], info["cos_cutoff"], normal, lam, 64, 256)
+    return e
+
+
+def tracer_verdicts(em_dir, bs_dir, mu0):
+    """bit 0: the shadow ray along the emitter sample clears the terrain; bit 1: the BSDF ray
+    escapes.  Works on numpy arrays and torch tensors of shape (3, spp, n) / (spp, n, 3)."""
+    return (em_dir >= mu0) * 1 + (bs_dir >= mu0) * 2
+
+
+@pytest.mark.parametrize("occluder", list(OCCLUDERS))
+def test_oracle_occluded_estimator_unbiased(occluder):
+    """With the tracer's verdicts on direct_diffuse_rays' rays, the estimator converges to
+    (1/pi) int L V max(0, n.w) dw: both halves are gated by their own ray's visibility, so MIS
+    stays unbiased (path.cpp:176-250).  fp64 oracle, as test_oracle_estimator_unbiased."""
+    mu0 = OCCLUDERS[occluder]
+    n_pts, spp = 1 << 13, 8
+    normal = NORMALS["tilted"]
+    em = O.Oracle(SCENE, "rgb", "jit", "f64")
+    normals = np.tile(np.asarray(normal, dtype=np.float32), (n_pts, 1))
+    e_d, b_d = O.direct_diffuse_rays(em, normals, 5, spp)
+    vis = tracer_verdicts(e_d[..., 2], b_d[..., 2], mu0).astype(np.uint8)
+    est = O.direct_diffuse(em, normals, 5, spp, vis=vis)
+    q = occluded_quadrature(SCENE, "rgb", normal, mu0)
+    se = est.std(axis=1) / math.sqrt(n_pts)
+    assert np.all(np.abs(est.mean(axis=1) - q) < 5 * se + 2e-4 * q), (est.mean(axis=1), q, se)
+    # and the occluder matters: the unoccluded estimate is well above it
+    assert np.all(O.direct_diffuse(em, normals, 5, spp).mean(axis=1) > q * 1.05)
+
+
 def test_direct_diffuse_host_errors():
     L = ss.lib()
     h = C.c_void_p()
@@ -129,16 +173,27 @@ def test_direct_diffuse_host_errors():
     nrm = ss._capi.Vec3In(0, 0, 0)
     out = (C.c_float * 3)()
     # null normals / output
-    assert L.sunsky_direct_diffuse(h, nrm, None, None, 0, 0, 0, 1, 1, None, 1, None) != 0
+    assert L.sunsky_direct_diffuse(h, nrm, None, None, 0, 0, 0, 1, None, 0, 1, None, 1, None) != 0
     buf = (C.c_float * 3)()
     p = C.cast(buf, C.c_void_p).value
     nrm = ss._capi.Vec3In(p, p, p)
-    assert L.sunsky_direct_diffuse(h, nrm, None, None, 0, 0, 0, 0, 1, out, 1, None) != 0   # spp = 0
+    assert L.sunsky_direct_diffuse(h, nrm, None, None, 0, 0, 0, 0, None, 0, 1, out, 1, None) != 0   # spp = 0
     assert b"spp" in L.sunsky_last_error()
-    assert L.sunsky_direct_diffuse(h, nrm, None, out, 4, 1, 0, 1, 1, out, 1, None) != 0     # RGB + lambdas
-    assert L.sunsky_direct_diffuse(h, nrm, None, None, 0, 0, 0, 1, 1, out, 1, None) != 0    # host-only emitter
+    assert L.sunsky_direct_diffuse(h, nrm, None, out, 4, 1, 0, 1, None, 0, 1, out, 1, None) != 0     # RGB + lambdas
+    assert L.sunsky_direct_diffuse(h, nrm, None, None, 0, 0, 0, 1, None, 0, 1, out, 1, None) != 0    # host-only emitter
     assert b"host-only" in L.sunsky_last_error()
-    assert L.sunsky_direct_diffuse(h, nrm, None, None, 0, 0, 0, 1, 0, out, 1, None) == 0    # n = 0: no-op
+    assert L.sunsky_direct_diffuse(h, nrm, None, None, 0, 0, 0, 1, None, 0, 0, out, 1, None) == 0    # n = 0: no-op
+    vis = (C.c_uint8 * 4)()
+    assert L.sunsky_direct_diffuse(h, nrm, None, None, 0, 0, 0, 1, vis, 1, 2, out, 2, None) != 0     # vis_stride < n
+    assert b"vis_stride" in L.sunsky_last_error()
+    o3 = ss._capi.Vec3Out(p, p, p)
+    null3 = ss._capi.Vec3Out(None, None, None)
+    assert L.sunsky_direct_diffuse_rays(h, nrm, 0, 1, 1, null3, o3, 1, None) != 0          # null ray planes
+    assert L.sunsky_direct_diffuse_rays(h, nrm, 0, 0, 1, o3, o3, 1, None) != 0             # spp = 0
+    assert L.sunsky_direct_diffuse_rays(h, nrm, 0, 1, 2, o3, o3, 1, None) != 0             # ray_stride < n
+    assert L.sunsky_direct_diffuse_rays(h, nrm, 0, 1, 1, o3, o3, 1, None) != 0             # host-only emitter
+    assert b"host-only" in L.sunsky_last_error()
+    assert L.sunsky_direct_diffuse_rays(h, nrm, 0, 1, 0, o3, o3, 0, None) == 0             # n = 0: no-op
     L.sunsky_emitter_destroy(h)
     L.sunsky_props_destroy(props)
 
@@ -207,3 +262,100 @@ def test_direct_diffuse_deterministic_and_seeded():
     a, b = em.direct_diffuse(nrm, 1, 3), em.direct_diffuse(nrm, 1, 3)
     c = em.direct_diffuse(nrm, 2, 3)
     assert torch.equal(a, b) and not torch.equal(a, c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", ["fast", "reference"])
+@pytest.mark.parametrize("frame", ["identity", "rotated"])
+def test_direct_diffuse_rays_parity(precision, frame):
+    """sunsky_direct_diffuse_rays writes the directions oracle.direct_diffuse_rays samples on
+    the same streams (sampling bounds of test_gpu_parity.py: p99.9 < 2e-6, max < 1e-4), with
+    the same lanes zeroed (no ray needed) except where a sample sits on a discontinuity."""
+    import torch
+    scene = dict(SCENE, to_world=_rot_x(0.35)) if frame == "rotated" else SCENE
+    em = ss.SunskyEmitter(scene, "rgb", precision=precision)
+    o32 = O.Oracle(scene, "rgb", "jit", "f32")
+    o32.override_w_sky(em.sky_sampling_w)
+    n, spp, seed = 1 << 14, 3, 21
+    normals = _gpu_normals(n, 9)
+    e_g, b_g = em.direct_diffuse_rays(torch.from_numpy(normals.T.copy()).cuda(), seed, spp)
+    e_g = e_g.permute(1, 2, 0).cpu().numpy()
+    b_g = b_g.permute(1, 2, 0).cpu().numpy()
+    e_o, b_o = O.direct_diffuse_rays(o32, normals, seed, spp)
+    for g, o in ((e_g, e_o), (b_g, b_o)):
+        zg, zo = ~g.any(axis=2), ~o.any(axis=2)
+        assert (zg != zo).mean() < 1e-3, (zg != zo).mean()
+        both = ~zg & ~zo
+        dlt = np.abs(g[both] - o[both]).max(axis=1)
+        assert np.quantile(dlt, 0.999) < 2e-6 and dlt.max() < 1e-4, (np.quantile(dlt, 0.999), dlt.max())
+        assert np.allclose(np.linalg.norm(g[both], axis=1), 1.0, atol=1e-5)
+    assert (~e_g.any(axis=2)).mean() > 0.05          # some emitter samples fall below the point's horizon
+
+
+def _occluded_inputs(em, n, spp, seed, mu0, normals):
+    import torch
+    nrm = torch.from_numpy(normals.T.copy()).cuda()
+    e_d, b_d = em.direct_diffuse_rays(nrm, seed, spp)
+    vis = tracer_verdicts(e_d[2], b_d[2], mu0).to(torch.uint8)     # the caller's tracer, on the GPU
+    return nrm, vis
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+@pytest.mark.parametrize("occluder", list(OCCLUDERS))
+def test_direct_diffuse_occluded_parity(variant, occluder):
+    """Per point, the occluded GPU estimate equals oracle.direct_diffuse given the same
+    verdicts (computed from the GPU's rays), at the unoccluded test's bound."""
+    import torch
+    em = ss.SunskyEmitter(SCENE, variant)
+    o32 = O.Oracle(SCENE, variant, "jit", "f32")
+    o32.override_w_sky(em.sky_sampling_w)
+    n, spp, seed = 1 << 14, 4, 17
+    normals = _gpu_normals(n, 5)
+    nrm, vis = _occluded_inputs(em, n, spp, seed, OCCLUDERS[occluder], normals)
+    rng = np.random.default_rng(6)
+    lam = rng.uniform(360, 720, (4, n)).astype(np.float32) if variant == "spectral" else None
+    out = em.direct_diffuse(nrm, seed, spp, None if lam is None else torch.from_numpy(lam).cuda(), visibility=vis)
+    got = out.cpu().numpy().astype(np.float64)
+    ref = O.direct_diffuse(o32, normals, seed, spp, lam, vis=vis.cpu().numpy())
+    v = vis.cpu().numpy()
+    assert (v != 3).mean() > 0.05 and (v != 0).mean() > 1e-3   # the occluder hides a real share of rays
+    rel = (np.abs(got - ref) / np.maximum(np.abs(ref), 1e-3 * np.abs(ref).max())).max(axis=0)
+    assert np.quantile(rel, 0.995) < 2e-4, np.quantile(rel, [0.5, 0.99, 0.995, 1.0])
+    assert abs(got.mean() - ref.mean()) < 1e-3 * abs(ref.mean())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("occluder", list(OCCLUDERS))
+def test_direct_diffuse_occluded_unbiased(occluder):
+    """2^20 points x 16 spp behind the terrain: the GPU estimate matches the occluded quadrature
+    within 5 standard errors + 1.5e-3 (as test_direct_diffuse_unbiased)."""
+    mu0 = OCCLUDERS[occluder]
+    em = ss.SunskyEmitter(SCENE, "rgb")
+    n, spp = 1 << 20, 16
+    nv = np.asarray(NORMALS["tilted"], dtype=np.float32)
+    nrm, vis = _occluded_inputs(em, n, spp, 321, mu0, np.tile(nv, (n, 1)))
+    est = em.direct_diffuse(nrm, 321, spp, visibility=vis).double()
+    mean, se = est.mean(dim=1).cpu().numpy(), (est.std(dim=1) / math.sqrt(n)).cpu().numpy()
+    q = occluded_quadrature(SCENE, "rgb", NORMALS["tilted"], mu0)
+    assert np.all(np.abs(mean - q) < 5 * se + 1.5e-3 * q), (mean, q, se)
+
+
+@pytest.mark.gpu
+def test_direct_diffuse_visibility_all_and_none():
+    """All bits set is the unoccluded call bit for bit; no bit set is black; each half alone
+    adds up to the whole (the two halves are separate sums)."""
+    import torch
+    em = ss.SunskyEmitter(SCENE, "rgb")
+    n, spp = 4099, 3
+    nrm = torch.from_numpy(_gpu_normals(n, 8).T.copy()).cuda()
+    free = em.direct_diffuse(nrm, 9, spp)
+    full = em.direct_diffuse(nrm, 9, spp, visibility=torch.full((spp, n), 3, dtype=torch.uint8, device="cuda"))
+    none = em.direct_diffuse(nrm, 9, spp, visibility=torch.zeros((spp, n), dtype=torch.uint8, device="cuda"))
+    nee = em.direct_diffuse(nrm, 9, spp, visibility=torch.ones((spp, n), dtype=torch.uint8, device="cuda"))
+    bsdf = em.direct_diffuse(nrm, 9, spp, visibility=torch.full((spp, n), 2, dtype=torch.uint8, device="cuda"))
+    assert torch.equal(free, full)
+    assert torch.count_nonzero(none) == 0
+    assert torch.allclose(nee + bsdf, free, rtol=1e-5, atol=1e-6 * float(free.abs().max()))
+    with pytest.raises(ValueError):
+        em.direct_diffuse(nrm, 9, spp, visibility=torch.zeros((spp + 1, n), dtype=torch.uint8, device="cuda"))

@@ -64,3 +64,58 @@ def test_eval_and_sampling_replay_bitwise(variant):
     for a, b, old in zip(captured, eager2, eager):
         assert torch.equal(a, b)
         assert not torch.equal(a, old)
+
+
+def test_replay_reads_the_updated_emitter_state():
+    """Kernels read the emitter state from device memory (include/sunsky_amd.h), so a graph
+    captured before params.update() replays with the new parameters: equal to an eager call
+    after the update, different from the pre-update result."""
+    em = ss.SunskyEmitter(angles_dict(3.0, 0.3, np.deg2rad(50), 0.3, 1.0, 1.0), "rgb")
+    n = 1 << 14
+    wi, _ = _inputs(n, 3)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        em.eval(ss.SurfaceInteraction3f(wi=wi))
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        captured = em.eval(ss.SurfaceInteraction3f(wi=wi))
+    g.replay()
+    torch.cuda.synchronize()
+    before = captured.clone()
+    params = em.traverse()
+    params["turbidity"] = 6.5
+    params.update()
+    g.replay()
+    torch.cuda.synchronize()
+    eager = em.eval(ss.SurfaceInteraction3f(wi=wi))
+    torch.cuda.synchronize()
+    assert torch.equal(captured, eager)
+    assert not torch.equal(captured, before)
+
+
+def test_direct_diffuse_with_visibility_replays_bitwise():
+    """The occluded caller pair (rays, then shading with the tracer's verdicts) captures too."""
+    em = ss.SunskyEmitter(angles_dict(3.0, 0.3, np.deg2rad(50), 0.3, 1.0, 1.0), "rgb")
+    n, spp = 1 << 14, 2
+    nrm = torch.nn.functional.normalize(torch.rand((3, n), device="cuda") + 0.2, dim=0)
+
+    def step():
+        e_d, b_d = em.direct_diffuse_rays(nrm, 4, spp)
+        vis = ((e_d[2] >= 0.4).to(torch.uint8) + 2 * (b_d[2] >= 0.4).to(torch.uint8))
+        return em.direct_diffuse(nrm, 4, spp, visibility=vis)
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        captured = step()
+    g.replay()
+    torch.cuda.synchronize()
+    eager = step()
+    torch.cuda.synchronize()
+    assert torch.equal(captured, eager)

@@ -138,6 +138,15 @@ __device__ __forceinline__ float div_by_rcp(float a, float b, float rb) {
     return a / b;
 }
 
+// A wave-uniform float the compiler may not re-derive per lane: the sampling loops
+// select between the reciprocals 1 / w_sky and 1 / (1 - w_sky) (div_exact's rb), and
+// without this InstCombine folds select(p, 1 / a, 1 / b) into 1 / select(p, a, b), a
+// full per-lane division (13 VALU + v_rcp) in every sample.  Same value, bit for bit.
+__device__ __forceinline__ float uniform_f(float x) {
+    asm("" : "+v"(x));   // a value the optimiser cannot look through (no instruction)
+    return x;
+}
+
 template <bool FAST>
 __device__ __forceinline__ float div_exact(float a, float b, float rb) {
     if constexpr (FAST) return div_by_rcp(a, b, rb);
@@ -1153,7 +1162,7 @@ __device__ __forceinline__ void sample_direction_body(
     }
     __shared__ SamplerLds<FAST, SPEC> S;
     stage_sampler_lds<FAST, SPEC>(K, &S);
-    const float w_sun = 1.f - K.w_sky, inv_w = 1.f / K.w_sky, inv_w_sun = 1.f / w_sun;   // div_exact
+    const float w_sun = 1.f - K.w_sky, inv_w = uniform_f(1.f / K.w_sky), inv_w_sun = uniform_f(1.f / w_sun);
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     // the next sample's u is loaded before this one's work, so its HBM latency overlaps the
     // ~500 VALU instructions of a sample: 4.4 % faster, bitwise the same (interleaved A/B,
@@ -1365,7 +1374,7 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
                                                 float* __restrict__ weight, size_t wstride) {
     __shared__ SamplerLds<FAST, SPEC> S;
     stage_sampler_lds<FAST, SPEC>(K, &S);
-    const float w_sun = 1.f - K.w_sky, inv_w = 1.f / K.w_sky, inv_w_sun = 1.f / w_sun;   // div_exact
+    const float w_sun = 1.f - K.w_sky, inv_w = uniform_f(1.f / K.w_sky), inv_w_sun = uniform_f(1.f / w_sun);
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         bool act = active ? active[i] != 0 : true;
@@ -1461,7 +1470,7 @@ __device__ __forceinline__ void direct_diffuse_body(
     size_t ostride) {
     __shared__ SamplerLds<FAST, SPEC> S;
     stage_sampler_lds<FAST, SPEC>(K, &S);
-    const float w_sun = 1.f - K.w_sky, inv_w = 1.f / K.w_sky, inv_w_sun = 1.f / w_sun;   // div_exact
+    const float w_sun = 1.f - K.w_sky, inv_w = uniform_f(1.f / K.w_sky), inv_w_sun = uniform_f(1.f / w_sun);
     constexpr int C = SPEC ? 4 : 3;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -1567,7 +1576,7 @@ __device__ __forceinline__ void direct_diffuse_rays_body(
     __shared__ TgmmLds T;
     stage_tgmm(K, &T);
     __syncthreads();
-    const float w_sun = 1.f - K.w_sky, inv_w = 1.f / K.w_sky, inv_w_sun = 1.f / w_sun;   // div_exact
+    const float w_sun = 1.f - K.w_sky, inv_w = uniform_f(1.f / K.w_sky), inv_w_sun = uniform_f(1.f / w_sun);
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const float3_ nrm = mk3(nx[i], ny[i], nz[i]);

@@ -840,7 +840,10 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
         const bool lean = !it_p.x && !ds_dist && !ds_p.x && !active;
         const KernelId k = spec ? (lean ? K_SAMPLE_DIRECTION_SPEC_LEAN : K_SAMPLE_DIRECTION_SPEC)
                                 : (lean ? K_SAMPLE_DIRECTION_RGB_LEAN : K_SAMPLE_DIRECTION_RGB);
-        launch(e->fn(k), grid_for(e->mod, k, n), (hipStream_t)stream, args);
+        // the fast RGB LEAN kernel is wave-sorted: one wave takes a window of 4 x 64 samples
+        const size_t items =
+            k == K_SAMPLE_DIRECTION_RGB_LEAN && e->precision == SUNSKY_PRECISION_FAST ? (n + 3) / 4 : n;
+        launch(e->fn(k), grid_for(e->mod, k, items), (hipStream_t)stream, args);
     });
 }
 

@@ -886,20 +886,28 @@ __device__ __forceinline__ int discrete_sample_reuse(const SunskyKArgs& K, const
     const float s = value * K.gauss_sum;
     const bool jit = K.semantics == kJit;
     const int end = jit ? kNbMixture - 1 : K.gauss_last;
-    int idx, cnt;
+    auto pred = [&](int j) {
+        const float c = T.cdf[j < kNbMixture ? j : kNbMixture - 1];
+        return j < end && (jit ? (((c < s) || c == 0.f) && (c != K.gauss_sum)) : (c < s));
+    };
+    int idx;
     if (value >= 0.f && value < 1.f) {
-        idx = T.guide[(int)(value * (float)kGaussGuideSize)];
-        cnt = K.gauss_guide_span;
+        // the predicate (and j < end) holds on a prefix of the entries, and the answer lies
+        // in [guide, guide + span]: the index is guide + the number of true tests among
+        // the span entries.  A wave-uniform trip count with no early exit: no divergent
+        // loop, no exec-mask bookkeeping.
+        const int g = T.guide[(int)(value * (float)kGaussGuideSize)];
+        int add = 0;
+#pragma unroll 1
+        for (int k = 0; k < K.gauss_guide_span; ++k) add += pred(g + k) ? 1 : 0;
+        idx = g + add;
     } else {   // outside [0, 1) (or NaN): the full search
         idx = jit ? 0 : K.gauss_first;
-        cnt = kNbMixture;
-    }
-    for (int k = 0; k < cnt; ++k) {
-        if (idx >= end) break;
-        const float c = T.cdf[idx];
-        const bool p = jit ? (((c < s) || c == 0.f) && (c != K.gauss_sum)) : (c < s);
-        if (!p) break;
-        ++idx;
+#pragma unroll 1
+        for (int k = 0; k < kNbMixture; ++k) {
+            if (!pred(idx)) break;
+            ++idx;
+        }
     }
     const float pmf = T.pmf[idx];
     const float cdf_prev = idx > 0 ? T.cdf[idx - 1] : 0.f;
@@ -1231,6 +1239,121 @@ __device__ __forceinline__ void sample_direction_body(
                 weight[(size_t)k * wstride + i] = isfinite(w) ? w : 0.f;
             }
         }
+    }
+}
+
+// One LEAN RGB sample (u -> d, pdf, weight), the per-sample work of
+// sample_direction_body<FAST, false, true> in the same operation order.
+template <bool FAST>
+__device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const SamplerLds<FAST, false>& S, float sx,
+                                               float sy, float inv_w, float inv_w_sun, float o[7]) {
+    const bool pick_sky = sx < K.w_sky;
+    const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
+    const bool act = sd.z >= 0.f;
+    const float3_ d = to_world(K, sd);
+    float skyp, sunp;
+    compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+    const float pd = lerpf_(sunp, skyp, K.w_sky);
+    o[0] = d.x; o[1] = d.y; o[2] = d.z; o[3] = pd;
+    float e[3];
+    eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, to_local(K, d), act, e, S.rows);
+    const float inv_pd = fdiv<FAST>(1.f, pd);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float w = FAST ? e[c] * inv_pd : e[c] / pd;
+        o[4 + c] = isfinite(w) ? w : 0.f;
+    }
+}
+
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+// Wave-sorted LEAN RGB sample_direction (sunsky.cpp:399-441).  A wave takes a window of
+// 64 R consecutive samples, ranks them sky picks first (ballot + mbcnt, stable), and runs
+// R 64-lane passes over the ranked order: only the pass holding the sky/sun boundary runs
+// both the TGMM sampling branch and the sun-disc polynomial, the others run one of them.
+// The window goes through a wave-private LDS block (no workgroup barrier): each lane
+// writes its samples' u at their ranks, pass p reads ranks [64p, 64p + 64) and writes its
+// 7 outputs back at the same ranks (the rows of u it just consumed), and each lane then
+// reads its own samples' outputs from their ranks, so the global loads and the
+// non-temporal stores stay coalesced in sample order.  Each sample is computed by
+// sample_one_rgb from its own u: bitwise the outputs of sample_direction_body<FAST, false, true>.
+template <bool FAST, int R>
+__device__ __forceinline__ void sample_direction_sorted_body(
+    const SunskyKArgs& K, const float* __restrict__ ux, const float* __restrict__ uy, size_t n,
+    float* __restrict__ dx, float* __restrict__ dy, float* __restrict__ dz, float* __restrict__ pdf,
+    float* __restrict__ weight, size_t wstride) {
+    constexpr int W = 64 * R;
+    __shared__ SamplerLds<FAST, false> S;
+    __shared__ float X[SS_BLOCK / 64][7][W];
+    stage_sampler_lds<FAST, false>(K, &S);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float(*Y)[W] = X[wv];
+    const float inv_w = uniform_f(1.f / K.w_sky), inv_w_sun = uniform_f(1.f / (1.f - K.w_sky));
+    const size_t nwin = (n + W - 1) / W;
+    const size_t wstep = (size_t)gridDim.x * (SS_BLOCK / 64);
+    // the next window's u is loaded before this window's passes (its HBM latency overlaps them)
+    float na[R], nb[R];
+    auto load_window = [&](size_t w) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t i = w * W + (size_t)(r * 64 + lane);
+            na[r] = i < n ? ux[i] : 1.f;   // past the end: a sun pick, computed and not stored
+            nb[r] = i < n ? uy[i] : 0.5f;
+        }
+    };
+    size_t w = (size_t)blockIdx.x * (SS_BLOCK / 64) + wv;
+    if (w < nwin) load_window(w);
+    for (; w < nwin; w += wstep) {
+        const size_t base = w * W;
+        int slot[R];
+        {
+            float a[R], b[R];
+            uint64_t m[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                a[r] = na[r];
+                b[r] = nb[r];
+            }
+            if (w + wstep < nwin) load_window(w + wstep);
+#pragma unroll
+            for (int r = 0; r < R; ++r) m[r] = __ballot(a[r] < K.w_sky);
+            int psun = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) psun += __popcll(m[r]);
+            int psky = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const bool sky = (m[r] >> lane) & 1;
+                slot[r] = sky ? psky + lanes_below(m[r]) : psun + lanes_below(~m[r]);
+                Y[0][slot[r]] = a[r];
+                Y[1][slot[r]] = b[r];
+                const int c = __popcll(m[r]);
+                psky += c;
+                psun += 64 - c;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+        for (int p = 0; p < R; ++p) {
+            const int q = p * 64 + lane;
+            float o[7];
+            sample_one_rgb<FAST>(K, S, Y[0][q], Y[1][q], inv_w, inv_w_sun, o);
+#pragma unroll
+            for (int k = 0; k < 7; ++k) Y[k][q] = o[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        float* const planes[7] = {dx, dy, dz, pdf, weight, weight + wstride, weight + 2 * wstride};
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t i = base + (size_t)(r * 64 + lane);
+            if (i < n) {
+#pragma unroll
+                for (int k = 0; k < 7; ++k) store_nt(Y[k][slot[r]], planes[k] + i);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -2203,10 +2326,26 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_fast, true, false, false)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_ref, false, false, false)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_fast, true, true, false)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_ref, false, true, false)
-SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_fast, true, false, true)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_ref, false, false, true)
+// the unsorted LEAN RGB fast form, kept for A/B timing against the wave-sorted product kernel
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_plain_fast, true, false, true)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_fast, true, true, true)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_ref, false, true, true)
+
+#define SS_SAMPLE_DIRECTION_SORTED(NAME, FAST, R)                                                             \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
+        const SunskyKArgs* __restrict__ Kp, const float* ux, const float* uy, const float* px, const float* py, const float* pz,   \
+        const float* lam, size_t lstride, int nlam, const uint8_t* active, size_t n, float* dx, float* dy,     \
+        float* dz, float* pdf, float* dist, float* opx, float* opy, float* opz, float* weight, size_t wstride) { \
+        sample_direction_sorted_body<FAST, R>(*Kp, ux, uy, n, dx, dy, dz, pdf, weight, wstride);              \
+    }
+// LEAN RGB fast sample_direction (the C ABI's common call): wave-sorted windows of 4 x 64
+// samples.  R = 4 measured fastest (kbench sweep, profiles/r02_v11_ws_sweep.log): R = 2 / 3
+// sort less of the divergence away, R = 5 / 6 are held to 3 waves/SIMD by their LDS.  The
+// reference-precision LEAN kernel stays unsorted: hipcc's fp contraction is decided per
+// kernel after inlining, and in the _ref form the sorted body did not reproduce the general
+// kernel's bits (the fast form does, test_wave_sorted_lean_rgb_kernel_ragged_sizes).
+SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_fast, true, 4)
 
 
 #define SS_PDF_DIRECTION(NAME, VEC, FAST)                                                                     \

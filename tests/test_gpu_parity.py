@@ -243,6 +243,31 @@ def test_sample_direction_lean_kernel_bitwise(variant, precision):
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)
+def test_wave_sorted_lean_rgb_kernel_ragged_sizes(precision):
+    """The RGB LEAN kernel ranks each wave's 4 x 64-sample window sky picks first and
+    writes the outputs back in sample order: bit for bit the general kernel, for batch
+    sizes that end inside a window, a row or a lane (1 ... 2^20 + 1), all-sky and all-sun
+    windows, u.x exactly at w_sky and next to it, at 0 and at 1 - ulp."""
+    em = ss.SunskyEmitter(angles_dict(3.0, 1.1, np.deg2rad(60), 0.3, 1.0, 1.0), "rgb", precision=precision)
+    w = np.float32(em.sky_sampling_w)
+    rng = np.random.default_rng(11)
+    it = ss.Interaction3f()
+    special = np.array([w, np.nextafter(w, 0, dtype=np.float32), np.nextafter(w, 1, dtype=np.float32), 0.0,
+                        np.nextafter(np.float32(1), 0, dtype=np.float32)], np.float32)
+    for n in (1, 5, 63, 64, 65, 255, 256, 257, 1000, 1024, 4097, 65537, (1 << 20) + 1):
+        u = rng.random((n, 2), dtype=np.float32)
+        u[: min(n, 5), 0] = special[: min(n, 5)]
+        if n >= 2048:
+            u[256:512, 0] *= w          # an all-sky window
+            u[512:768, 0] = w + (1 - w) * u[512:768, 0]   # an all-sun window
+        ut = soa(u)
+        ds_full, w_full = em.sample_direction(it, ut)
+        ds_lean, w_lean = em.sample_direction(it, ut, positions=False)
+        for a, b in ((ds_full.d, ds_lean.d), (ds_full.pdf, ds_lean.pdf), (w_full, w_lean)):
+            assert np.array_equal(host(a).view(np.uint32), host(b).view(np.uint32)), n
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("elev_deg", [0.1, 0.6, 3.0, 20.0, 60.0, 89.5])
 def test_sun_disc_weights_across_elevations(elev_deg, precision):
     """Sun-picked samples (sunsky.cpp:697-701) at sun elevations whose disc spans one to

@@ -112,6 +112,18 @@ int main(int argc, char** argv) {
     if (sampling) {
         std::vector<float> u(2 * n);
         for (auto& v : u) v = U(rng);
+        // KB_SORT_U=1: u.x ascending, so every wave is all-sky or all-sun (the divergence-free
+        // bound of sample_direction; outputs differ from the unsorted run by construction)
+        // KB_SORT_U=2: only partitioned, sky picks (u.x < w_sky) first, each class in its
+        // random order (the bound of removing the sky/sun divergence alone)
+        if (const char* su = std::getenv("KB_SORT_U")) {
+            if (std::atoi(su) == 2) {
+                const float ws = model.kargs().w_sky;
+                std::stable_partition(u.begin(), u.begin() + n, [ws](float x) { return x < ws; });
+            } else {
+                std::sort(u.begin(), u.begin() + n);
+            }
+        }
         CK(hipMemcpy(wx, u.data(), n * 4, hipMemcpyHostToDevice));
         CK(hipMemcpy(wy, u.data() + n, n * 4, hipMemcpyHostToDevice));
         CK(hipMalloc(&dd, 3 * n * 4)); CK(hipMalloc(&pdf, n * 4)); CK(hipMalloc(&wgt, 3 * n * 4));
@@ -172,18 +184,29 @@ int main(int argc, char** argv) {
             CK(hipEventElapsedTime(&ms, e0, e1));
             double us = 1e3 * ms / iters;
             // checksum against the first kernel
-            std::vector<float> h((size_t)nout * n);
-            CK(hipMemcpy(h.data(), sampling ? (mode == "pdf" ? pdf : wgt) : out, h.size() * 4, hipMemcpyDeviceToHost));
+            // sample mode: d (3 planes), pdf and the weight (3 planes) all enter the check
+            const bool samp7 = mode == "sample";
+            std::vector<float> h((size_t)(samp7 ? 7 : nout) * n);
+            if (samp7) {
+                CK(hipMemcpy(h.data(), dd, 3 * n * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(h.data() + 3 * n, pdf, n * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(h.data() + 4 * n, wgt, 3 * n * 4, hipMemcpyDeviceToHost));
+            } else {
+                CK(hipMemcpy(h.data(), sampling ? (mode == "pdf" ? pdf : wgt) : out, h.size() * 4, hipMemcpyDeviceToHost));
+            }
             double maxrel = 0;
+            size_t ndiff = 0;
             if (ref.empty()) ref = h;
             else
                 for (size_t i = 0; i < h.size(); ++i) {
+                    if (std::memcmp(&h[i], &ref[i], 4) != 0) ++ndiff;
                     double d = std::fabs((double)h[i] - ref[i]) / std::max(1e-6, std::fabs((double)ref[i]));
                     if (d > maxrel) maxrel = d;
                 }
-            std::printf("%-36s bpcu=%-4d grid=%-6u %9.2f us  %7.1f GB/s  %.3e evals/s  maxrel-vs-first=%.2e\n",
+            std::printf("%-36s bpcu=%-4d grid=%-6u %9.2f us  %7.1f GB/s  %.3e evals/s  maxrel-vs-first=%.2e  "
+                        "bitdiff=%zu\n",
                         argv[a], mult, grid, us, bytes / (us * 1e-6) / 1e9, (spec ? 11.0 : 1.0) * n / (us * 1e-6),
-                        maxrel);
+                        maxrel, ndiff);
             std::fflush(stdout);
             // KB_AB=<other.hsaco>: the same kernel from a second code object, timed in
             // alternating bursts (KB_AB_ROUNDS of them) so clock and thermal drift hit

@@ -290,11 +290,11 @@ def parity_c3(em, d_scene, wi, out, n_check=1 << 19, n_sun=1 << 13):
     return dict(st, checked_dirs=wi_all.shape[0], kernel="sunsky_eval_spec_nodes_v4")
 
 
-def parity_c4(em, d_scene, u, d, pdf_s, wgt, pdf_q, n_check=1 << 19):
+def parity_c4(em, d_scene, u, d, pdf_s, wgt, pdf_q, n_check=1 << 19, semantics="jit"):
     """C4 parity on the first n_check samples: directions vs the oracle's sampler on the
     same u, and pdf / pdf_direction / weight at the GPU's own directions."""
     O = _oracle()
-    o32, o64 = O.Oracle(d_scene, "rgb", "jit", "f32"), O.Oracle(d_scene, "rgb", "jit", "f64")
+    o32, o64 = O.Oracle(d_scene, "rgb", semantics, "f32"), O.Oracle(d_scene, "rgb", semantics, "f64")
     o32.override_w_sky(em.sky_sampling_w)
     o64.override_w_sky(em.sky_sampling_w)
     uh = u[:, :n_check].T.cpu().numpy()
@@ -620,66 +620,71 @@ def main():
                                                 "note": "16M rays x 4 random wavelengths in [360, 720] nm "
                                                         "(reads wi + lambda, writes 4 radiances)"}
         del lam4, rays_out
-        # C4: sample_direction + pdf_direction, 64M samples (per GPU)
+        # C4: sample_direction + pdf_direction, 64M samples (per GPU); JIT semantics (w_sky from
+        # the quadrature) and the scalar variants' w_sky = 0.5 (sunsky.cpp:778-783)
         ns = 4 * n
         kfx = "ref" if args.precision == "reference" else "fast"
-        smp = ss.SunskyEmitter(dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), "rgb", precision=args.precision,
-                               device=dev)
-        g = torch.Generator(device=dev)
-        g.manual_seed(99 + rank)
-        u = torch.rand((2, ns), generator=g, device=dev)
-        d = torch.empty((3, ns), dtype=torch.float32, device=dev)
-        pdf_s = torch.empty(ns, dtype=torch.float32, device=dev)
-        wgt = torch.empty((3, ns), dtype=torch.float32, device=dev)
-        pdf_q = torch.empty(ns, dtype=torch.float32, device=dev)
-        nul_in = ss._capi.Vec3In(None, None, None)
-        nul_out = ss._capi.Vec3Out(None, None, None)
-        d_out = ss._capi.Vec3Out(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr())
-        d_in = ss._capi.Vec3In(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr())
+        for sem, key in (("jit", "sampling_C4"), ("scalar", "sampling_C4_scalar_w05")):
+            smp_s = ss.SunskyEmitter(dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), "rgb", semantics=sem,
+                                     precision=args.precision, device=dev)
+            g = torch.Generator(device=dev)
+            g.manual_seed(99 + rank)
+            u = torch.rand((2, ns), generator=g, device=dev)
+            d = torch.empty((3, ns), dtype=torch.float32, device=dev)
+            pdf_s = torch.empty(ns, dtype=torch.float32, device=dev)
+            wgt = torch.empty((3, ns), dtype=torch.float32, device=dev)
+            pdf_q = torch.empty(ns, dtype=torch.float32, device=dev)
+            nul_in = ss._capi.Vec3In(None, None, None)
+            nul_out = ss._capi.Vec3Out(None, None, None)
+            d_out = ss._capi.Vec3Out(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr())
+            d_in = ss._capi.Vec3In(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr())
 
-        def sample_step():   # ds.dist / ds.p not requested (NULL): 36 B per sample
-            rc = lib.sunsky_sample_direction(smp._h, u[0].data_ptr(), u[1].data_ptr(), nul_in, None, 0, 0, None, ns,
-                                             d_out, pdf_s.data_ptr(), None, nul_out, wgt.data_ptr(), ns, stream)
-            if rc:
-                raise RuntimeError(lib.sunsky_last_error().decode())
+            def sample_step():   # ds.dist / ds.p not requested (NULL): 36 B per sample
+                rc = lib.sunsky_sample_direction(smp_s._h, u[0].data_ptr(), u[1].data_ptr(), nul_in, None, 0, 0, None,
+                                                 ns, d_out, pdf_s.data_ptr(), None, nul_out, wgt.data_ptr(), ns, stream)
+                if rc:
+                    raise RuntimeError(lib.sunsky_last_error().decode())
 
-        def pdf_step():      # 16 B per sample
-            rc = lib.sunsky_pdf_direction(smp._h, d_in, None, ns, pdf_q.data_ptr(), stream)
-            if rc:
-                raise RuntimeError(lib.sunsky_last_error().decode())
+            def pdf_step():      # 16 B per sample
+                rc = lib.sunsky_pdf_direction(smp_s._h, d_in, None, ns, pdf_q.data_ptr(), stream)
+                if rc:
+                    raise RuntimeError(lib.sunsky_last_error().decode())
 
-        for _ in range(2):
-            sample_step()
-            pdf_step()
-        reps = max(3, args.steps // 4)
-        t_s, t_p = KernelTimer(), KernelTimer()
-        t_s.begin()
-        for _ in range(reps):
-            sample_step()
-        t_s.end(reps)
-        t_p.begin()
-        for _ in range(reps):
-            pdf_step()
-        t_p.end(reps)
-        ms_s, ms_p = t_s.mean_ms(), t_p.mean_ms()
-        ms = ms_s + ms_p
-        sec["sampling_C4"] = {"samples_per_s": ns / (ms * 1e-3), "ms": ms, "samples": ns,
-                              "sample_direction_ms": ms_s, "pdf_direction_ms": ms_p,
-                              "achieved_GBps": BYTES_SAMPLE * ns / (ms * 1e-3) / 1e9,
-                              "note": "sample_direction (reads u; writes d, pdf, RGB weight) + pdf_direction "
-                                      "(reads d; writes pdf)"}
-        vs, vp = valu_floor("sunsky_sample_direction_rgb_lean_" + kfx), valu_floor("sunsky_pdf_direction_v4_" + kfx)
-        if vs and vp:
-            sec["sampling_C4"]["valu_roofline"] = {
-                "bound": "valu", "unit": "ms",
-                "sample_direction": dict(vs, achieved_ms=ms_s, frac=vs["issue_floor_ms"] / ms_s),
-                "pdf_direction": dict(vp, achieved_ms=ms_p, frac=vp["issue_floor_ms"] / ms_p),
-                "note": "frac = VALU-issue floor (PMC instruction counts x issue cycles / (1024 SIMDs x 2.4 GHz)) "
-                        "/ measured launch time; HBM frac of the same launches is achieved_GBps / 8000"}
-        if rank == 0:
-            sec["sampling_C4"]["parity"] = parity_c4(smp, dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), u, d,
-                                                     pdf_s, wgt, pdf_q)
-        del u, d, pdf_s, wgt, pdf_q
+            for _ in range(2):
+                sample_step()
+                pdf_step()
+            reps = max(3, args.steps // 4)
+            t_s, t_p = KernelTimer(), KernelTimer()
+            t_s.begin()
+            for _ in range(reps):
+                sample_step()
+            t_s.end(reps)
+            t_p.begin()
+            for _ in range(reps):
+                pdf_step()
+            t_p.end(reps)
+            ms_s, ms_p = t_s.mean_ms(), t_p.mean_ms()
+            ms = ms_s + ms_p
+            sec[key] = {"samples_per_s": ns / (ms * 1e-3), "ms": ms, "samples": ns,
+                        "sample_direction_ms": ms_s, "pdf_direction_ms": ms_p, "w_sky": smp_s.sky_sampling_w,
+                        "achieved_GBps": BYTES_SAMPLE * ns / (ms * 1e-3) / 1e9,
+                        "note": "sample_direction (reads u; writes d, pdf, RGB weight) + pdf_direction "
+                                "(reads d; writes pdf); " + ("JIT semantics, w_sky from the quadrature" if sem == "jit"
+                                                             else "scalar semantics, w_sky = 0.5")}
+            vs, vp = valu_floor("sunsky_sample_direction_rgb_lean_" + kfx), valu_floor("sunsky_pdf_direction_v4_" + kfx)
+            if sem == "jit" and vs and vp:
+                sec[key]["valu_roofline"] = {
+                    "bound": "valu", "unit": "ms",
+                    "sample_direction": dict(vs, achieved_ms=ms_s, frac=vs["issue_floor_ms"] / ms_s),
+                    "pdf_direction": dict(vp, achieved_ms=ms_p, frac=vp["issue_floor_ms"] / ms_p),
+                    "note": "frac = VALU-issue floor (PMC instruction counts x issue cycles / (1024 SIMDs x 2.4 GHz)) "
+                            "/ measured launch time; HBM frac of the same launches is achieved_GBps / 8000"}
+            if rank == 0:
+                sec[key]["parity"] = parity_c4(smp_s, dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), u, d,
+                                               pdf_s, wgt, pdf_q, semantics=sem)
+            del u, d, pdf_s, wgt, pdf_q
+            if sem == "jit":
+                smp = smp_s
         # caller (§8f row 4): direct sun+sky light at 16M diffuse points x 4 spp, emitter + BSDF
         # sampling with MIS fused in one kernel (sunsky_direct_diffuse); reads 12 B normal, writes 12 B RGB
         npts, spp = n, 4

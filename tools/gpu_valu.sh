@@ -15,6 +15,7 @@ run() {   # name mode n kernel
   timeout -s KILL 90 rocprofv3 --pmc $C -d $R/gpurun_out/valu/$1 -o $1 --output-format csv -- $KB $H $2 $3 5 64 $4 > $R/gpurun_out/valu/$1.log 2>&1
 }
 run sample sample 67108864 ${SAMPLE_KERNEL:-sunsky_sample_direction_rgb_lean_fast} && \
+run sample_plain sample 67108864 sunsky_sample_direction_rgb_lean_plain_fast && \
 run pdf pdf 67108864 sunsky_pdf_direction_v4_fast && \
 run rgb rgb 16777216 sunsky_eval_rgb_v4_fast && \
 run spec spec 16777216 sunsky_eval_spec_nodes_v4_fast

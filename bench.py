@@ -737,8 +737,24 @@ def main():
         del full
 
     # ------------------------------------------- configs[4]: spectral shard + gather
+    watchdog, printed = None, False
     if (args.c5 or world > 1) and not args.no_c5:
         del outs
+        # A rank whose communicator setup fails leaves the others waiting in a collective
+        # (RCCL init, a barrier).  The watchdog keeps that from costing the bench line: past
+        # the limit rank 0 prints the line with the C5 error and every rank exits 0.
+        import threading
+
+        def c5_timeout():
+            if rank == 0 and not printed:
+                result["c5_spectral_shard_gather"] = {"error": f"timed out after {c5_limit:.0f} s (a rank stuck in "
+                                                               "a collective); value is unaffected"}
+                print(json.dumps(result), flush=True)
+            os._exit(0)
+        c5_limit = float(os.environ.get("SUNSKY_BENCH_C5_TIMEOUT", "150"))
+        watchdog = threading.Timer(c5_limit, c5_timeout)
+        watchdog.daemon = True
+        watchdog.start()
         try:
             c5 = run_c5(args, world, rank, dev, coll_dev, rehearsal)
         except Exception as exc:   # reported beside `value`; never fail the bench line
@@ -750,9 +766,12 @@ def main():
         if not args.no_cpu and world == 1:   # the CPU baseline: rank 0 at N=1 only
             result["cpu_baseline"] = cpu_baseline(wi.T.cpu().numpy())
         print(json.dumps(result), flush=True)
+        printed = True
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if watchdog is not None:
+        watchdog.cancel()
 
 
 if __name__ == "__main__":

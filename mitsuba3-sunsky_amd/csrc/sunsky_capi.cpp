@@ -83,7 +83,7 @@ enum KernelId {
     K_EVAL_SPEC_RAYS_V4, K_EVAL_SPEC_RAYS_V1, K_SAMPLE_DIRECTION_RGB, K_SAMPLE_DIRECTION_SPEC, K_PDF_DIRECTION_V4, K_PDF_DIRECTION_V1, K_SAMPLE_WAVELENGTHS_RGB,
     K_SAMPLE_WAVELENGTHS_SPEC, K_SAMPLE_RAY_RGB, K_SAMPLE_RAY_SPEC, K_BAKE_RGB, K_BAKE_SPEC,
     K_DIRECT_DIFFUSE_RGB, K_DIRECT_DIFFUSE_SPEC, K_SAMPLE_DIRECTION_RGB_LEAN, K_SAMPLE_DIRECTION_SPEC_LEAN,
-    K_DIRECT_DIFFUSE_RAYS, K_COUNT
+    K_DIRECT_DIFFUSE_RAYS, K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
@@ -92,7 +92,8 @@ const char* kKernelNames[K_COUNT] = {
     "sunsky_sample_wavelengths_rgb",
     "sunsky_sample_wavelengths_spec", "sunsky_sample_ray_rgb", "sunsky_sample_ray_spec",
     "sunsky_bake_latlong_rgb", "sunsky_bake_latlong_spec", "sunsky_direct_diffuse_rgb", "sunsky_direct_diffuse_spec",
-    "sunsky_sample_direction_rgb_lean", "sunsky_sample_direction_spec_lean", "sunsky_direct_diffuse_rays"};
+    "sunsky_sample_direction_rgb_lean", "sunsky_sample_direction_spec_lean", "sunsky_direct_diffuse_rays",
+    "sunsky_sample_direction_rgb_lean_plain"};
 
 // eval kernels instantiated twice: eval(si) negates wi at compile time,
 // eval_direction(ds) uses ds.d as is (the "_dir" kernels)
@@ -166,6 +167,7 @@ int blocks_per_cu(KernelId k) {
         case K_EVAL_SPEC_BCAST_V4: case K_EVAL_SPEC_BCAST_V1: case K_EVAL_SPEC_NODES_V4: return 64;
         case K_SAMPLE_DIRECTION_RGB: case K_SAMPLE_DIRECTION_SPEC: case K_PDF_DIRECTION_V4: case K_PDF_DIRECTION_V1:
         case K_SAMPLE_DIRECTION_RGB_LEAN: case K_SAMPLE_DIRECTION_SPEC_LEAN:
+        case K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN:
             return 64;
         case K_BAKE_RGB: case K_BAKE_SPEC: return 64;
         case K_DIRECT_DIFFUSE_RGB: case K_DIRECT_DIFFUSE_SPEC: case K_DIRECT_DIFFUSE_RAYS: return 64;
@@ -838,9 +840,14 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
         // the common call (no it.p, ds.dist, ds.p or mask) takes the kernel with those
         // paths compiled out: same results, no SGPR spills (sampling)
         const bool lean = !it_p.x && !ds_dist && !ds_p.x && !active;
+        // SUNSKY_AMD_UNSORTED_SAMPLING=1: the unsorted LEAN RGB kernel (A/B timing and the bitwise
+        // sorted-vs-unsorted test); read per call so a test can switch it
+        const char* uns = std::getenv("SUNSKY_AMD_UNSORTED_SAMPLING");
+        const bool unsorted = uns && uns[0] == '1';
         const KernelId k = spec ? (lean ? K_SAMPLE_DIRECTION_SPEC_LEAN : K_SAMPLE_DIRECTION_SPEC)
-                                : (lean ? K_SAMPLE_DIRECTION_RGB_LEAN : K_SAMPLE_DIRECTION_RGB);
-        // the fast RGB LEAN kernel is wave-sorted: one wave takes a window of 4 x 64 samples
+                                : (lean ? (unsorted ? K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN : K_SAMPLE_DIRECTION_RGB_LEAN)
+                                        : K_SAMPLE_DIRECTION_RGB);
+        // the fast LEAN RGB kernel is wave-sorted: one wave takes a window of 4 x 64 samples
         const size_t items =
             k == K_SAMPLE_DIRECTION_RGB_LEAN && e->precision == SUNSKY_PRECISION_FAST ? (n + 3) / 4 : n;
         launch(e->fn(k), grid_for(e->mod, k, items), (hipStream_t)stream, args);

@@ -1242,14 +1242,15 @@ __device__ __forceinline__ void sample_direction_body(
     }
 }
 
-// One LEAN RGB sample (u -> d, pdf, weight), the per-sample work of
-// sample_direction_body<FAST, false, true> in the same operation order.
+// One RGB sample (u -> d, pdf, weight), the per-sample work of
+// sample_direction_body<FAST, false, LEAN> in the same operation order; `act` is the
+// caller's mask (true in the LEAN form).
 template <bool FAST>
 __device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const SamplerLds<FAST, false>& S, float sx,
-                                               float sy, float inv_w, float inv_w_sun, float o[7]) {
+                                               float sy, bool act, float inv_w, float inv_w_sun, float o[7]) {
     const bool pick_sky = sx < K.w_sky;
     const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
-    const bool act = sd.z >= 0.f;
+    act = act && (sd.z >= 0.f);
     const float3_ d = to_world(K, sd);
     float skyp, sunp;
     compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
@@ -1269,21 +1270,31 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
-// Wave-sorted LEAN RGB sample_direction (sunsky.cpp:399-441).  A wave takes a window of
+// Wave-sorted RGB sample_direction (sunsky.cpp:399-441).  A wave takes a window of
 // 64 R consecutive samples, ranks them sky picks first (ballot + mbcnt, stable), and runs
 // R 64-lane passes over the ranked order: only the pass holding the sky/sun boundary runs
 // both the TGMM sampling branch and the sun-disc polynomial, the others run one of them.
 // The window goes through a wave-private LDS block (no workgroup barrier): each lane
-// writes its samples' u at their ranks, pass p reads ranks [64p, 64p + 64) and writes its
-// 7 outputs back at the same ranks (the rows of u it just consumed), and each lane then
-// reads its own samples' outputs from their ranks, so the global loads and the
-// non-temporal stores stay coalesced in sample order.  Each sample is computed by
-// sample_one_rgb from its own u: bitwise the outputs of sample_direction_body<FAST, false, true>.
-template <bool FAST, int R>
+// writes its samples' u (and, FULL, the caller's mask) at their ranks, pass p reads ranks
+// [64p, 64p + 64) and writes its 7 outputs back at the same ranks (the rows it just
+// consumed), and each lane then reads its own samples' outputs from their ranks, so the
+// global loads and the non-temporal stores stay coalesced in sample order.  FULL adds
+// the optional it.p / ds.dist / ds.p / mask of the general kernel: ds.dist and ds.p are
+// functions of d and it.p, computed after the un-sort from each lane's own it.p.  Each
+// sample is computed by sample_one_rgb from its own u: bitwise the outputs of
+// sample_direction_body<FAST, false, !FULL>.
+template <bool FAST, int R, bool FULL>
 __device__ __forceinline__ void sample_direction_sorted_body(
-    const SunskyKArgs& K, const float* __restrict__ ux, const float* __restrict__ uy, size_t n,
-    float* __restrict__ dx, float* __restrict__ dy, float* __restrict__ dz, float* __restrict__ pdf,
-    float* __restrict__ weight, size_t wstride) {
+    const SunskyKArgs& K, const float* __restrict__ ux, const float* __restrict__ uy,
+    const float* __restrict__ px, const float* __restrict__ py, const float* __restrict__ pz,
+    const uint8_t* __restrict__ active, size_t n, float* __restrict__ dx, float* __restrict__ dy,
+    float* __restrict__ dz, float* __restrict__ pdf, float* __restrict__ dist, float* __restrict__ opx,
+    float* __restrict__ opy, float* __restrict__ opz, float* __restrict__ weight, size_t wstride) {
+    if constexpr (!FULL) {
+        px = py = pz = nullptr;
+        active = nullptr;
+        dist = opx = opy = opz = nullptr;
+    }
     constexpr int W = 64 * R;
     __shared__ SamplerLds<FAST, false> S;
     __shared__ float X[SS_BLOCK / 64][7][W];
@@ -1329,6 +1340,10 @@ __device__ __forceinline__ void sample_direction_sorted_body(
                 slot[r] = sky ? psky + lanes_below(m[r]) : psun + lanes_below(~m[r]);
                 Y[0][slot[r]] = a[r];
                 Y[1][slot[r]] = b[r];
+                if (FULL && active) {
+                    const size_t i = base + (size_t)(r * 64 + lane);
+                    Y[2][slot[r]] = (i < n && active[i] != 0) ? 1.f : 0.f;
+                }
                 const int c = __popcll(m[r]);
                 psky += c;
                 psun += 64 - c;
@@ -1338,8 +1353,9 @@ __device__ __forceinline__ void sample_direction_sorted_body(
 #pragma unroll 1
         for (int p = 0; p < R; ++p) {
             const int q = p * 64 + lane;
+            const bool act = FULL && active ? Y[2][q] != 0.f : true;
             float o[7];
-            sample_one_rgb<FAST>(K, S, Y[0][q], Y[1][q], inv_w, inv_w_sun, o);
+            sample_one_rgb<FAST>(K, S, Y[0][q], Y[1][q], act, inv_w, inv_w_sun, o);
 #pragma unroll
             for (int k = 0; k < 7; ++k) Y[k][q] = o[k];
         }
@@ -1351,6 +1367,14 @@ __device__ __forceinline__ void sample_direction_sorted_body(
             if (i < n) {
 #pragma unroll
                 for (int k = 0; k < 7; ++k) store_nt(Y[k][slot[r]], planes[k] + i);
+                if (FULL && (dist || opx)) {   // as sample_direction_body: ds.dist, ds.p (sunsky.cpp:417-420)
+                    const float3_ d = mk3(Y[0][slot[r]], Y[1][slot[r]], Y[2][slot[r]]);
+                    float3_ itp = mk3(px ? px[i] : 0.f, py ? py[i] : 0.f, pz ? pz[i] : 0.f);
+                    float3_ rel = mk3(itp.x - K.bs_center[0], itp.y - K.bs_center[1], itp.z - K.bs_center[2]);
+                    float dd = 2.f * fmaxf(K.bs_radius, sqrtf(dot3(rel, rel)));
+                    if (dist) dist[i] = dd;
+                    if (opx) { opx[i] = fmaf(d.x, dd, itp.x); opy[i] = fmaf(d.y, dd, itp.y); opz[i] = fmaf(d.z, dd, itp.z); }
+                }
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -2329,15 +2353,18 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_ref, false, true, false)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_ref, false, false, true)
 // the unsorted LEAN RGB fast form, kept for A/B timing against the wave-sorted product kernel
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_plain_fast, true, false, true)
+// reference-precision twin of the unsorted LEAN form (the C ABI loads every kernel in both precisions)
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_plain_ref, false, false, true)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_fast, true, true, true)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_ref, false, true, true)
 
-#define SS_SAMPLE_DIRECTION_SORTED(NAME, FAST, R)                                                             \
+#define SS_SAMPLE_DIRECTION_SORTED(NAME, FAST, R, FULL)                                                           \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
         const SunskyKArgs* __restrict__ Kp, const float* ux, const float* uy, const float* px, const float* py, const float* pz,   \
         const float* lam, size_t lstride, int nlam, const uint8_t* active, size_t n, float* dx, float* dy,     \
         float* dz, float* pdf, float* dist, float* opx, float* opy, float* opz, float* weight, size_t wstride) { \
-        sample_direction_sorted_body<FAST, R>(*Kp, ux, uy, n, dx, dy, dz, pdf, weight, wstride);              \
+        sample_direction_sorted_body<FAST, R, FULL>(*Kp, ux, uy, px, py, pz, active, n, dx, dy, dz, pdf, dist, \
+                                                    opx, opy, opz, weight, wstride);                           \
     }
 // LEAN RGB fast sample_direction (the C ABI's common call): wave-sorted windows of 4 x 64
 // samples.  R = 4 measured fastest (kbench sweep, profiles/r02_v11_ws_sweep.log): R = 2 / 3
@@ -2345,7 +2372,11 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_ref, false, true, true)
 // reference-precision LEAN kernel stays unsorted: hipcc's fp contraction is decided per
 // kernel after inlining, and in the _ref form the sorted body did not reproduce the general
 // kernel's bits (the fast form does, test_wave_sorted_lean_rgb_kernel_ragged_sizes).
-SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_fast, true, 4)
+SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_fast, true, 4, false)
+// The general call (it.p, ds.dist, ds.p, mask) in the same windows: bitwise the unsorted kernel
+// (test_wave_sorted_rgb_kernels_bitwise_vs_unsorted) but 2 % slower (125 VGPRs and 28 SGPR spills,
+// 4 waves/SIMD; profiles/r02_v13_ab_sample_full.log), so the C ABI keeps the unsorted general kernel.
+SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_full_sorted_fast, true, 4, true)
 
 
 #define SS_PDF_DIRECTION(NAME, VEC, FAST)                                                                     \

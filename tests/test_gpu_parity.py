@@ -243,17 +243,26 @@ def test_sample_direction_lean_kernel_bitwise(variant, precision):
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)
-def test_wave_sorted_lean_rgb_kernel_ragged_sizes(precision):
-    """The RGB LEAN kernel ranks each wave's 4 x 64-sample window sky picks first and
-    writes the outputs back in sample order: bit for bit the general kernel, for batch
+def test_wave_sorted_rgb_kernels_bitwise_vs_unsorted(precision, monkeypatch):
+    """The fast LEAN RGB sample_direction kernel ranks each wave's 4 x 64-sample window sky
+    picks first and writes the outputs back in sample order.  Against the unsorted kernel
+    (SUNSKY_AMD_UNSORTED_SAMPLING=1) the outputs d, pdf and weight are bit for bit the same,
+    and both equal the general call's (+ it.p, ds.dist, ds.p, an active mask), for batch
     sizes that end inside a window, a row or a lane (1 ... 2^20 + 1), all-sky and all-sun
-    windows, u.x exactly at w_sky and next to it, at 0 and at 1 - ulp."""
-    em = ss.SunskyEmitter(angles_dict(3.0, 1.1, np.deg2rad(60), 0.3, 1.0, 1.0), "rgb", precision=precision)
+    windows, u.x at w_sky and next to it, at 0 and at 1 - ulp, and a rotated emitter."""
+    d = angles_dict(3.0, 1.1, np.deg2rad(60), 0.3, 1.0, 1.0)
+    d["to_world"] = np.array([[0, 0, 1, 0], [1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 0, 1]], np.float64)
+    em = ss.SunskyEmitter(d, "rgb", precision=precision)
     w = np.float32(em.sky_sampling_w)
     rng = np.random.default_rng(11)
-    it = ss.Interaction3f()
     special = np.array([w, np.nextafter(w, 0, dtype=np.float32), np.nextafter(w, 1, dtype=np.float32), 0.0,
                         np.nextafter(np.float32(1), 0, dtype=np.float32)], np.float32)
+
+    def run(ut, it, mask, positions):
+        ds, wt = em.sample_direction(it, ut, active=mask, positions=positions)
+        outs = [ds.d, ds.pdf, wt] + ([ds.p, ds.dist] if positions else [])
+        return [host(x).view(np.uint32).copy() for x in outs]
+
     for n in (1, 5, 63, 64, 65, 255, 256, 257, 1000, 1024, 4097, 65537, (1 << 20) + 1):
         u = rng.random((n, 2), dtype=np.float32)
         u[: min(n, 5), 0] = special[: min(n, 5)]
@@ -261,10 +270,20 @@ def test_wave_sorted_lean_rgb_kernel_ragged_sizes(precision):
             u[256:512, 0] *= w          # an all-sky window
             u[512:768, 0] = w + (1 - w) * u[512:768, 0]   # an all-sun window
         ut = soa(u)
-        ds_full, w_full = em.sample_direction(it, ut)
-        ds_lean, w_lean = em.sample_direction(it, ut, positions=False)
-        for a, b in ((ds_full.d, ds_lean.d), (ds_full.pdf, ds_lean.pdf), (w_full, w_lean)):
-            assert np.array_equal(host(a).view(np.uint32), host(b).view(np.uint32)), n
+        p = torch.from_numpy(rng.normal(size=(3, n)).astype(np.float32) * 10).cuda()
+        mask = torch.from_numpy(rng.random(n) < 0.8).cuda()
+        monkeypatch.delenv("SUNSKY_AMD_UNSORTED_SAMPLING", raising=False)
+        lean = run(ut, ss.Interaction3f(), None, False)
+        full = run(ut, ss.Interaction3f(p=p), None, True)
+        monkeypatch.setenv("SUNSKY_AMD_UNSORTED_SAMPLING", "1")
+        plain = run(ut, ss.Interaction3f(), None, False)
+        for a_, b_, c_ in zip(lean, plain, full):
+            assert np.array_equal(a_, b_) and np.array_equal(a_, c_), n
+        # the general call with a mask: masked samples carry zero weight, the others the LEAN values
+        masked = run(ut, ss.Interaction3f(p=p), mask, True)
+        mk = host(mask)
+        assert np.all(masked[2][:, ~mk] == 0) and np.array_equal(masked[2][:, mk], lean[2][:, mk]), n
+        assert np.array_equal(masked[0], lean[0]), n
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)

@@ -148,6 +148,15 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(cz[c], wz, n * 4, hipMemcpyDeviceToDevice));
     }
     const float* nullf = nullptr;
+    const bool full = std::getenv("KB_SAMPLE_FULL") != nullptr;
+    const float *fpx = nullptr, *fpy = nullptr, *fpz = nullptr;
+    float *fdist = nullptr, *fox = nullptr, *foy = nullptr, *foz = nullptr;
+    if (full) {   // it.p: the direction buffers (any finite points do); outputs: 4 more planes
+        fpx = wz; fpy = wz; fpz = wz;
+        float* buf = nullptr;
+        CK(hipMalloc(&buf, 4 * n * 4));
+        fdist = buf; fox = buf + n; foy = buf + 2 * n; foz = buf + 3 * n;
+    }
     float* nullo = nullptr;
     size_t zero = 0;
     int nl0 = 0;
@@ -167,8 +176,12 @@ int main(int argc, char** argv) {
             void* args_spec[] = {&K, &L, &wx, &wy, &wz, &active, &n, &out, &ostride, &sign};
             void* args_sample[] = {&K, &wx, &wy, &nullf, &nullf, &nullf, &nullf, &zero, &nl0, &active, &n,
                                    &dd, &ddy, &ddz, &pdf, &nullo, &nullo, &nullo, &nullo, &wgt, &n};
+            // KB_SAMPLE_FULL=1: the general call, it.p in, ds.dist and ds.p out (Mitsuba's DirectionSample)
+            void* args_sample_full[] = {&K, &wx, &wy, &fpx, &fpy, &fpz, &nullf, &zero, &nl0, &active, &n,
+                                        &dd, &ddy, &ddz, &pdf, &fdist, &fox, &foy, &foz, &wgt, &n};
             void* args_pdf[] = {&K, &dd, &ddy, &ddz, &active, &n, &pdf};
-            void** args = spec ? args_spec : mode == "sample" ? args_sample : mode == "pdf" ? args_pdf : args_rgb;
+            void** args = spec ? args_spec : mode == "sample" ? (full ? args_sample_full : args_sample)
+                                            : mode == "pdf" ? args_pdf : args_rgb;
             for (int w = 0; w < 3; ++w) CK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
             hipEvent_t e0, e1;
             CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));

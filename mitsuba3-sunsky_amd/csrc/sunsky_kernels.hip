@@ -1266,6 +1266,14 @@ __device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const Sampl
     }
 }
 
+// Orders a wave's own LDS accesses across the phases of a sorted window: an IR-level
+// wavefront-scope fence (no instruction on gfx950: a wave's LDS operations execute in
+// issue order) plus the scheduling barrier.
+__device__ __forceinline__ void wave_lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
@@ -1349,7 +1357,7 @@ __device__ __forceinline__ void sample_direction_sorted_body(
                 psun += 64 - c;
             }
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_order();
 #pragma unroll 1
         for (int p = 0; p < R; ++p) {
             const int q = p * 64 + lane;
@@ -1359,7 +1367,7 @@ __device__ __forceinline__ void sample_direction_sorted_body(
 #pragma unroll
             for (int k = 0; k < 7; ++k) Y[k][q] = o[k];
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_order();
         float* const planes[7] = {dx, dy, dz, pdf, weight, weight + wstride, weight + 2 * wstride};
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -1377,7 +1385,7 @@ __device__ __forceinline__ void sample_direction_sorted_body(
                 }
             }
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_order();
     }
 }
 

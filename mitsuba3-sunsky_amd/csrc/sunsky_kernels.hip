@@ -28,6 +28,14 @@
 #include "sunsky_staging.h"
 #include "sunsky_types.h"
 
+// fp contraction within a source expression only (C's FP_CONTRACT on), not across
+// statements: hipcc's default lets the backend fuse a product into a later statement's
+// add depending on the surrounding kernel, so the same inlined device function could
+// round differently in two kernels.  With this, one sample / direction computes the
+// same bits in every kernel that evaluates it (LEAN vs general vs wave-sorted sampling,
+// eval vs eval_direction, sharded vs whole batches).  Instruction counts unchanged.
+#pragma clang fp contract(on)
+
 using namespace sunsky;
 
 #define SS_BLOCK 256
@@ -816,16 +824,18 @@ struct TgPair {
     f32x2 mphi, mth, kphi, kth, c;
 };
 
+template <bool FAST>
 struct TgmmLds {
     Gaussian gauss[kNbMixture];                  // full mixture: sample_sky
     TgPair tp[kNbMixture / 2];
-    Gaussian tref[kNbMixture];                   // compacted, reference-order tgmm_pdf
+    Gaussian tref[FAST ? 1 : kNbMixture];        // compacted, reference-order tgmm_pdf (_ref kernels)
     float cdf[kNbMixture], pmf[kNbMixture];
     float inv_pmfn[kNbMixture];                  // 1 / RN(pmf * gauss_norm) (div_by_rcp)
     uint8_t guide[kGaussGuideSize];
 };
 
-__device__ __forceinline__ void stage_tgmm(const SunskyKArgs& K, TgmmLds* s) {
+template <bool FAST>
+__device__ __forceinline__ void stage_tgmm(const SunskyKArgs& K, TgmmLds<FAST>* s) {
     lds_copy(s->gauss, K.gauss, kNbMixture);
     lds_copy(s->cdf, K.gauss_cdf, kNbMixture);
     lds_copy(s->pmf, K.gauss_pmf, kNbMixture);
@@ -843,29 +853,33 @@ __device__ __forceinline__ void stage_tgmm(const SunskyKArgs& K, TgmmLds* s) {
             pair[4] = g.inv_sigma_phi * c;
             pair[6] = g.inv_sigma_theta * c;
             pair[8] = g.coef * kInvTwoPi;
-            s->tref[i] = g;
+            if constexpr (!FAST) s->tref[i] = g;
         } else {
             pair[0] = pair[2] = pair[4] = pair[6] = pair[8] = 0.f;
         }
     }
 }
 
+// Only what the variant reads: RGB keeps 3 sky channels and no spectral tables, the
+// fast kernels no reference-order gaussians.
+template <bool FAST, int N> struct ChanLdsN { typename ChanSel<FAST>::T c[N]; };
+
 template <bool FAST, bool SPEC>
 struct SamplerLds {
-    TgmmLds tgmm;
-    ChanLds<FAST> chans;                          // spectral weights (per-lane channel index)
-    SpecDistLds sdist;
-    float sun[SPEC ? kSunSpecTableSize : 4];      // spectral: the whole turbidity-lerped table
-    SunRowsRgb rows[SPEC ? 0 : 1];                // RGB: the disc's segments, channels interleaved
-    float ld[kNbWavelengths * kNbSunLdParams];
+    TgmmLds<FAST> tgmm;
+    ChanLdsN<FAST, SPEC ? kNbWavelengths : 3> chans;   // spectral: per-lane channel index
+    SpecDistLds sdist[SPEC ? 1 : 0];
+    float sun[SPEC ? kSunSpecTableSize : 0];       // spectral: the whole turbidity-lerped table
+    SunRowsRgb rows[SPEC ? 0 : 1];                 // RGB: the disc's segments, channels interleaved
+    float ld[SPEC ? kNbWavelengths * kNbSunLdParams : 0];
 };
 
 template <bool FAST, bool SPEC>
 __device__ __forceinline__ void stage_sampler_lds(const SunskyKArgs& K, SamplerLds<FAST, SPEC>* s) {
-    stage_tgmm(K, &s->tgmm);
-    stage_chans<FAST>(K, &s->chans);
-    if (SPEC) {
-        stage_spec_dist(K, &s->sdist);
+    stage_tgmm<FAST>(K, &s->tgmm);
+    lds_copy(s->chans.c, chan_table<FAST>(K), SPEC ? kNbWavelengths : 3);
+    if constexpr (SPEC) {
+        stage_spec_dist(K, &s->sdist[0]);
         lds_copy(s->ld, K.sun_ld, kNbWavelengths * kNbSunLdParams);
     }
     if constexpr (SPEC) lds_copy(s->sun, K.sun_table, kSunSpecTableSize);
@@ -881,7 +895,7 @@ __device__ __forceinline__ void stage_sampler_lds(const SunskyKArgs& K, SamplerL
 // (SunskyKArgs::gauss_guide) and tests at most gauss_guide_span further entries:
 // the same result as the full scan, ~1-2 LDS reads per lane instead of 19.
 template <bool FAST>
-__device__ __forceinline__ int discrete_sample_reuse(const SunskyKArgs& K, const TgmmLds& T, float value,
+__device__ __forceinline__ int discrete_sample_reuse(const SunskyKArgs& K, const TgmmLds<FAST>& T, float value,
                                                      float* reused) {
     const float s = value * K.gauss_sum;
     const bool jit = K.semantics == kJit;
@@ -934,7 +948,7 @@ __device__ __forceinline__ float3_ sphdir_dev(float theta, float phi) {
 
 // sample_sky, sunsky.cpp:661-689
 template <bool FAST>
-__device__ __forceinline__ float3_ sample_sky(const SunskyKArgs& K, const TgmmLds& T, float ux, float uy) {
+__device__ __forceinline__ float3_ sample_sky(const SunskyKArgs& K, const TgmmLds<FAST>& T, float ux, float uy) {
     float temp;
     int idx = discrete_sample_reuse<FAST>(K, T, ux, &temp);
     const Gaussian& g = T.gauss[idx];
@@ -995,7 +1009,7 @@ __device__ __forceinline__ float3_ sample_sun(const SunskyKArgs& K, float ux, fl
 // operands.  Same functions on the same arguments as sample_sky / sample_sun: bitwise
 // the same directions.
 template <bool FAST>
-__device__ __forceinline__ float3_ sample_sky_or_sun(const SunskyKArgs& K, const TgmmLds& T, bool pick_sky,
+__device__ __forceinline__ float3_ sample_sky_or_sun(const SunskyKArgs& K, const TgmmLds<FAST>& T, bool pick_sky,
                                                      float ux, float uy, float inv_w, float inv_w_sun) {
     const float a = div_exact<FAST>(pick_sky ? ux : ux - K.w_sky, pick_sky ? K.w_sky : 1.f - K.w_sky,
                                     pick_sky ? inv_w : inv_w_sun);
@@ -1043,7 +1057,7 @@ __device__ __forceinline__ float3_ sample_sky_or_sun(const SunskyKArgs& K, const
 
 // The FAST mixture sum of tgmm_pdf at a wrapped (phi, theta), one pair of
 // gaussians per iteration, one fma per gaussian in mixture order.
-__device__ __forceinline__ float tgmm_sum_fast(const SunskyKArgs& K, const TgmmLds& T, float phi, float theta) {
+__device__ __forceinline__ float tgmm_sum_fast(const SunskyKArgs& K, const TgmmLds<true>& T, float phi, float theta) {
     float pdf = 0.f;
     const int np = (K.tgmm_count + 1) >> 1;
 #pragma unroll 2
@@ -1061,7 +1075,7 @@ __device__ __forceinline__ float tgmm_sum_fast(const SunskyKArgs& K, const TgmmL
 // tgmm_pdf, sunsky.cpp:732-763, with the per-gaussian truncation volume hoisted
 // to the host (coef = weight / volume); same summation order as the reference.
 template <bool FAST>
-__device__ __forceinline__ float tgmm_pdf(const SunskyKArgs& K, const TgmmLds& T, float phi, float theta,
+__device__ __forceinline__ float tgmm_pdf(const SunskyKArgs& K, const TgmmLds<FAST>& T, float phi, float theta,
                                           bool active) {
     phi -= K.sun_phi - 0.5f * kPi;
     phi = phi < 0.f ? phi + kTwoPi : phi;
@@ -1086,7 +1100,7 @@ __device__ __forceinline__ float tgmm_pdf(const SunskyKArgs& K, const TgmmLds& T
 
 // compute_pdfs, sunsky.cpp:711-723
 template <bool FAST>
-__device__ __forceinline__ void compute_pdfs(const SunskyKArgs& K, const TgmmLds& T, float3_ d, bool check_sun,
+__device__ __forceinline__ void compute_pdfs(const SunskyKArgs& K, const TgmmLds<FAST>& T, float3_ d, bool check_sun,
                                              bool active, float* sky_pdf, float* sun_pdf) {
     float sin_theta = safe_sqrt_sel<FAST>(fmaf(d.x, d.x, d.y * d.y));
     active = active && (d.z >= 0.f) && (sin_theta != 0.f);
@@ -1396,8 +1410,8 @@ __device__ __forceinline__ void pdf_direction_body(const SunskyKArgs& K, const f
                                                    const float* __restrict__ dy, const float* __restrict__ dz,
                                                    const uint8_t* __restrict__ active, size_t n,
                                                    float* __restrict__ pdf) {
-    __shared__ TgmmLds T;
-    stage_tgmm(K, &T);
+    __shared__ TgmmLds<FAST> T;
+    stage_tgmm<FAST>(K, &T);
     __syncthreads();
     const float3_ sn = mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]);
     const size_t nvec = n / VEC;
@@ -1556,7 +1570,7 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
             DirTerms t = dir_terms<FAST>(K, wo, act);
             add_sun_terms<FAST>(K, t);
             float lam[4];
-            sample_wavelengths_one<FAST>(K, S.chans.c, S.sdist, S.sun, S.ld, t, wls[i], lam, w);
+            sample_wavelengths_one<FAST>(K, S.chans.c, S.sdist[0], S.sun, S.ld, t, wls[i], lam, w);
             for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = lam[k];
             nw = 4;
         }
@@ -1728,8 +1742,8 @@ __device__ __forceinline__ void direct_diffuse_rays_body(
     const SunskyKArgs& K, const float* __restrict__ nx, const float* __restrict__ ny, const float* __restrict__ nz,
     uint32_t seed, uint32_t spp, size_t n, float* __restrict__ ex, float* __restrict__ ey, float* __restrict__ ez,
     float* __restrict__ bx, float* __restrict__ by, float* __restrict__ bz, size_t rstride) {
-    __shared__ TgmmLds T;
-    stage_tgmm(K, &T);
+    __shared__ TgmmLds<FAST> T;
+    stage_tgmm<FAST>(K, &T);
     __syncthreads();
     const float w_sun = 1.f - K.w_sky, inv_w = uniform_f(1.f / K.w_sky), inv_w_sun = uniform_f(1.f / w_sun);
     const size_t stride = (size_t)gridDim.x * blockDim.x;

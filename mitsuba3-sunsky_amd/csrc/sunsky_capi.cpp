@@ -847,9 +847,8 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
         const KernelId k = spec ? (lean ? K_SAMPLE_DIRECTION_SPEC_LEAN : K_SAMPLE_DIRECTION_SPEC)
                                 : (lean ? (unsorted ? K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN : K_SAMPLE_DIRECTION_RGB_LEAN)
                                         : K_SAMPLE_DIRECTION_RGB);
-        // the fast LEAN RGB kernel is wave-sorted: one wave takes a window of 4 x 64 samples
-        const size_t items =
-            k == K_SAMPLE_DIRECTION_RGB_LEAN && e->precision == SUNSKY_PRECISION_FAST ? (n + 3) / 4 : n;
+        // the LEAN RGB kernels are wave-sorted: one wave takes a window of 4 x 64 samples
+        const size_t items = k == K_SAMPLE_DIRECTION_RGB_LEAN ? (n + 3) / 4 : n;
         launch(e->fn(k), grid_for(e->mod, k, items), (hipStream_t)stream, args);
     });
 }

@@ -2372,7 +2372,6 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_fast, true, false, false)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_ref, false, false, false)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_fast, true, true, false)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_ref, false, true, false)
-SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_ref, false, false, true)
 // the unsorted LEAN RGB fast form, kept for A/B timing against the wave-sorted product kernel
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_plain_fast, true, false, true)
 // reference-precision twin of the unsorted LEAN form (the C ABI loads every kernel in both precisions)
@@ -2388,13 +2387,14 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_ref, false, true, true)
         sample_direction_sorted_body<FAST, R, FULL>(*Kp, ux, uy, px, py, pz, active, n, dx, dy, dz, pdf, dist, \
                                                     opx, opy, opz, weight, wstride);                           \
     }
-// LEAN RGB fast sample_direction (the C ABI's common call): wave-sorted windows of 4 x 64
+// LEAN RGB sample_direction (the C ABI's common call): wave-sorted windows of 4 x 64
 // samples.  R = 4 measured fastest (kbench sweep, profiles/r02_v11_ws_sweep.log): R = 2 / 3
-// sort less of the divergence away, R = 5 / 6 are held to 3 waves/SIMD by their LDS.  The
-// reference-precision LEAN kernel stays unsorted: hipcc's fp contraction is decided per
-// kernel after inlining, and in the _ref form the sorted body did not reproduce the general
-// kernel's bits (the fast form does, test_wave_sorted_lean_rgb_kernel_ragged_sizes).
+// sort less of the divergence away, R = 5 / 6 are held to 3 waves/SIMD by their LDS.  Both
+// precisions reproduce the general kernel's bits (test_sample_direction_lean_kernel_bitwise,
+// test_wave_sorted_rgb_kernels_bitwise_vs_unsorted) since the file contracts within
+// expressions only (the pragma at the top).
 SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_fast, true, 4, false)
+SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_ref, false, 4, false)
 // The general call (it.p, ds.dist, ds.p, mask) in the same windows: bitwise the unsorted kernel
 // (test_wave_sorted_rgb_kernels_bitwise_vs_unsorted) but 2 % slower (125 VGPRs and 28 SGPR spills,
 // 4 waves/SIMD; profiles/r02_v13_ab_sample_full.log), so the C ABI keeps the unsorted general kernel.

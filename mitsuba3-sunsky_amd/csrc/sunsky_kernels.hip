@@ -304,9 +304,22 @@ __device__ __forceinline__ void add_sun_terms(const SunskyKArgs& K, DirTerms& t)
     if (t.hit_sun) {
         if constexpr (FAST) {
             float elevation = elevation_fast(t.cos_theta);
-            float seg = cbrt_unit_fast(2.f * elevation * kInvPi) * (float)kNbSunSegments;
-            int pos = seg > 0.f ? (int)floorf(seg) : 0;
-            pos = pos < kNbSunSegments - 1 ? pos : kNbSunSegments - 1;
+            int pos;
+#ifndef SS_PROBE_CBRT_SEGMENT   // probe build (A/B of the cbrt search): never in the product
+            if (K.sun_seg_nb >= 0) {
+#else
+            if (false) {
+#endif
+                // the segment starts the disc straddles (host, SunskyKArgs::sun_seg_bound):
+                // one compare per start instead of cbrt (v_log, v_exp, v_rcp, Newton step)
+                pos = K.sun_row_lo;
+#pragma unroll 1
+                for (int k = 0; k < K.sun_seg_nb; ++k) pos += elevation >= K.sun_seg_bound[k] ? 1 : 0;
+            } else {
+                float seg = cbrt_unit_fast(2.f * elevation * kInvPi) * (float)kNbSunSegments;
+                pos = seg > 0.f ? (int)floorf(seg) : 0;
+                pos = pos < kNbSunSegments - 1 ? pos : kNbSunSegments - 1;
+            }
             float frac = (float)pos * (1.f / (float)kNbSunSegments);
             t.sun_pos = pos;
             t.sun_x = elevation - kHalfPi * (frac * frac * frac);

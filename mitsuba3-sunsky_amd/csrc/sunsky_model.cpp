@@ -461,6 +461,21 @@ void SunskyModel::stage_geometry() {
         const double seg = std::cbrt(2.0 * std::min(lo, 0.5 * 3.14159265358979323846) / 3.14159265358979323846) *
                            (double)kNbSunSegments;
         k_.sun_row_lo = std::min((int)std::floor(seg), kNbSunSegments - 1);
+        // segment starts inside [lo, hi] (the disc's elevations with the same margin): the
+        // FAST kernels count the ones a direction's elevation has passed instead of taking
+        // cbrt(2 elevation / pi) (sunsky.cpp:579-587).  A start is pi/2 (j / 45)^3, the value
+        // the kernels subtract for x, in fp32 as the kernels form it.
+        const double hi = std::min((double)eta + (double)sun_half_aperture_ + 1e-3, 0.5 * 3.14159265358979323846);
+        int nb = 0;
+        for (int j = k_.sun_row_lo + 1; j < kNbSunSegments; ++j) {
+            const float frac = (float)j * (1.f / (float)kNbSunSegments);
+            const float start = kHalfPi * (frac * frac * frac);
+            if ((double)start > hi) break;
+            if (nb == kSunRowsStaged) { nb = -1; break; }
+            k_.sun_seg_bound[nb++] = start;
+        }
+        k_.sun_seg_nb = nb;
+        for (int k = std::max(nb, 0); k < kSunRowsStaged; ++k) k_.sun_seg_bound[k] = 0.f;
     }
 
     // ---------------- TGMM, sunsky.h:438-501

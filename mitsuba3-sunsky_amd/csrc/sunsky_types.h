@@ -106,6 +106,12 @@ struct SunskyKArgs {
     const float* sun_table;  // device: 45x3x4x6 (RGB) or 45x11x4 (spectral), turbidity-lerped
     const float* sun_ld;     // device: 11x6 limb darkening (spectral only)
     int   sun_row_lo;        // first elevation segment a direction inside the sun disc can reach
+    // Segment search by comparison (FAST sun-disc terms): a disc direction's segment is
+    // sun_row_lo + #{k < sun_seg_nb : elevation >= sun_seg_bound[k]}, the bounds being the
+    // elevations pi/2 (j / 45)^3 of the segment starts j the disc straddles; sun_seg_nb < 0
+    // (a disc over more than kSunRowsStaged segments) keeps the cbrt search.
+    int   sun_seg_nb;
+    float sun_seg_bound[kSunRowsStaged];
     // -------- sky sampling (TGMM + DiscreteDistribution)
     Gaussian gauss[kNbMixture];
     float gauss_cdf[kNbMixture];   // unnormalised inclusive prefix sum

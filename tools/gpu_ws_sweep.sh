@@ -6,4 +6,4 @@ mkdir -p $R/gpurun_out
 export SUNSKY_AMD_DATASET=$R/mitsuba3-sunsky_amd/data/sunsky_datasets.pack
 H=$R/mitsuba3-sunsky_amd/build/sunsky_kernels.hsaco
 O=$R/gpurun_out/ws_sweep.log
-timeout -k 10 200 $R/tools/build/kbench $H sample 67108864 20 ${BPCU:-4,8,16,32,64} sunsky_sample_direction_rgb_lean_fast ${VARIANTS:-sunsky_sample_direction_rgb_ws4_fast sunsky_sample_direction_rgb_ws5_fast sunsky_sample_direction_rgb_ws6_fast} >> $O 2>&1
+timeout -k 10 200 $R/tools/build/kbench $H sample 67108864 20 ${BPCU:-4,8,16,32,64} sunsky_sample_direction_rgb_lean_fast ${VARIANTS:-sunsky_sample_direction_rgb_lean_plain_fast} >> $O 2>&1

@@ -682,6 +682,33 @@ def main():
             if rank == 0:
                 sec[key]["parity"] = parity_c4(smp_s, dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), u, d,
                                                pdf_s, wgt, pdf_q, semantics=sem)
+            if sem == "jit":
+                # the general call a Mitsuba integrator makes (DirectionSample3f with p and dist): it.p
+                # in, ds.p and ds.dist out as well (+28 B per sample); the unsorted general kernel
+                itp = torch.randn((3, ns), generator=g, device=dev)
+                dist_o = torch.empty(ns, dtype=torch.float32, device=dev)
+                pos_o = torch.empty((3, ns), dtype=torch.float32, device=dev)
+                p_in = ss._capi.Vec3In(itp[0].data_ptr(), itp[1].data_ptr(), itp[2].data_ptr())
+                p_out = ss._capi.Vec3Out(pos_o[0].data_ptr(), pos_o[1].data_ptr(), pos_o[2].data_ptr())
+
+                def general_step():
+                    rc = lib.sunsky_sample_direction(smp_s._h, u[0].data_ptr(), u[1].data_ptr(), p_in, None, 0, 0,
+                                                     None, ns, d_out, pdf_s.data_ptr(), dist_o.data_ptr(), p_out,
+                                                     wgt.data_ptr(), ns, stream)
+                    if rc:
+                        raise RuntimeError(lib.sunsky_last_error().decode())
+                general_step()
+                t_g = KernelTimer()
+                t_g.begin()
+                for _ in range(reps):
+                    general_step()
+                t_g.end(reps)
+                ms_g = t_g.mean_ms()
+                sec[key]["sample_direction_general_ms"] = ms_g
+                sec[key]["sample_direction_general_note"] = (
+                    "the same samples with it.p in and ds.p, ds.dist out (64 B per sample), the unsorted general "
+                    "kernel; not part of samples_per_s")
+                del itp, dist_o, pos_o
             del u, d, pdf_s, wgt, pdf_q
             if sem == "jit":
                 smp = smp_s

@@ -64,12 +64,14 @@ int main(int argc, char** argv) {
     props.set_float("albedo", spec || sampling ? 0.3 : 0.1);
     double th = (90.0 - (sampling ? 30.0 : 45.0)) * M_PI / 180.0;
     props.set_vector3("sun_direction", (float)std::sin(th), 0.f, (float)std::cos(th));
-    SunskyModel model(props, spec ? kSpectral : kRGB, kJit, pack_path);
+    // KB_SAMPLE_SPEC=1 (sample mode): the spectral emitter, 4 random wavelengths per sample
+    const bool sspec = mode == "sample" && std::getenv("KB_SAMPLE_SPEC") != nullptr;
+    SunskyModel model(props, spec || sspec ? kSpectral : kRGB, kJit, pack_path);
 
     int cu = 0;
     CK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0));
     float *d_sun, *d_ld;
-    CK(hipMalloc(&d_sun, sizeof(float) * kSunRgbTableSize));
+    CK(hipMalloc(&d_sun, sizeof(float) * std::max(kSunRgbTableSize, kSunSpecTableSize)));
     CK(hipMalloc(&d_ld, sizeof(float) * 66));
     CK(hipMemcpy(d_sun, model.sun_table().data(), sizeof(float) * model.sun_table().size(), hipMemcpyHostToDevice));
     CK(hipMemcpy(d_ld, model.sun_ld().data(), sizeof(float) * 66, hipMemcpyHostToDevice));
@@ -126,7 +128,7 @@ int main(int argc, char** argv) {
         }
         CK(hipMemcpy(wx, u.data(), n * 4, hipMemcpyHostToDevice));
         CK(hipMemcpy(wy, u.data() + n, n * 4, hipMemcpyHostToDevice));
-        CK(hipMalloc(&dd, 3 * n * 4)); CK(hipMalloc(&pdf, n * 4)); CK(hipMalloc(&wgt, 3 * n * 4));
+        CK(hipMalloc(&dd, 3 * n * 4)); CK(hipMalloc(&pdf, n * 4)); CK(hipMalloc(&wgt, 4 * n * 4));
         if (mode == "pdf") {   // directions on the whole sphere
             for (size_t i = 0; i < n; ++i) {
                 float ct = 2 * U(rng) - 1, ph = 2.f * (float)M_PI * U(rng), st = std::sqrt(std::max(0.f, 1 - ct * ct));
@@ -148,6 +150,14 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(cz[c], wz, n * 4, hipMemcpyDeviceToDevice));
     }
     const float* nullf = nullptr;
+    int nl4 = 4;
+    float* lamp = nullptr;
+    if (sspec) {
+        std::vector<float> l(4 * n);
+        for (auto& v : l) v = 360.f + 360.f * U(rng);
+        CK(hipMalloc(&lamp, 4 * n * 4));
+        CK(hipMemcpy(lamp, l.data(), 4 * n * 4, hipMemcpyHostToDevice));
+    }
     const bool full = std::getenv("KB_SAMPLE_FULL") != nullptr;
     const float *fpx = nullptr, *fpy = nullptr, *fpz = nullptr;
     float *fdist = nullptr, *fox = nullptr, *foy = nullptr, *foz = nullptr;
@@ -174,7 +184,8 @@ int main(int argc, char** argv) {
             unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((items + 255) / 256, (size_t)cu * mult));
             void* args_rgb[] = {&K, &wx, &wy, &wz, &active, &n, &out, &ostride, &sign};
             void* args_spec[] = {&K, &L, &wx, &wy, &wz, &active, &n, &out, &ostride, &sign};
-            void* args_sample[] = {&K, &wx, &wy, &nullf, &nullf, &nullf, &nullf, &zero, &nl0, &active, &n,
+            void* args_sample[] = {&K, &wx, &wy, &nullf, &nullf, &nullf, sspec ? (void*)&lamp : (void*)&nullf,
+                                   sspec ? (void*)&n : (void*)&zero, sspec ? (void*)&nl4 : (void*)&nl0, &active, &n,
                                    &dd, &ddy, &ddz, &pdf, &nullo, &nullo, &nullo, &nullo, &wgt, &n};
             // KB_SAMPLE_FULL=1: the general call, it.p in, ds.dist and ds.p out (Mitsuba's DirectionSample)
             void* args_sample_full[] = {&K, &wx, &wy, &fpx, &fpy, &fpz, &nullf, &zero, &nl0, &active, &n,

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the ws2/ws3/ws4 spectral variants were removed after this measurement: profiles/r02_v17_ab_spec_sorted_reverted.log)
 # Spectral wave-sorted sample_direction variants (R = 2, 3, 4) vs the spectral LEAN kernel,
 # 64M samples x 4 wavelengths (kbench KB_SAMPLE_SPEC): bitwise check + interleaved A/B.
 set -o pipefail

@@ -38,7 +38,8 @@ def test_eval_and_sampling_replay_bitwise(variant):
         e = em.eval(si)
         ds, w = em.sample_direction(it, u)
         p = em.pdf_direction(it, ds)
-        return e, ds.d, ds.pdf, w, p
+        dl, wl = em.sample_direction(it, u, positions=False)   # the LEAN (RGB: wave-sorted) kernel
+        return e, ds.d, ds.pdf, w, p, dl.d, dl.pdf, wl
 
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())

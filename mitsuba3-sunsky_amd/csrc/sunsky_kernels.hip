@@ -1624,6 +1624,58 @@ __device__ __forceinline__ float mis_power(float a, float b) {
     return isfinite(w) ? w : 0.f;
 }
 
+// The emitter-sampling half of one direct_diffuse sample, RGB (path.cpp:204-228): the
+// factor and the weight of `acc += scale * w`; scale = w = 0 where the reference adds
+// nothing (occluded, pdf 0, below the surface): fma(0, 0, acc) is acc.
+template <bool FAST>
+__device__ __forceinline__ void dd_emitter_rgb(const SunskyKArgs& K, const SamplerLds<FAST, false>& S, float3_ nrm,
+                                               float u0, float u1, unsigned v, float inv_w, float inv_w_sun,
+                                               float* scale, float w[3]) {
+    const bool pick_sky = u0 < K.w_sky;
+    const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, u0, u1, inv_w, inv_w_sun);
+    const bool act = sd.z >= 0.f;
+    const float3_ d = to_world(K, sd);
+    float skyp, sunp;
+    compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+    const float pd = lerpf_(sunp, skyp, K.w_sky);
+    const float cos_em = dot3(nrm, d);
+    *scale = 0.f;
+    w[0] = w[1] = w[2] = 0.f;
+    if ((v & 1u) && pd != 0.f && cos_em > 0.f) {
+        const float bpdf = kInvPi * cos_em;     // diffuse eval / pdf: rho / pi cos, cos / pi
+        *scale = bpdf * mis_power<FAST>(pd, bpdf);
+        float e[3];
+        eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, to_local(K, d), act, e, S.rows);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float x = e[c] / pd;
+            w[c] = isfinite(x) ? x : 0.f;
+        }
+    }
+}
+
+// The BSDF-sampling half, RGB (path.cpp:176-196): square_to_cosine_hemisphere, the miss,
+// pdf_direction of the escaped ray and the power-heuristic MIS, accumulated into acc.
+template <bool FAST>
+__device__ __forceinline__ void dd_bsdf_rgb(const SunskyKArgs& K, const SamplerLds<FAST, false>& S, float3_ nrm,
+                                            float3_ fs, float3_ ft, float u2, float u3, unsigned v, float acc[3]) {
+    float px, py;
+    disk_concentric_dev<FAST>(u2, u3, &px, &py);
+    const float lz = safe_sqrt_sel<FAST>(1.f - fmaf(px, px, py * py));
+    const float bpdf = kInvPi * lz;
+    if ((v & 2u) && bpdf > 0.f) {
+        const float3_ dw = frame_to_world(fs, ft, nrm, mk3(px, py, lz));
+        const float3_ wo = to_local(K, dw);
+        float bskyp, bsunp;
+        compute_pdfs<FAST>(K, S.tgmm, wo, true, true, &bskyp, &bsunp);
+        const float mis = mis_power<FAST>(bpdf, lerpf_(bsunp, bskyp, K.w_sky));
+        float e[3];
+        eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, wo, wo.z >= 0.f, e, S.rows);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) acc[c] = fmaf(e[c], mis, acc[c]);
+    }
+}
+
 // The sky-and-sun lighting of an unoccluded diffuse point, as the path
 // integrator gathers it in one vertex (src/integrators/path.cpp:176-250 with
 // the smooth diffuse BSDF of src/bsdfs/diffuse.cpp:100-180, the sun/sky the
@@ -1675,6 +1727,14 @@ __device__ __forceinline__ void direct_diffuse_body(
             const float u0 = rng.next_float(), u1 = rng.next_float();
             const float u2 = rng.next_float(), u3 = rng.next_float();
             const unsigned v = vis ? (unsigned)vis[(size_t)smp * vstride + i] : 3u;
+            if constexpr (!SPEC) {
+                float scale, w[3];
+                dd_emitter_rgb<FAST>(K, S, nrm, u0, u1, v, inv_w, inv_w_sun, &scale, w);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) acc[c] = fmaf(scale, w[c], acc[c]);
+                dd_bsdf_rgb<FAST>(K, S, nrm, fs, ft, u2, u3, v, acc);
+                continue;
+            }
             // ---- emitter sampling: sample_direction (sunsky.cpp:399-441)
             const bool pick_sky = u0 < K.w_sky;
             float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, u0, u1, inv_w, inv_w_sun);
@@ -1688,15 +1748,7 @@ __device__ __forceinline__ void direct_diffuse_body(
                 const float bpdf = kInvPi * cos_em;     // diffuse eval / pdf: rho / pi cos, cos / pi
                 const float scale = bpdf * mis_power<FAST>(pd, bpdf);
                 const float3_ wo = to_local(K, d);
-                if constexpr (!SPEC) {
-                    float e[3];
-                    eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, wo, act, e, S.rows);
-#pragma unroll
-                    for (int c = 0; c < 3; ++c) {
-                        const float w = e[c] / pd;
-                        acc[c] = fmaf(scale, isfinite(w) ? w : 0.f, acc[c]);
-                    }
-                } else {
+                {
                     DirTerms t = dir_terms<FAST>(K, wo, act);
                     add_sun_terms<FAST>(K, t);
 #pragma unroll

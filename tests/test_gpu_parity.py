@@ -464,6 +464,72 @@ def test_full_size_rgb_16M_against_oracle():
         assert np.all(np.isfinite(out))
 
 
+def test_full_size_c3_spectral_16M_x11_against_oracle():
+    """BASELINE config 3 at full size: 16,777,216 directions x the 11 model wavelengths through
+    the C3 node kernel (T = 3, albedo 0.3), every (direction, lambda) lane against the oracle at
+    the DESIGN.md §6 bar."""
+    n = 1 << 24
+    wo = hemisphere_wo(n, seed=1)
+    d = angles_dict(3.0, 0.0, np.deg2rad(45), 0.3, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, "spectral")
+    nodes = [float(x) for x in range(320, 721, 40)]
+    out = host(em.eval_spectral_broadcast(soa(-wo), nodes))          # (11, n)
+    o32, o64 = O.Oracle(d, "spectral", "jit", "f32"), O.Oracle(d, "spectral", "jit", "f64")
+    lam = np.repeat(np.asarray(nodes, np.float32)[:, None], n, 1)
+    sm = sun_mask(o32, wo)
+    assert sm.sum() > 50
+    a = o32.eval(-wo, lam)
+    b = o64.eval(-wo, lam)
+    del lam
+    st = assert_parity(out.T, a.T, b.T, sm)
+    print(f"C3 full size: sky max rel vs o32 {st['sky_max_rel_vs_o32']:.2e}, "
+          f"sun max rel vs o64 {st['sun_max_rel_vs_o64']:.2e} (o32 itself {st['sun_o32_max_rel_vs_o64']:.2e})")
+    assert np.all(np.isfinite(out))
+
+
+def test_full_size_c4_sampling_64M():
+    """BASELINE config 4 at full size: 67,108,864 samples through the wave-sorted LEAN
+    sample_direction and pdf_direction (T = 3, albedo 0.3, sun elevation 30 deg).  On all
+    samples: finite outputs, unit directions, and pdf_direction(d) == the sampled pdf wherever
+    the reference evaluates the same formula (sky picks, sun picks inside the cone); on every
+    64th sample: directions, pdf and weights against the oracle's sampler on the same u."""
+    n = 1 << 26
+    d_scene = dict(angles_dict(3.0, 0.0, np.deg2rad(60), 0.3, 1.0, 1.0))
+    em = ss.SunskyEmitter(d_scene, "rgb")
+    g = torch.Generator(device="cuda").manual_seed(99)
+    u = torch.rand((2, n), generator=g, device="cuda")
+    ds, w = em.sample_direction(ss.Interaction3f(), u, positions=False)
+    pq = em.pdf_direction(ss.Interaction3f(), ds)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(w).all()) and bool(torch.isfinite(ds.pdf).all()) and bool((ds.pdf >= 0).all())
+    norm = ds.d.double().norm(dim=0)
+    assert float((norm - 1).abs().max()) < 1e-5
+    info = O.Oracle(d_scene, "rgb", "jit", "f32").info()
+    sdir = torch.tensor(info["sun_dir_local"], dtype=torch.float32, device="cuda")
+    inside = (sdir[:, None] * ds.d).sum(0) >= info["cos_cutoff"]
+    same = (u[0] < em.sky_sampling_w) | inside
+    rel = ((ds.pdf - pq).abs() / pq.abs().clamp_min(1e-6 * float(pq.max())))[same]
+    assert float(rel.max()) < 1e-6, float(rel.max())
+    # strided subsample against the oracle (bench.py parity_c4's bars)
+    idx = torch.arange(0, n, 64, device="cuda")
+    uh = u[:, idx].T.cpu().numpy()
+    gd, gp, gw = host(ds.d[:, idx]).T, host(ds.pdf[idx]), host(w[:, idx]).T
+    o32, o64 = O.Oracle(d_scene, "rgb", "jit", "f32"), O.Oracle(d_scene, "rgb", "jit", "f64")
+    o32.override_w_sky(em.sky_sampling_w)
+    o64.override_w_sky(em.sky_sampling_w)
+    ref = o32.sample_direction(uh)
+    derr = np.abs(gd - ref["d"]).max(axis=1)
+    assert derr.max() < 1e-4 and np.quantile(derr, 0.999) < 2e-6, (derr.max(), np.quantile(derr, 0.999))
+    ins = gd @ info["sun_dir_local"] >= info["cos_cutoff"]
+    sm_same = (uh[:, 0] < em.sky_sampling_w) | ins
+    pref = o32.pdf_direction(gd)
+    assert max_rel(gp[sm_same], pref[sm_same]) < 1e-5
+    up = gd[:, 2] >= 0
+    w32 = (o32.eval(-gd) / gp[:, None]).astype(np.float32)
+    w64 = o64.eval(-gd) / gp[:, None].astype(np.float64)
+    assert_parity(gw[up], w32[up], w64[up], ins[up], rtol=2e-5)
+
+
 def test_batches_beyond_int32_indices():
     """Maximum sizes: 2^31 + 4099 lanes (element indices and byte offsets past 2^31, a
     ragged VEC=1 tail) for eval (RGB), sample_direction (LEAN) and pdf_direction.  The

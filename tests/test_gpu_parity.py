@@ -257,6 +257,9 @@ def test_wave_sorted_rgb_kernels_bitwise_vs_unsorted(precision, monkeypatch):
     rng = np.random.default_rng(11)
     special = np.array([w, np.nextafter(w, 0, dtype=np.float32), np.nextafter(w, 1, dtype=np.float32), 0.0,
                         np.nextafter(np.float32(1), 0, dtype=np.float32)], np.float32)
+    # out-of-range samples the reference does not guard against: both kernels must still agree
+    odd = np.array([[np.nan, 0.5], [-0.0, 0.3], [-1e-30, 0.7], [1.0, 0.2], [1.5, 0.9], [np.inf, 0.1],
+                    [0.2, np.nan], [0.9, -0.25], [0.1, 1.0], [0.6, 0.0]], np.float32)
 
     def run(ut, it, mask, positions):
         ds, wt = em.sample_direction(it, ut, active=mask, positions=positions)
@@ -269,6 +272,7 @@ def test_wave_sorted_rgb_kernels_bitwise_vs_unsorted(precision, monkeypatch):
         if n >= 2048:
             u[256:512, 0] *= w          # an all-sky window
             u[512:768, 0] = w + (1 - w) * u[512:768, 0]   # an all-sun window
+            u[1000:1010] = odd
         ut = soa(u)
         p = torch.from_numpy(rng.normal(size=(3, n)).astype(np.float32) * 10).cuda()
         mask = torch.from_numpy(rng.random(n) < 0.8).cuda()

@@ -712,6 +712,53 @@ def main():
             del u, d, pdf_s, wgt, pdf_q
             if sem == "jit":
                 smp = smp_s
+        # the spectral variant's sampling call (Mitsuba Spectrum<Float, 4>: 4 wavelengths per sample),
+        # LEAN (d, pdf, 4 weights) + pdf_direction; parity: tests/test_gpu_parity.py (spectral sampling)
+        smp_sp = ss.SunskyEmitter(dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), "spectral", precision=args.precision,
+                                  device=dev)
+        g_sp = torch.Generator(device=dev)
+        g_sp.manual_seed(199 + rank)
+        u_sp = torch.rand((2, ns), generator=g_sp, device=dev)
+        lam_sp = 360.0 + 360.0 * torch.rand((4, ns), generator=g_sp, device=dev)
+        d_sp = torch.empty((3, ns), dtype=torch.float32, device=dev)
+        p_sp = torch.empty(ns, dtype=torch.float32, device=dev)
+        w_sp = torch.empty((4, ns), dtype=torch.float32, device=dev)
+        q_sp = torch.empty(ns, dtype=torch.float32, device=dev)
+        dsp_out = ss._capi.Vec3Out(d_sp[0].data_ptr(), d_sp[1].data_ptr(), d_sp[2].data_ptr())
+        dsp_in = ss._capi.Vec3In(d_sp[0].data_ptr(), d_sp[1].data_ptr(), d_sp[2].data_ptr())
+        nul_in = ss._capi.Vec3In(None, None, None)
+        nul_out = ss._capi.Vec3Out(None, None, None)
+
+        def spec_sample_step():
+            rc = lib.sunsky_sample_direction(smp_sp._h, u_sp[0].data_ptr(), u_sp[1].data_ptr(), nul_in,
+                                             lam_sp.data_ptr(), 4, ns, None, ns, dsp_out, p_sp.data_ptr(), None,
+                                             nul_out, w_sp.data_ptr(), ns, stream)
+            if rc:
+                raise RuntimeError(lib.sunsky_last_error().decode())
+
+        def spec_pdf_step():
+            rc = lib.sunsky_pdf_direction(smp_sp._h, dsp_in, None, ns, q_sp.data_ptr(), stream)
+            if rc:
+                raise RuntimeError(lib.sunsky_last_error().decode())
+
+        spec_sample_step()
+        spec_pdf_step()
+        t_ss, t_sq = KernelTimer(), KernelTimer()
+        t_ss.begin()
+        for _ in range(reps):
+            spec_sample_step()
+        t_ss.end(reps)
+        t_sq.begin()
+        for _ in range(reps):
+            spec_pdf_step()
+        t_sq.end(reps)
+        ms_ss, ms_sq = t_ss.mean_ms(), t_sq.mean_ms()
+        sec["sampling_C4_spectral_4lambda"] = {
+            "samples_per_s": ns / ((ms_ss + ms_sq) * 1e-3), "sample_direction_ms": ms_ss, "pdf_direction_ms": ms_sq,
+            "samples": ns, "achieved_GBps": (8 + 16 + 12 + 4 + 16 + 12 + 4) * ns / ((ms_ss + ms_sq) * 1e-3) / 1e9,
+            "note": "spectral emitter, C4 sun: sample_direction with 4 per-sample wavelengths (reads u + 4 lambda, "
+                    "writes d, pdf, 4 weights; the unsorted LEAN kernel) + pdf_direction"}
+        del u_sp, lam_sp, d_sp, p_sp, w_sp, q_sp
         # caller (§8f row 4): direct sun+sky light at 16M diffuse points x 4 spp, emitter + BSDF
         # sampling with MIS fused in one kernel (sunsky_direct_diffuse); reads 12 B normal, writes 12 B RGB
         npts, spp = n, 4

@@ -290,18 +290,21 @@ def parity_c3(em, d_scene, wi, out, n_check=1 << 19, n_sun=1 << 13):
     return dict(st, checked_dirs=wi_all.shape[0], kernel="sunsky_eval_spec_nodes_v4")
 
 
-def parity_c4(em, d_scene, u, d, pdf_s, wgt, pdf_q, n_check=1 << 19, semantics="jit"):
+def parity_c4(em, d_scene, u, d, pdf_s, wgt, pdf_q, n_check=1 << 19, semantics="jit", lam=None):
     """C4 parity on the first n_check samples: directions vs the oracle's sampler on the
-    same u, and pdf / pdf_direction / weight at the GPU's own directions."""
+    same u, and pdf / pdf_direction / weight at the GPU's own directions.  lam: the
+    spectral variant's (4, n) per-sample wavelengths (RGB when None)."""
     O = _oracle()
-    o32, o64 = O.Oracle(d_scene, "rgb", semantics, "f32"), O.Oracle(d_scene, "rgb", semantics, "f64")
+    variant = "rgb" if lam is None else "spectral"
+    o32, o64 = O.Oracle(d_scene, variant, semantics, "f32"), O.Oracle(d_scene, variant, semantics, "f64")
     o32.override_w_sky(em.sky_sampling_w)
     o64.override_w_sky(em.sky_sampling_w)
     uh = u[:, :n_check].T.cpu().numpy()
     gd = d[:, :n_check].T.cpu().numpy()
     gp, gq = pdf_s[:n_check].cpu().numpy(), pdf_q[:n_check].cpu().numpy()
     gw = wgt[:, :n_check].T.cpu().numpy()
-    ref = o32.sample_direction(uh)
+    lh = None if lam is None else lam[:, :n_check].cpu().numpy()
+    ref = o32.sample_direction(uh, wavelengths=lh)
     derr = np.abs(gd - ref["d"]).max(axis=1)
     inf = o32.info()
     inside = gd @ inf["sun_dir_local"] >= inf["cos_cutoff"]
@@ -310,11 +313,14 @@ def parity_c4(em, d_scene, u, d, pdf_s, wgt, pdf_q, n_check=1 << 19, semantics="
     floor = 1e-6 * np.abs(pref).max()
     rel_p = np.abs(gp[same] - pref[same]) / np.maximum(np.abs(pref[same]), floor)
     rel_q = np.abs(gq - pref) / np.maximum(np.abs(pref), floor)
-    w32 = (o32.eval(-gd) / gp[:, None]).astype(np.float32)
-    w64 = o64.eval(-gd) / gp[:, None].astype(np.float64)
+    e32, e64 = o32.eval(-gd, lh), o64.eval(-gd, lh)
+    if lh is not None:
+        e32, e64 = e32.T, e64.T
+    w32 = (e32 / gp[:, None]).astype(np.float32)
+    w64 = e64 / gp[:, None].astype(np.float64)
     up = gd[:, 2] >= 0
     st = lane_stats(gw[up], w32[up], w64[up], inside[up], rtol=2e-5)
-    return {"checked_samples": n_check, "dir_max_abs_delta": float(derr.max()),
+    return {"checked_samples": n_check, "variant": variant, "dir_max_abs_delta": float(derr.max()),
             "dir_p999_abs_delta": float(np.quantile(derr, 0.999)),
             "pdf_max_rel_vs_o32": float(rel_p.max()), "pdf_direction_max_rel_vs_o32": float(rel_q.max()),
             "weight": st, "pass": bool(derr.max() < 1e-4 and rel_p.max() < 1e-5 and rel_q.max() < 1e-5
@@ -758,6 +764,9 @@ def main():
             "samples": ns, "achieved_GBps": (8 + 16 + 12 + 4 + 16 + 12 + 4) * ns / ((ms_ss + ms_sq) * 1e-3) / 1e9,
             "note": "spectral emitter, C4 sun: sample_direction with 4 per-sample wavelengths (reads u + 4 lambda, "
                     "writes d, pdf, 4 weights; the unsorted LEAN kernel) + pdf_direction"}
+        if rank == 0:
+            sec["sampling_C4_spectral_4lambda"]["parity"] = parity_c4(
+                smp_sp, dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), u_sp, d_sp, p_sp, w_sp, q_sp, lam=lam_sp)
         del u_sp, lam_sp, d_sp, p_sp, w_sp, q_sp
         # caller (§8f row 4): direct sun+sky light at 16M diffuse points x 4 spp, emitter + BSDF
         # sampling with MIS fused in one kernel (sunsky_direct_diffuse); reads 12 B normal, writes 12 B RGB

@@ -277,6 +277,23 @@ class Oracle:
         f.argtypes = [C.c_void_p, C.c_double]
         f(self._h, float(w_sky))
 
+    def override_spectral_distr(self, pdf):
+        """Adopt the product's staged wavelength-distribution nodes (sunsky.cpp:870-885) and
+        rebuild the CDF with the oracle's compute_cdf (distr_1d.h:513-585), so wavelength
+        sampling parity isolates the kernels from the independently staged quadrature."""
+        pdf = np.ascontiguousarray(pdf, dtype=np.float64)
+        f = self._fn("override_spectral_distr")
+        f.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+        if f(self._h, _ptr(pdf), int(pdf.size)) != 0:
+            raise ValueError(lib().oracle_last_error().decode())
+
+    def adopt_sampling_state(self, em):
+        """Adopt everything the product stages from its own quadrature that sampling reads:
+        w_sky and (spectral) the wavelength distribution's nodes.  em: a sunsky_amd emitter."""
+        self.override_w_sky(em.sky_sampling_w)
+        if self.spectral:
+            self.override_spectral_distr(em.table("spectral_pdf"))
+
     def hw_sun_radiance(self, turbidity, wavelength, elevation, gamma):
         return self._fn("hw_sun_radiance")(self._h, turbidity, wavelength, elevation, gamma)
 

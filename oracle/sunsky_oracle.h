@@ -103,6 +103,10 @@ void oracle_sun_coordinates(int year, int month, int day, float hour, float minu
                            R *weight);                                                           \
     /* test hook: adopt another implementation's staged sky/sun sampling weight */             \
     void oracle_override_w_sky_##SFX(oracle_##SFX *o, double w_sky);                            \
+    /* test hook: adopt another implementation's staged wavelength-distribution nodes (the    \
+       pdf values of sunsky.cpp:870-885) and rebuild the CDF from them (distr_1d.h:513-585);  \
+       returns 0, or 1 if size is not 2..10 or a value is negative / not finite */            \
+    int oracle_override_spectral_distr_##SFX(oracle_##SFX *o, const double *pdf, int size);    \
     /* HW solar radiance (restates ArHosekSkyModel.c:686-784 on the packed tables) */          \
     R oracle_hw_sun_radiance_##SFX(const oracle_##SFX *o, R turbidity, R wavelength,            \
                            R elevation, R gamma);

@@ -128,3 +128,26 @@ def assert_parity(gpu, o32, o64, sunlanes, rtol=1e-5):
     st = parity_stats(gpu, o32, o64, sunlanes)
     print("parity", {k: (f"{v:.3e}" if isinstance(v, float) else v) for k, v in st.items()})
     return st
+
+
+def lambda_pdf(o, lam):
+    """ContinuousDistribution::eval_pdf_normalized (distr_1d.h:428-446) of the oracle's
+    wavelength distribution over [360, 720] at lam, in fp64 (nodes and integral from the
+    oracle, after it adopted the product's nodes)."""
+    inf = o.info()
+    y = inf["spec_pdf"].astype(np.float64)
+    x = (np.asarray(lam, np.float64) - 360.0) / (360.0 / (y.size - 1))
+    i = np.clip(np.floor(x).astype(int), 0, y.size - 2)
+    t = x - i
+    return (y[i] + t * (y[i + 1] - y[i])) / inf["spec_integral"]
+
+
+def assert_lambda_parity(lam_g, lam_o):
+    """Same sample, same wavelength: every lane within 1e-5 relative of the fp32 oracle that
+    adopted the product's nodes (the product and the oracle invert the same CDF with the same
+    fp32 operations, so in practice the wavelengths are equal bit for bit)."""
+    rel = np.abs(lam_g.astype(np.float64) - lam_o) / np.abs(lam_o)
+    assert rel.max() <= 1e-5, (rel.max(), np.argmax(rel))
+    same = float(np.mean(lam_g == lam_o.astype(np.float32)))
+    print(f"lambda: max rel {rel.max():.3e}, bitwise equal {same:.6f}")
+    return same

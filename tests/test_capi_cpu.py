@@ -63,6 +63,24 @@ def test_host_staging_matches_oracle(variant, semantics, d):
     assert inf["flags"] == (0x04 | 0x10)
 
 
+@pytest.mark.parametrize("variant,semantics,d", [c for c in CASES if c[0] == "spectral"])
+def test_adopted_spectral_nodes_rebuild_the_products_cdf(variant, semantics, d):
+    """The oracle adopts the product's wavelength-distribution nodes (sunsky.cpp:870-885) and
+    rebuilds the CDF with its own compute_cdf restatement (distr_1d.h:513-585): the result
+    equals the product's staged CDF bit for bit, so the GPU wavelength-sampling tests compare
+    the sampling kernels alone."""
+    em = ss.SunskyEmitter(d, variant=variant, semantics=semantics, device="host")
+    o = O.Oracle(d, variant, semantics, "f32")
+    o.override_spectral_distr(em.table("spectral_pdf"))
+    inf = o.info()
+    np.testing.assert_array_equal(inf["spec_pdf"].astype(np.float32), em.table("spectral_pdf"))
+    np.testing.assert_array_equal(inf["spec_cdf"].astype(np.float32), em.table("spectral_cdf"))
+    with pytest.raises(ValueError, match="spectral pdf"):
+        o.override_spectral_distr(np.array([1.0, -1.0]))
+    with pytest.raises(ValueError, match="size"):
+        o.override_spectral_distr(np.ones(11))
+
+
 def test_parameter_errors_match_reference_messages():
     with pytest.raises(ValueError, match="Turbidity value"):
         ss.SunskyEmitter({"turbidity": 0.5}, device="host")

@@ -804,11 +804,15 @@ def main():
     if args.gather and world > 1:
         # configs[4]'s final step: the radiance shards gathered to rank 0 through the C ABI's
         # RCCL gather (sunsky_gather_radiance); reported beside `value`, never in it.
+        # One communicator (cached per group and device) and one untimed gather first, so the
+        # timed call is the transfer, not RCCL init and connection setup.
         from sunsky_amd.sharding import gather_radiance
+        src = outs[0] if not rehearsal else outs[0].cpu()
+        full = gather_radiance(src, n * world)
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        full = gather_radiance(outs[0] if not rehearsal else outs[0].cpu(), n * world)
+        full = gather_radiance(src, n * world, out=full)
         torch.cuda.synchronize()
         gt = time.perf_counter() - t0
         if rank == 0:
@@ -842,6 +846,7 @@ def main():
             c5 = run_c5(args, world, rank, dev, coll_dev, rehearsal)
         except Exception as exc:   # reported beside `value`; never fail the bench line
             c5 = {"error": f"{type(exc).__name__}: {exc}"}
+        watchdog.cancel()          # C5 is over: a slow cpu_baseline / teardown is not a C5 timeout
         if rank == 0:
             result["c5_spectral_shard_gather"] = c5
 

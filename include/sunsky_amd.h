@@ -153,7 +153,13 @@ int sunsky_emitter_get_param(const sunsky_emitter *e, const char *name, float *o
  * kernels on `stream`, writing the emitter's device state in place.  Batch calls on
  * `stream` after this one see the new state; the call does not wait for the device.
  * Work on other streams must be ordered by the caller (the reference's contract:
- * parameters_changed is not concurrent with rendering).  Capturable in a hipGraph. */
+ * parameters_changed is not concurrent with rendering).  Not capturable: called on a
+ * stream that is capturing a hipGraph it returns SUNSKY_ERROR_INVALID_VALUE and changes
+ * nothing (update outside the capture; captured batch calls read the current state).
+ * An update the device staging rejects (a negative wavelength-distribution node, as
+ * ContinuousDistribution's constructor checks) is reported by the next call that reads
+ * the state back (get_info / get_table / the blocking form), which restores and restages
+ * the previous parameters. */
 int sunsky_emitter_parameters_changed_async(sunsky_emitter *e, void *stream);
 /* Blocking form: _async on the default (null) stream, then waits for the staging. */
 int sunsky_emitter_parameters_changed(sunsky_emitter *e);

@@ -292,6 +292,7 @@ struct sunsky_emitter {
     hipEvent_t ring_ev[kRing] = {};
     bool ring_used[kRing] = {};
     int ring_i = 0;
+    bool restoring = false;                    // restaging the previous state after a rejection
     mutable hipEvent_t stage_done = nullptr;   // recorded after the last device staging
     mutable float* d_jvp = nullptr;   // eval_jvp tangent tables (layout: sunsky_kernels.hip)
     mutable float* d_vjp = nullptr;   // eval_vjp basis-tangent tables
@@ -407,6 +408,8 @@ struct sunsky_emitter {
             hip_check(hipModuleLaunchKernel(mod->quad_finish, 1, 1, 1, 256, 1, 1, 0, s, qargs, nullptr),
                       "hipModuleLaunchKernel(sunsky_stage_quad_finish)");
         }
+        if (const char* f = std::getenv("SUNSKY_AMD_FAULT_STAGE_STATUS"))   // test fault injection
+            if (*f == '1' && model->semantics() == kJit && !restoring) hip_check(hipMemsetAsync(d_status, 1, 1, s), "hipMemsetAsync");
         hip_check(hipEventRecord(stage_done, s), "hipEventRecord");
         ++rev;
     }
@@ -423,8 +426,30 @@ struct sunsky_emitter {
         hip_check(hipMemcpy(st.data(), d_sun_table, sizeof(float) * st.size(), hipMemcpyDeviceToHost), "hipMemcpy");
         int status = 0;
         hip_check(hipMemcpy(&status, d_status, sizeof(int), hipMemcpyDeviceToHost), "hipMemcpy");
-        model->adopt_device_stage(dk, st.data());
         auto* self = const_cast<sunsky_emitter*>(this);
+        if (status) {
+            // The device staging rejected the update (a negative wavelength-distribution
+            // node, the check of ContinuousDistribution's constructor).  As the reference
+            // throws from parameters_changed and keeps its old state: restore the previous
+            // committed parameters, restage them, and report the error once, here.
+            hip_check(hipMemset(d_status, 0, sizeof(int)), "hipMemset");
+            if (restoring)   // the restored state itself is rejected (e.g. at creation)
+                throw std::runtime_error("ContinuousDistribution: entries must be non-negative!");
+            model->revert_last_commit();
+            self->restoring = true;
+            try {
+                self->stage_async(nullptr);
+                hip_check(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
+                sync_host();
+            } catch (...) {
+                self->restoring = false;
+                throw;
+            }
+            self->restoring = false;
+            throw std::runtime_error("ContinuousDistribution: entries must be non-negative! (update rejected by the "
+                                     "device staging; the previous parameters were restored)");
+        }
+        model->adopt_device_stage(dk, st.data());
         const SunskyKArgs& hk = model->kargs();
         std::memcpy(self->kargs.sky, hk.sky, sizeof(hk.sky));
         std::memcpy(self->kargs.fsky, hk.fsky, sizeof(hk.fsky));
@@ -436,7 +461,6 @@ struct sunsky_emitter {
         self->kargs.spec_norm = hk.spec_norm;
         self->kargs.spec_interval = hk.spec_interval;
         self->kargs.spec_inv_interval = hk.spec_inv_interval;
-        if (status) throw std::runtime_error("ContinuousDistribution: entries must be non-negative!");
     }
 
     hipFunction_t fn(KernelId k) const {
@@ -585,6 +609,18 @@ int sunsky_emitter_parameters_changed_async(sunsky_emitter* e, void* stream) {
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     return guarded([&] {
         const bool gpu = e->device >= 0;
+        if (gpu) {
+            // The update is a host + stream operation (pinned-image copy, events), not a
+            // graph node: refuse it during capture before anything is committed or queued.
+            DeviceScope g(e->device);
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            hip_check(hipStreamIsCapturing((hipStream_t)stream, &cs), "hipStreamIsCapturing");
+            if (cs != hipStreamCaptureStatusNone) {
+                e->model->discard_pending();
+                throw std::invalid_argument("parameters_changed cannot be captured into a hipGraph: update the "
+                                            "emitter outside the capture (a captured graph reads the current state)");
+            }
+        }
         e->model->parameters_changed(/*radiance_on_host=*/!gpu);   // keeps the scene bounding sphere
         if (gpu) {
             DeviceScope g(e->device);
@@ -624,6 +660,9 @@ int sunsky_emitter_set_scene(sunsky_emitter* e, int bbox_valid, const float cent
             static_assert(offsetof(SunskyKArgs, bs_radius) == offsetof(SunskyKArgs, bs_center) + 3 * sizeof(float),
                           "bounding sphere layout");
             float bs[4] = {k.bs_center[0], k.bs_center[1], k.bs_center[2], k.bs_radius};
+            // a staging still queued on another stream copies the whole state block (with
+            // the old sphere): let it land first, then write the sphere in place
+            hip_check(hipEventSynchronize(e->stage_done), "hipEventSynchronize");
             hip_check(hipMemcpy((char*)e->d_state + offsetof(SunskyKArgs, bs_center), bs, sizeof(bs),
                                 hipMemcpyHostToDevice), "hipMemcpy");
         }

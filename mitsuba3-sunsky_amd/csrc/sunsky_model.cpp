@@ -272,6 +272,7 @@ SunskyModel::SunskyModel(const Properties& props, int variant, int semantics, co
     k_.bs_center[0] = k_.bs_center[1] = k_.bs_center[2] = 0.f;   // unit bounding sphere until set_scene
     k_.bs_radius = 1.f;
     commit();
+    previous_ = committed_;   // nothing before the construction to go back to
 
     std::vector<std::string> unq = props.unqueried();
     if (!unq.empty()) {
@@ -779,6 +780,7 @@ void SunskyModel::parameters_changed(bool radiance_on_host) {
 }
 
 void SunskyModel::commit() {
+    previous_ = committed_;
     Snapshot& c = committed_;
     c.turbidity = turbidity_; c.sky_scale = sky_scale_; c.sun_scale = sun_scale_;
     c.albedo = albedo_; c.time = time_; c.location = location_;
@@ -806,6 +808,11 @@ void SunskyModel::rollback() {
     k_ = c.k;
     k_.bs_center[0] = bs[0]; k_.bs_center[1] = bs[1]; k_.bs_center[2] = bs[2]; k_.bs_radius = bs[3];
     radiance_stale_ = c.radiance_stale;
+}
+
+void SunskyModel::revert_last_commit() {
+    committed_ = previous_;
+    rollback();
 }
 
 int SunskyModel::get_param(const std::string& name, float* out, int cap) const {

@@ -77,6 +77,11 @@ public:
     int semantics() const { return semantics_; }
     bool radiance_stale() const { return radiance_stale_; }
     void adopt_device_stage(const SunskyKArgs& device_kargs, const float* sun_table);
+    // The device staging rejected the last committed update: make the commit before it the
+    // committed state again and restore it (the caller restages the device).
+    void revert_last_commit();
+    // Drop parameter values set since the last commit (an update refused before staging).
+    void discard_pending() { rollback(); }
     static void quadrature_nodes(std::vector<float>* x, std::vector<float>* w);
     // Tangent of the eval tables for param (JvpParam) along `tangent`
     // (turbidity: 1 value; albedo: 1 or nch; sun_direction: 3, world space).
@@ -126,7 +131,7 @@ private:
         SunskyKArgs k;
         bool radiance_stale;
     };
-    Snapshot committed_;
+    Snapshot committed_, previous_;
     void commit();
     void rollback();
 };

@@ -60,14 +60,29 @@ def gather_shards(local, n_total, dst=0, group=None, bufs=None):
     return bufs if rank == dst else None
 
 
-def gather_radiance(local, n_total, dst=0, group=None, comm=None):
+_COMMS = {}
+
+
+def radiance_comm(group=None, device=None):
+    """The process's RadianceComm for (group, device), created on first use and kept: a
+    communicator costs an RCCL init plus connection setup, far more than one gather.
+    Collective on first use (every rank of the group calls it)."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    key = (id(group) if group is not None else None, dev.index)
+    comm = _COMMS.get(key)
+    if comm is None or comm._h is None:
+        comm = _COMMS[key] = RadianceComm(group, dev)
+    return comm
+
+
+def gather_radiance(local, n_total, dst=0, group=None, comm=None, out=None):
     """Gather every rank's (C, n_r) radiance shard into the (C, n_total) buffer on `dst`
-    (None elsewhere).  GPU shards go through the C ABI's RCCL gather (`comm`, a
-    RadianceComm, made on first use if None); CPU shards (gloo) through
+    (None elsewhere).  GPU shards go through the C ABI's RCCL gather (`comm`, or the
+    cached radiance_comm(group, device)); CPU shards (gloo) through
     torch.distributed.gather of padded shards."""
     if local.is_cuda:
-        comm = comm if comm is not None else RadianceComm(group, local.device)
-        return comm.gather(local, n_total, root=dst)
+        comm = comm if comm is not None else radiance_comm(group, local.device)
+        return comm.gather(local, n_total, root=dst, out=out)
     bufs = gather_shards(local, n_total, dst, group)
     if bufs is None:
         return None
@@ -129,7 +144,3 @@ class RadianceComm:
                                            C.c_void_p(st.cuda_stream)))
         return out if self.rank == root else None
 
-
-def gather_radiance_rccl(comm, local, n_total, dst=0, out=None):
-    """sunsky_gather_radiance through a RadianceComm: no padding, no concatenation."""
-    return comm.gather(local, n_total, root=dst, out=out)

@@ -120,3 +120,64 @@ def test_direct_diffuse_with_visibility_replays_bitwise():
     eager = step()
     torch.cuda.synchronize()
     assert torch.equal(captured, eager)
+
+
+def test_update_is_refused_inside_a_capture():
+    """parameters_changed_async is a host + stream operation (include/sunsky_amd.h): on a
+    capturing stream it raises and changes nothing -- the parameter keeps its committed value,
+    the captured eval replays the old state, and the same update outside the capture works."""
+    d = angles_dict(3.0, 0.3, np.deg2rad(50), 0.3, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, "rgb")
+    n = 1 << 12
+    wi, _ = _inputs(n, 5)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        em.eval(ss.SurfaceInteraction3f(wi=wi))
+    torch.cuda.current_stream().wait_stream(side)
+    before = em.eval(ss.SurfaceInteraction3f(wi=wi)).clone()
+    params = em.traverse()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        captured = em.eval(ss.SurfaceInteraction3f(wi=wi))
+        params["turbidity"] = 6.5
+        with pytest.raises(ValueError, match="hipGraph"):
+            params.update()
+    assert em.get_param("turbidity") == 3.0 and params["turbidity"] == 3.0
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(captured, before)
+    params["turbidity"] = 6.5
+    params.update()
+    fresh = ss.SunskyEmitter(dict(d, turbidity=6.5), "rgb")
+    assert torch.equal(em.eval(ss.SurfaceInteraction3f(wi=wi)), fresh.eval(ss.SurfaceInteraction3f(wi=wi)))
+
+
+def test_update_rejected_by_the_device_staging_restores_the_previous_state(monkeypatch):
+    """A negative wavelength-distribution node found by the device staging (the check of
+    ContinuousDistribution's constructor, distr_1d.h) rejects the update as the reference's
+    parameters_changed does: the next read-back raises once, the previous parameters are
+    restored and restaged on the device, and later calls see the old state.  The status is
+    forced with the SUNSKY_AMD_FAULT_STAGE_STATUS fault injection."""
+    d = angles_dict(3.0, 0.3, np.deg2rad(50), 0.3, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, "spectral")
+    n = 1 << 12
+    wi, _ = _inputs(n, 6)
+    lam = torch.full((4, n), 550.0, device="cuda")
+    before = em.eval(ss.SurfaceInteraction3f(wi=wi, wavelengths=lam)).clone()
+    params = em.traverse()
+    params["turbidity"] = 6.5
+    monkeypatch.setenv("SUNSKY_AMD_FAULT_STAGE_STATUS", "1")
+    params.update()                        # async: nothing waits for the device
+    monkeypatch.delenv("SUNSKY_AMD_FAULT_STAGE_STATUS")
+    with pytest.raises(ValueError, match="non-negative"):
+        em.info()
+    assert em.info()["turbidity"] == 3.0 and em.get_param("turbidity") == 3.0
+    assert torch.equal(em.eval(ss.SurfaceInteraction3f(wi=wi, wavelengths=lam)), before)
+    np.testing.assert_array_equal(em.table("sky_params"), ss.SunskyEmitter(d, "spectral").table("sky_params"))
+    params = em.traverse()
+    params["turbidity"] = 6.5
+    params.update()
+    fresh = ss.SunskyEmitter(dict(d, turbidity=6.5), "spectral")
+    assert torch.equal(em.eval(ss.SurfaceInteraction3f(wi=wi, wavelengths=lam)),
+                       fresh.eval(ss.SurfaceInteraction3f(wi=wi, wavelengths=lam)))

@@ -35,6 +35,7 @@ import sunsky_amd as ss  # noqa: E402
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 N_DIRS = 1 << 24          # 16,777,216 (BASELINE.json configs[1])
 TURBIDITIES = (2.0, 6.0, 10.0)
+NB = 4                    # rotating headline input batches (4 x 201 MB > the 256 MiB Infinity Cache)
 BYTES_RGB = 24            # 12 B wi + 12 B RGB per direction
 BYTES_SPEC_PER_DIR = 12 + 11 * 4
 BYTES_SAMPLE = 52
@@ -97,6 +98,27 @@ def pmc_traffic(kernel):
     if not rec:
         return None, None
     return rec["traffic_bytes"], os.path.relpath(files[-1], ROOT)
+
+
+def burst_profile(kernel):
+    """rocprofv3 kernel-trace statistics of the timed headline burst alone (bench.py
+    --headline-only under tools/gpu_r03_prof.sh; tools/burst_stats.py keeps the last
+    3 x steps dispatches) from the newest profiles/rNN_*burst_stats.json.  None if absent."""
+    import glob
+    import re
+
+    def version(path):
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(path))]
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_burst_stats.json")), key=version)
+    if not files:
+        return None
+    with open(files[-1]) as fh:
+        rec = json.load(fh)
+    if rec.get("kernel") != kernel:
+        return None
+    return {"rocprof_mean_us": rec["mean_us"], "rocprof_mean_x3_ms": rec["mean_x_per_step_ms"],
+            "rocprof_first_launch_of_step_us": rec["first_launch_of_step_mean_us"],
+            "rocprof_other_launches_us": rec["other_launches_mean_us"], "source": os.path.relpath(files[-1], ROOT)}
 
 
 def valu_floor(kernel):
@@ -424,6 +446,8 @@ def main():
                     help="also run configs[4]: spectral 11-lambda eval of --c5-dirs per GPU + gather to rank 0 "
                          "(default on when more than one rank runs; --no-c5 turns it off)")
     ap.add_argument("--no-c5", action="store_true")
+    ap.add_argument("--headline-only", action="store_true",
+                    help="run the settle, warmup and timed headline steps only (for a rocprof trace of the burst)")
     ap.add_argument("--c5-dirs", type=int, default=1 << 26, help="directions per GPU for --c5 (default 64M)")
     args = ap.parse_args()
 
@@ -445,16 +469,22 @@ def main():
             dist.init_process_group(backend)
 
     n = args.n
-    wi = -hemisphere_dirs(n, seed=1234 + rank, device=dev)     # si.wi = -wo
+    # NB input batches of n directions (4 x 201 MB > the 256 MiB Infinity Cache), one per step
+    # in rotation: every step's first launch reads its directions from HBM; its other two
+    # launches re-read them at the next turbidity, as the workload (one batch x T{2,6,10}) does.
+    batches = [-hemisphere_dirs(n, seed=1234 + 1000 * k + rank, device=dev) for k in range(NB)]   # si.wi = -wo
+    wi = batches[0]
     ems = [ss.SunskyEmitter(sun_dict(t), "rgb", precision=args.precision, device=dev) for t in TURBIDITIES]
     outs = [torch.empty((3, n), dtype=torch.float32, device=dev) for _ in TURBIDITIES]
     lib = ss.lib()
-    vin = ss._capi.Vec3In(wi[0].data_ptr(), wi[1].data_ptr(), wi[2].data_ptr())
+    vins = [ss._capi.Vec3In(b[0].data_ptr(), b[1].data_ptr(), b[2].data_ptr()) for b in batches]
+    vin = vins[0]
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    def step():
+    def step(i):
+        v = vins[i % NB]
         for em, out in zip(ems, outs):
-            rc = lib.sunsky_eval(em._h, vin, None, 0, 0, None, n, out.data_ptr(), n, stream)
+            rc = lib.sunsky_eval(em._h, v, None, 0, 0, None, n, out.data_ptr(), n, stream)
             if rc:
                 raise RuntimeError(lib.sunsky_last_error().decode())
 
@@ -462,19 +492,21 @@ def main():
     # W warmup steps (a step is ~0.2 ms, so a handful of warmups alone is too short).
     torch.cuda.synchronize()
     t_settle = time.perf_counter()
+    i = 0
     while time.perf_counter() - t_settle < 0.5:
-        step()
+        step(i)
+        i += 1
         torch.cuda.synchronize()
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        step(i + k)
     timer = KernelTimer()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     timer.begin()
-    for _ in range(args.steps):
-        step()
+    for k in range(args.steps):
+        step(k)
     timer.end(args.steps * len(TURBIDITIES))
     torch.cuda.synchronize()
     if world > 1:
@@ -487,15 +519,18 @@ def main():
     kernel_ms = timer.mean_ms()
     evals_per_step = len(TURBIDITIES) * n
     value = evals_per_step * world * args.steps / elapsed
+    if args.headline_only:     # the timed burst alone (rocprofv3 --kernel-trace --stats of exactly it)
+        if rank == 0:
+            print(json.dumps({"metric": "headline burst only", "value": value, "ms_per_step": elapsed / args.steps * 1e3,
+                              "kernel_ms": kernel_ms, "steps": args.steps, "warmup": args.warmup}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
-    # Headline kernel with the Infinity Cache defeated: 4 distinct 16M-direction
-    # batches (805 MB of inputs > the 256 MiB Infinity Cache) evaluated round-robin, so
-    # every launch reads its inputs from HBM (roofline "frac_cold").
-    cold_in = [-hemisphere_dirs(n, seed=777 + 13 * k + rank, device=dev) for k in range(4)]
-    cold_v = [ss._capi.Vec3In(c[0].data_ptr(), c[1].data_ptr(), c[2].data_ptr()) for c in cold_in]
-
+    # Headline kernel with every launch's inputs from HBM: the NB batches evaluated
+    # round-robin at one turbidity (roofline "frac_all_cold").
     def cold_step():
-        for k, v in enumerate(cold_v):
+        for k, v in enumerate(vins):
             rc = lib.sunsky_eval(ems[0]._h, v, None, 0, 0, None, n, outs[k % 3].data_ptr(), n, stream)
             if rc:
                 raise RuntimeError(lib.sunsky_last_error().decode())
@@ -507,11 +542,12 @@ def main():
     tm.begin()
     for _ in range(reps):
         cold_step()
-    tm.end(reps * len(cold_v))
+    tm.end(reps * len(vins))
     cold_ms = tm.mean_ms()
-    del cold_in, cold_v
-    # the bitwise outputs of the parity check below are the timed step's: recompute them
-    step()
+    del batches[1:]
+    vins = vins[:1]
+    # the bitwise outputs of the parity check below are the timed step's on batch 0: recompute them
+    step(0)
     torch.cuda.synchronize()
 
     result = None
@@ -531,18 +567,20 @@ def main():
                        **({"rehearsal": f"{world} ranks on {ndev} GPU(s), gloo"} if rehearsal else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
-                         "achieved_cold": BYTES_RGB * n / (cold_ms * 1e-3) / 1e9,
-                         "frac_cold": BYTES_RGB * n / (cold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "kernel_ms_cold": cold_ms,
-                         "cache_note": "the timed step evaluates one 201 MB input batch at 3 turbidities, so "
-                                       "launches 2 and 3 of a step (and launch 1, after the previous step) find "
-                                       "the inputs in the 256 MiB Infinity Cache; *_cold is the same kernel with "
-                                       "4 rotating batches (inputs from HBM).  PMC FETCH_SIZE counts Infinity-"
-                                       "Cache hits too (MI355X_MICROARCH.md 'HBM'), so `traffic` is bytes past "
-                                       "the L2, not HBM-only bytes",
+                         "achieved_all_cold": BYTES_RGB * n / (cold_ms * 1e-3) / 1e9,
+                         "frac_all_cold": BYTES_RGB * n / (cold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "kernel_ms_all_cold": cold_ms,
+                         "cache_note": f"the timed steps rotate over {NB} distinct 201 MB input batches (805 MB > "
+                                       "the 256 MiB Infinity Cache): launch 1 of a step reads its directions from "
+                                       "HBM, launches 2 and 3 (the next turbidities of the same batch) may find "
+                                       "them in the Infinity Cache, as the workload re-reads them.  *_all_cold "
+                                       "evaluates the batches round-robin so every launch reads from HBM.  PMC "
+                                       "FETCH_SIZE counts Infinity-Cache hits too (MI355X_MICROARCH.md 'HBM'), so "
+                                       "`traffic` is bytes past the L2, not HBM-only bytes",
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": kname,
-                         "kernel_ms": kernel_ms, "bytes_per_launch": BYTES_RGB * n},
+                         "kernel_ms": kernel_ms, "bytes_per_launch": BYTES_RGB * n,
+                         "profile": burst_profile(kname)},
             "parity": parity,
         }
 

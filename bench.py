@@ -35,6 +35,7 @@ import sunsky_amd as ss  # noqa: E402
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 N_DIRS = 1 << 24          # 16,777,216 (BASELINE.json configs[1])
 TURBIDITIES = (2.0, 6.0, 10.0)
+SUN_SLACK = [1.25]         # sun-disc lane bound k (tests/helpers.py SUN_SLACK): 1.25 fast, 4 reference
 NB = 4                    # rotating headline input batches (4 x 201 MB > the 256 MiB Infinity Cache)
 BYTES_RGB = 24            # 12 B wi + 12 B RGB per direction
 BYTES_SPEC_PER_DIR = 12 + 11 * 4
@@ -206,7 +207,7 @@ def cpu_baseline(wi_host, budget_s=12.0):
 def lane_stats(got, a, b, sun, rtol=1e-5):
     """Parity figures of tests/helpers.py, per lane population:
     sky lanes against the fp32 oracle (bound rtol|o32| + |o32 - o64|), sun-disc lanes
-    against the fp64 oracle (bound rtol|o64| + 4|o32 - o64|), each with its worst lane
+    against the fp64 oracle (bound rtol|o64| + k|o32 - o64|, k = SUN_SLACK), each with its worst lane
     as a fraction of the bound and its plain max relative error; for the sun lanes the
     fp32 oracle's own error against fp64 is reported beside the GPU's.  Lanes where
     fp32 and fp64 disagree by > 1e-3 (a horizon / disc-edge mask flipped by rounding)
@@ -232,7 +233,7 @@ def lane_stats(got, a, b, sun, rtol=1e-5):
         rg, ra = np.abs(g - r64) / den, np.abs(r32 - r64) / den
         st.update(sun_lanes=int(sun.sum()), sun_max_rel_vs_o64=float(rg[keep].max()),
                   sun_o32_max_rel_vs_o64=float(ra[keep].max()),
-                  sun_worst_vs_bound=float((np.abs(g - r64) / (rtol * np.abs(r64) + 4 * np.abs(r32 - r64)
+                  sun_worst_vs_bound=float((np.abs(g - r64) / (rtol * np.abs(r64) + SUN_SLACK[0] * np.abs(r32 - r64)
                                                                   + 1e-30)).max()))
     st["pass"] = st.get("sky_worst_vs_bound", 0) <= 1 and st.get("sun_worst_vs_bound", 0) <= 1
     return st
@@ -293,7 +294,7 @@ def parity_check(ems, wi, outs, n_check=1 << 20, n_sun=1 << 14):
         parts.append(lane_stats(got, o32.eval(wi_all), o64.eval(wi_all), sun))
     st = merge_stats(parts)
     return dict(st, checked_dirs=(n_check + n_sun) * len(TURBIDITIES),
-                bound="sky: |gpu-o32| <= 1e-5|o32| + |o32-o64|; sun disc: |gpu-o64| <= 1e-5|o64| + 4|o32-o64|")
+                bound=f"sky: |gpu-o32| <= 1e-5|o32| + |o32-o64|; sun disc: |gpu-o64| <= 1e-5|o64| + {SUN_SLACK[0]:g}|o32-o64|")
 
 
 def parity_c3(em, d_scene, wi, out, n_check=1 << 19, n_sun=1 << 13):
@@ -341,7 +342,10 @@ def parity_c4(em, d_scene, u, d, pdf_s, wgt, pdf_q, n_check=1 << 19, semantics="
     w32 = (e32 / gp[:, None]).astype(np.float32)
     w64 = e64 / gp[:, None].astype(np.float64)
     up = gd[:, 2] >= 0
-    st = lane_stats(gw[up], w32[up], w64[up], inside[up], rtol=2e-5)
+    # disc lanes include a 1e-6 band at the edge: the kernel's fp32 disc test may put the sun
+    # term on a lane the fp64 test leaves outside (tests/helpers.py disc_lanes)
+    disc = gd.astype(np.float64) @ inf["sun_dir_local"] >= inf["cos_cutoff"] - 1e-6
+    st = lane_stats(gw[up], w32[up], w64[up], disc[up], rtol=2e-5)
     return {"checked_samples": n_check, "variant": variant, "dir_max_abs_delta": float(derr.max()),
             "dir_p999_abs_delta": float(np.quantile(derr, 0.999)),
             "pdf_max_rel_vs_o32": float(rel_p.max()), "pdf_direction_max_rel_vs_o32": float(rel_q.max()),
@@ -450,6 +454,7 @@ def main():
                     help="run the settle, warmup and timed headline steps only (for a rocprof trace of the burst)")
     ap.add_argument("--c5-dirs", type=int, default=1 << 26, help="directions per GPU for --c5 (default 64M)")
     args = ap.parse_args()
+    SUN_SLACK[0] = 4.0 if args.precision == "reference" else 1.25
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

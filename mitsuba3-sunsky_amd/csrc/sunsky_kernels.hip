@@ -249,6 +249,7 @@ struct DirTerms {
     float r;        // 1 / (cos_theta + 0.01)
     float sq;       // safe_sqrt(cos_theta)
     float h;        // |wo -/+ n| / 2, so gamma = 2 asin(h) or pi - 2 asin(h)
+    float wx, wy;   // wo.x, wo.y (wo.z = cos_theta): the FAST sun disc's cos psi
     bool active, hit_sun;
     // sun-disc terms, filled by add_sun_terms() for hit_sun lanes only
     int sun_pos;    // elevation segment (sunsky.cpp:579-587)
@@ -270,6 +271,8 @@ __device__ __forceinline__ DirTerms dir_terms(const SunskyKArgs& K, float3_ wo, 
     float3_ v = mk3(fmaf(-sg, sn.x, wo.x), fmaf(-sg, sn.y, wo.y), fmaf(-sg, sn.z, wo.z));
     float h = 0.5f * (FAST ? fast_sqrt(dot3(v, v)) : sqrtf(dot3(v, v)));
     t.h = h;
+    t.wx = wo.x;
+    t.wy = wo.y;
     float temp = 2.f * (FAST ? asin_half_chord(h) : asinf(h));
     t.gamma = d >= 0.f ? temp : kPi - temp;
     if (FAST) {
@@ -323,9 +326,22 @@ __device__ __forceinline__ void add_sun_terms(const SunskyKArgs& K, DirTerms& t)
             float frac = (float)pos * (1.f / (float)kNbSunSegments);
             t.sun_pos = pos;
             t.sun_x = elevation - kHalfPi * (frac * frac * frac);
-            float h2 = t.h * t.h;
-            float sg2 = 4.f * h2 * (1.f - h2);                    // sin^2(gamma)
-            t.sun_cpsi = fast_sqrt(fmaxf(fmaf(-K.inv_sin2_half_ap, sg2, 1.f), 0.f));   // v_sqrt_f32, 1 ulp
+            // cos^2 psi = 1 - sin^2(gamma) / sin^2(half aperture) cancels towards the limb, where
+            // d cos psi / d gamma is unbounded: its inputs in fp64.  With v = wo - n (exact in
+            // fp32 next to the sun, the reference's subtraction) and |v|^2 = 4 h^2,
+            // sin^2(gamma) = sin^2(2 asin h) = |v|^2 (1 - |v|^2 / 4); the fp32 products widen
+            // exactly.  One rounding to fp32 before the square root (relative 3e-8 on cos psi).
+#ifdef SS_PROBE_F32_CPSI   // probe build (A/B of the fp32 form it replaced): never in the product
+            const float h2 = t.h * t.h, sg2 = 4.f * h2 * (1.f - h2);
+            t.sun_cpsi = fast_sqrt(fmaxf(fmaf(-K.inv_sin2_half_ap, sg2, 1.f), 0.f));
+            if (sg2 >= 0.f) return;
+#endif
+            const double vx = (double)(t.wx - K.sun_n[0]), vy = (double)(t.wy - K.sun_n[1]),
+                         vz = (double)(t.cos_theta - K.sun_n[2]);
+            const double v2 = fma(vz, vz, fma(vy, vy, vx * vx));
+            const double inv = (double)K.cpsi_inv_hi + (double)K.cpsi_inv_lo;
+            const float c2 = (float)fma(-inv, v2 * fma(-0.25, v2, 1.0), 1.0);
+            t.sun_cpsi = fast_sqrt(fmaxf(c2, 0.f));   // v_sqrt_f32, 1 ulp
         } else {
             t.sun_pos = sun_segment(t.cos_theta, &t.sun_x);
             t.sun_cpsi = cos_psi(t.gamma, K.inv_sin2_half_ap);

@@ -212,7 +212,8 @@ SunskyModel::SunskyModel(const Properties& props, int variant, int semantics, co
     if (turb < 1.f || 10.f < turb) throw std::invalid_argument(fmt("Turbidity value %f is out of range [1, 10]", turb));
     turbidity_ = turb;
     const float deg2rad = (float)(3.14159265358979323846 / 180.0);
-    sun_half_aperture_ = (0.5f * (float)props.get_float("sun_aperture", 0.5358)) * deg2rad;
+    sun_aperture_deg_ = (float)props.get_float("sun_aperture", 0.5358);
+    sun_half_aperture_ = (0.5f * sun_aperture_deg_) * deg2rad;
     if (sun_half_aperture_ <= 0.f || 0.5f * kPi <= sun_half_aperture_)
         throw std::invalid_argument(fmt("Invalid sun aperture angle: %f, must be in ]0, 90[ degrees!",
                                         2.0 * sun_half_aperture_ / deg2rad));
@@ -445,6 +446,12 @@ void SunskyModel::stage_geometry() {
     k_.cos_cutoff = cosf(sun_half_aperture_);
     float sh = sinf(sun_half_aperture_);
     k_.inv_sin2_half_ap = 1.f / (sh * sh);
+    {
+        const double shd = std::sin(0.5 * (double)sun_aperture_deg_ * (3.14159265358979323846 / 180.0));
+        const double inv = 1.0 / (shd * shd);
+        k_.cpsi_inv_hi = (float)inv;
+        k_.cpsi_inv_lo = (float)(inv - (double)k_.cpsi_inv_hi);
+    }
     // get_area_ratio, sunsky.h:99-101
     k_.area_ratio = (1.f - cosf((float)(kSunHalfApertureDeg * (3.14159265358979323846 / 180.0)))) /
                     (1.f - cosf(sun_half_aperture_));

@@ -105,7 +105,7 @@ private:
     std::vector<float> sky_params_ds_, sky_rad_ds_, sun_rad_ds_, sun_ld_, tgmm_tables_;
     float cie_y_[kNbWavelengths] = {0};
     // parameters
-    float turbidity_ = 3.f, sky_scale_ = 1.f, sun_scale_ = 1.f, sun_half_aperture_ = 0.f;
+    float turbidity_ = 3.f, sky_scale_ = 1.f, sun_scale_ = 1.f, sun_half_aperture_ = 0.f, sun_aperture_deg_ = 0.5358f;
     std::vector<float> albedo_;
     bool active_record_ = true;
     DateTime time_;

@@ -92,6 +92,9 @@ struct SunskyKArgs {
     float cos_cutoff;        // cos(sun_half_aperture)
     float half_aperture;     // m_sun_half_aperture
     float inv_sin2_half_ap;  // 1 / sin^2(half_aperture)  (compute_cos_psi, sunsky.h:385-392)
+    // FAST cos psi: 1 / sin^2 of the half aperture in fp64 (0.5 x the fp32 aperture in
+    // degrees, converted in fp64), as an unevaluated float pair hi + lo
+    float cpsi_inv_hi, cpsi_inv_lo;
     float area_ratio;        // get_area_ratio(half_aperture)
     float sky_scale, sun_scale;
     float sun_pdf;           // InvTwoPi / (1 - cos_cutoff) (warp.h:568-577)

@@ -107,9 +107,19 @@ def parity_stats(gpu, o32, o64, sunlanes):
     return st
 
 
-def assert_parity(gpu, o32, o64, sunlanes, rtol=1e-5):
-    """gpu/o32/o64: (n, c).  sky lanes: rel to o32; sun lanes: conditioning-aware vs o64.
-    Returns parity_stats() so callers can report the sun-lane error as a number."""
+SUN_SLACK = {"fast": 1.25, "reference": 4.0}
+
+
+def assert_parity(gpu, o32, o64, sunlanes, rtol=1e-5, precision="fast", sun_k=None):
+    """gpu/o32/o64: (n, c).  sky lanes: rel to o32; sun lanes: conditioning-aware vs o64,
+    |gpu - o64| <= rtol |o64| + k |o32 - o64| per lane with k = 1.25 for the fast kernels
+    (their cos psi comes from fp64 chord terms: more accurate than the reference's fp32) and
+    k = 4 for the reference-precision kernels, which repeat the reference's fp32 operations
+    with the GPU's libm (an ulp of sin(gamma) next to the limb moves a lane by ~1e-5); those
+    must also be as accurate as the fp32 reference overall (max over the sun lanes within
+    1.25 x the fp32 oracle's max).  sun_k overrides k (the aggregate check then applies when
+    k > 1.25).  Returns parity_stats()."""
+    k = SUN_SLACK[precision] if sun_k is None else sun_k
     sky = ~sunlanes
     if sky.any():
         g, a, b = gpu[sky].astype(np.float64), o32[sky].astype(np.float64), o64[sky]
@@ -122,10 +132,12 @@ def assert_parity(gpu, o32, o64, sunlanes, rtol=1e-5):
         assert strict.mean() >= 0.9999, f"sky lanes: only {strict.mean():.6f} within plain {rtol:g}"
     if sunlanes.any():
         g, a, b = gpu[sunlanes].astype(np.float64), o32[sunlanes].astype(np.float64), o64[sunlanes]
-        bound = rtol * np.abs(b) + 4 * np.abs(a - b) + 1e-30
+        bound = rtol * np.abs(b) + k * np.abs(a - b) + 1e-30
         bad = np.abs(g - b) > bound
         assert not bad.any(), f"sun lanes: {bad.sum()} over bound, worst {np.max(np.abs(g - b) / bound):.2f}x"
     st = parity_stats(gpu, o32, o64, sunlanes)
+    if k > 1.25 and "sun_max_rel_vs_o64" in st:
+        assert st["sun_max_rel_vs_o64"] <= 1.25 * max(st["sun_o32_max_rel_vs_o64"], rtol), st
     print("parity", {k: (f"{v:.3e}" if isinstance(v, float) else v) for k, v in st.items()})
     return st
 
@@ -151,3 +163,11 @@ def assert_lambda_parity(lam_g, lam_o):
     same = float(np.mean(lam_g == lam_o.astype(np.float32)))
     print(f"lambda: max rel {rel.max():.3e}, bitwise equal {same:.6f}")
     return same
+
+
+def disc_lanes(d, info, band=1e-6):
+    """Sun-disc lanes for the parity bars: directions within `band` of the disc edge count
+    as disc lanes too.  The kernel's (and the fp32 reference's) disc test is an fp32 dot
+    against the fp32 cos(half aperture); a lane the fp64 test puts just outside may carry
+    the sun term, at the limb where the fp32 reference's own cos psi error is largest."""
+    return (np.asarray(d, np.float64) @ info["sun_dir_local"]) >= info["cos_cutoff"] - band

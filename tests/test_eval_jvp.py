@@ -98,7 +98,7 @@ def test_eval_jvp_matches_finite_differences(variant, param):
     ref32, ref64 = (ref32.T, ref64.T) if variant == "spectral" else (ref32, ref64)
     cosg = wo @ inf["sun_dir_local"]
     sun = (cosg >= inf["cos_cutoff"]) & (wo[:, 2] >= 0)
-    assert_parity(val, ref32, ref64, sun)
+    assert_parity(val, ref32, ref64, sun, precision="reference")   # the AD kernels keep full precision
     mask = np.ones(wo.shape[0], bool)
     if param == "sun_direction":
         # the disc test flips under the perturbation and d gamma is singular at gamma = 0

@@ -17,7 +17,7 @@ import torch
 
 import oracle as O
 import sunsky_amd as ss
-from helpers import (angles_dict, assert_lambda_parity, assert_parity, hemisphere_wo, lambda_pdf, max_rel,
+from helpers import (angles_dict, disc_lanes, assert_lambda_parity, assert_parity, hemisphere_wo, lambda_pdf, max_rel,
                      sphere_wo, sun_cone_wo)
 
 pytestmark = pytest.mark.gpu
@@ -77,7 +77,7 @@ def test_c3_node_kernel_against_oracle(precision):
     a, b = o32.eval(wi, lam), o64.eval(wi, lam)
     sm = sun_mask(o32, wo)
     assert sm.sum() > 2500
-    st = assert_parity(out.T, a.T, b.T, sm)
+    st = assert_parity(out.T, a.T, b.T, sm, precision=precision)
     # the disc lanes are as accurate as the reference's own fp32 arithmetic
     assert st["sun_max_rel_vs_o64"] <= 1.25 * max(st["sun_o32_max_rel_vs_o64"], 1e-5), st
     assert np.all(out[:, wo[:, 2] < 0] == 0)
@@ -116,7 +116,10 @@ def test_eval_direction(variant, rotated):
     if variant == "spectral":
         a, b = a.T, b.T
     loc = (dirs.astype(np.float64) @ np.linalg.inv(M).T).astype(np.float32)
-    assert_parity(got.T, a, b, sun_mask(o32, loc))
+    # rotated: the fp32 to_local transform (the reference's too) rounds wo, and next to the limb
+    # that rounding, shared by the fp32 oracle, dominates |. - o64| lane by lane: k = 4 per lane
+    # and the aggregate bar (max within 1.25 x the fp32 oracle's)
+    assert_parity(got.T, a, b, sun_mask(o32, loc), sun_k=4.0 if rotated else None)
 
 
 # --------------------------------------------------------- sample_wavelengths
@@ -147,14 +150,14 @@ def test_sample_wavelengths(variant, semantics, precision):
     sm = sun_mask(o32, wo)
     if variant == "rgb":
         assert np.all(lam_g == 0)
-        assert_parity(w_g, o32.eval(wi), o64.eval(wi), sm)
+        assert_parity(w_g, o32.eval(wi), o64.eval(wi), sm, precision=precision)
         return
     assert_lambda_parity(lam_g, lam_o)
     assert lam_g.min() >= 360 and lam_g.max() <= 720
     # weights: the fp32 oracle's own eval / pdf; fp64 at the same wavelengths for the
     # conditioning slack of assert_parity (eval in fp64 over the oracle's lambda pdf)
     e64 = o64.eval(wi, lam_g.T).T
-    assert_parity(w_g, w_o.astype(np.float32), e64 / lambda_pdf(o64, lam_g), sm, rtol=1e-5)
+    assert_parity(w_g, w_o.astype(np.float32), e64 / lambda_pdf(o64, lam_g), sm, rtol=1e-5, precision=precision)
 
 
 # ----------------------------------------------------- C4 at 30 deg elevation
@@ -190,5 +193,5 @@ def test_c4_sampling_at_30deg_elevation(variant, precision):
     e32, e64 = o32.eval(-gd, lam), o64.eval(-gd, lam)
     if variant == "spectral":
         e32, e64 = e32.T, e64.T
-    assert_parity(gw, (e32 / gp[:, None]).astype(np.float32), e64 / gp[:, None].astype(np.float64), inside,
-                  rtol=2e-5)
+    assert_parity(gw, (e32 / gp[:, None]).astype(np.float32), e64 / gp[:, None].astype(np.float64), disc_lanes(gd, o32.info()),
+                  rtol=2e-5, precision=precision)

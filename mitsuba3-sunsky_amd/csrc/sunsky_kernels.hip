@@ -146,6 +146,14 @@ __device__ __forceinline__ float div_by_rcp(float a, float b, float rb) {
     return a / b;
 }
 
+// (lambda - 320) / 40, the per-lane wavelength's channel coordinate (sunsky.cpp:326), as
+// div_by_rcp by the correctly rounded 1/40: equal to the IEEE quotient for every float
+// (checked exhaustively on the host for |a| in [2^-100, 2^100]; below, the division
+// itself; inf / NaN give an invalid coordinate either way), without the division sequence.
+__device__ __forceinline__ float wavelength_node(float lambda) {
+    return div_by_rcp(lambda - kWavelength0, kWavelengthStep, 1.f / kWavelengthStep);
+}
+
 // A wave-uniform float the compiler may not re-derive per lane: the sampling loops
 // select between the reciprocals 1 / w_sky and 1 / (1 - w_sky) (div_exact's rb), and
 // without this InstCombine folds select(p, 1 / a, 1 / b) into 1 / select(p, a, b), a
@@ -526,7 +534,7 @@ template <bool FAST>
 __device__ __forceinline__ float eval_spec_one(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
                                                const float* sun_tab, const float* ld_tab, const DirTerms& t,
                                                float lambda) {
-    float nw = (lambda - kWavelength0) / kWavelengthStep;
+    float nw = wavelength_node(lambda);
     bool valid = (0.f <= nw) && (nw <= (float)(kNbWavelengths - 1));
     if (!(t.active && valid)) return 0.f;
     int lo = (int)floorf(nw), hi = lo + 1;
@@ -1276,11 +1284,107 @@ __device__ __forceinline__ void sample_direction_body(
         } else {
             DirTerms t = dir_terms<FAST>(K, wo, act);
             add_sun_terms<FAST>(K, t);
+            const float inv_pd = fdiv<FAST>(1.f, pd);
             for (int k = 0; k < nlam; ++k) {
                 float e = eval_spec_one<FAST>(K, S.chans.c, S.sun, S.ld, t, lam[(size_t)k * lstride + i]);
-                float w = e / pd;
+                float w = FAST ? e * inv_pd : e / pd;
                 weight[(size_t)k * wstride + i] = isfinite(w) ? w : 0.f;
             }
+        }
+    }
+}
+
+// Spectral eval at Mitsuba's 4 per-lane wavelengths (Spectrum<Float, 4>, sunsky.cpp:325-348)
+// without per-wavelength branches: the channel pair is clamped to (lo, lo + 1) with lo <= 9
+// and f in [0, 1].  lerpf_ (dr::lerp's fma(b, t, fnmadd(a, t, a))) returns a at t = 0 and
+// b at t = 1 exactly, so a node (f = 0, where eval_spec_one skips the lerp) and 720 nm
+// (lo = 10, f = 0 there; lo = 9, f = 1 here) give eval_spec_one's bits; the sun-disc
+// terms of the 4 wavelengths run in one branch per lane.
+template <bool FAST>
+__device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
+                                           const float* sun_tab, const float* ld_tab, const DirTerms& t,
+                                           const float lam[4], float e[4]) {
+    int lo[4];
+    float f[4];
+    bool ok[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float nw = wavelength_node(lam[k]);
+        ok[k] = t.active && (0.f <= nw) && (nw <= (float)(kNbWavelengths - 1));
+        const int c = ok[k] ? (int)floorf(nw) : 0;
+        lo[k] = c < kNbWavelengths - 2 ? c : kNbWavelengths - 2;
+        f[k] = ok[k] ? nw - (float)lo[k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        e[k] = lerpf_(sky_eval<FAST>(chans[lo[k]], t, K.sky_scale), sky_eval<FAST>(chans[lo[k] + 1], t, K.sky_scale),
+                      f[k]);
+    if (t.hit_sun) {
+#pragma unroll 1
+        for (int k = 0; k < 4; ++k) {
+            const int a = lo[k], b = a + 1;
+            const float sun = lerpf_(render_sun_spec(sun_tab, t.sun_pos, a, t.sun_x),
+                                     render_sun_spec(sun_tab, t.sun_pos, b, t.sun_x), f[k]);
+            float ld = 0.f;
+#pragma unroll
+            for (int j = 0; j < kNbSunLdParams; ++j)
+                ld += powif_(t.sun_cpsi, j) * lerpf_(ld_tab[a * kNbSunLdParams + j], ld_tab[b * kNbSunLdParams + j], f[k]);
+            e[k] += FAST ? K.sun_mul * (sun * ld) : K.sun_scale * sun * ld * K.area_ratio;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) e[k] = ok[k] ? e[k] : 0.f;
+}
+
+// LEAN spectral sample_direction with 4 wavelengths per sample (sunsky.cpp:399-441 in the
+// spectral variants, Spectrum<Float, 4>): the per-sample work of
+// sample_direction_body<FAST, true, true> with the wavelength loop unrolled and branchless
+// (eval_spec4), the next sample's u and 4 wavelengths loaded before this one's work, and
+// non-temporal stores.  Bitwise the general kernel's outputs.
+template <bool FAST>
+__device__ __forceinline__ void sample_direction_spec4_body(
+    const SunskyKArgs& K, const float* __restrict__ ux, const float* __restrict__ uy, const float* __restrict__ lam,
+    size_t lstride, size_t n, float* __restrict__ dx, float* __restrict__ dy, float* __restrict__ dz,
+    float* __restrict__ pdf, float* __restrict__ weight, size_t wstride) {
+    __shared__ SamplerLds<FAST, true> S;
+    stage_sampler_lds<FAST, true>(K, &S);
+    const float w_sun = 1.f - K.w_sky, inv_w = uniform_f(1.f / K.w_sky), inv_w_sun = uniform_f(1.f / w_sun);
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float nx = 0.f, ny = 0.f, nl[4] = {0.f, 0.f, 0.f, 0.f};
+    auto load = [&](size_t j) {
+        nx = ux[j];
+        ny = uy[j];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nl[k] = lam[(size_t)k * lstride + j];
+    };
+    if (i < n) load(i);
+    for (; i < n; i += stride) {
+        const float sx = nx, sy = ny;
+        float l[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) l[k] = nl[k];
+        if (i + stride < n) load(i + stride);
+        const bool pick_sky = sx < K.w_sky;
+        const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
+        const bool act = sd.z >= 0.f;
+        const float3_ d = to_world(K, sd);
+        float skyp, sunp;
+        compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+        const float pd = lerpf_(sunp, skyp, K.w_sky);
+        store_nt(d.x, dx + i);
+        store_nt(d.y, dy + i);
+        store_nt(d.z, dz + i);
+        store_nt(pd, pdf + i);
+        DirTerms t = dir_terms<FAST>(K, to_local(K, d), act);
+        add_sun_terms<FAST>(K, t);
+        float e[4];
+        eval_spec4<FAST>(K, S.chans.c, S.sun, S.ld, t, l, e);
+        const float inv_pd = fdiv<FAST>(1.f, pd);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float w = FAST ? e[k] * inv_pd : e[k] / pd;
+            store_nt(isfinite(w) ? w : 0.f, weight + (size_t)k * wstride + i);
         }
     }
 }
@@ -2457,8 +2561,22 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_ref, false, true, false)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_plain_fast, true, false, true)
 // reference-precision twin of the unsorted LEAN form (the C ABI loads every kernel in both precisions)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_plain_ref, false, false, true)
-SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_fast, true, true, true)
-SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_ref, false, true, true)
+// LEAN spectral: Mitsuba's 4 wavelengths per sample take the unrolled branchless body
+#define SS_SAMPLE_DIRECTION_SPEC_LEAN(NAME, FAST)                                                              \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
+        const SunskyKArgs* __restrict__ Kp, const float* ux, const float* uy, const float* px, const float* py, const float* pz,   \
+        const float* lam, size_t lstride, int nlam, const uint8_t* active, size_t n, float* dx, float* dy,     \
+        float* dz, float* pdf, float* dist, float* opx, float* opy, float* opz, float* weight, size_t wstride) { \
+        if (nlam == 4)                                                                                         \
+            sample_direction_spec4_body<FAST>(*Kp, ux, uy, lam, lstride, n, dx, dy, dz, pdf, weight, wstride);   \
+        else                                                                                                   \
+            sample_direction_body<FAST, true, true>(*Kp, ux, uy, px, py, pz, lam, lstride, nlam, active, n, dx,  \
+                                                    dy, dz, pdf, dist, opx, opy, opz, weight, wstride);        \
+    }
+SS_SAMPLE_DIRECTION_SPEC_LEAN(sunsky_sample_direction_spec_lean_fast, true)
+SS_SAMPLE_DIRECTION_SPEC_LEAN(sunsky_sample_direction_spec_lean_ref, false)
+// the previous LEAN spectral form (wavelength loop, lambda not prefetched), for A/B timing
+SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_loop_fast, true, true, true)
 
 #define SS_SAMPLE_DIRECTION_SORTED(NAME, FAST, R, FULL)                                                           \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \

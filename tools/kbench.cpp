@@ -55,6 +55,7 @@ int main(int argc, char** argv) {
         while (std::getline(ss, tok, ',')) bpcu.push_back(std::atoi(tok.c_str()));
     }
     const bool spec = mode == "spec";
+    const bool rays = mode == "rays";   // per-ray spectral eval, 4 random wavelengths per ray (Spectrum<Float, 4>)
     const bool sampling = mode == "sample" || mode == "pdf";
     const char* pack = std::getenv("SUNSKY_AMD_DATASET");
     std::string pack_path = pack ? pack : "mitsuba3-sunsky_amd/data/sunsky_datasets.pack";
@@ -66,7 +67,7 @@ int main(int argc, char** argv) {
     props.set_vector3("sun_direction", (float)std::sin(th), 0.f, (float)std::cos(th));
     // KB_SAMPLE_SPEC=1 (sample mode): the spectral emitter, 4 random wavelengths per sample
     const bool sspec = mode == "sample" && std::getenv("KB_SAMPLE_SPEC") != nullptr;
-    SunskyModel model(props, spec || sspec ? kSpectral : kRGB, kJit, pack_path);
+    SunskyModel model(props, spec || sspec || rays ? kSpectral : kRGB, kJit, pack_path);
 
     int cu = 0;
     CK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0));
@@ -91,7 +92,7 @@ int main(int argc, char** argv) {
         float ct = U(rng), ph = 2.f * (float)M_PI * U(rng), st = std::sqrt(std::max(0.f, 1 - ct * ct));
         hx[i] = -st * std::cos(ph); hy[i] = -st * std::sin(ph); hz[i] = -ct;
     }
-    const int nout = spec ? 11 : (mode == "pdf" ? 1 : 3);
+    const int nout = spec ? 11 : rays ? 4 : (mode == "pdf" ? 1 : 3);
     float *wx, *wy, *wz, *out;
     CK(hipMalloc(&wx, n * 4)); CK(hipMalloc(&wy, n * 4)); CK(hipMalloc(&wz, n * 4));
     CK(hipMalloc(&out, n * 4 * nout));
@@ -108,7 +109,7 @@ int main(int argc, char** argv) {
     const uint8_t* active = nullptr;
     size_t ostride = n;
     float sign = -1.f;
-    const double bytes = spec ? (12.0 + 44.0) * n : mode == "sample" ? 36.0 * n : mode == "pdf" ? 16.0 * n : 24.0 * n;
+    const double bytes = spec ? (12.0 + 44.0) * n : rays ? 44.0 * n : mode == "sample" ? 36.0 * n : mode == "pdf" ? 16.0 * n : 24.0 * n;
     // sampling inputs: u in [0,1)^2 (reuses wx / wy), outputs d (3 planes), pdf, RGB weight
     float *dd = nullptr, *pdf = nullptr, *wgt = nullptr;
     if (sampling) {
@@ -152,7 +153,7 @@ int main(int argc, char** argv) {
     const float* nullf = nullptr;
     int nl4 = 4;
     float* lamp = nullptr;
-    if (sspec) {
+    if (sspec || rays) {
         std::vector<float> l(4 * n);
         for (auto& v : l) v = 360.f + 360.f * U(rng);
         CK(hipMalloc(&lamp, 4 * n * 4));
@@ -191,7 +192,8 @@ int main(int argc, char** argv) {
             void* args_sample_full[] = {&K, &wx, &wy, &fpx, &fpy, &fpz, &nullf, &zero, &nl0, &active, &n,
                                         &dd, &ddy, &ddz, &pdf, &fdist, &fox, &foy, &foz, &wgt, &n};
             void* args_pdf[] = {&K, &dd, &ddy, &ddz, &active, &n, &pdf};
-            void** args = spec ? args_spec : mode == "sample" ? (full ? args_sample_full : args_sample)
+            void* args_rays[] = {&K, &wx, &wy, &wz, &lamp, &n, &nl4, &active, &n, &out, &ostride, &sign};
+            void** args = spec ? args_spec : rays ? args_rays : mode == "sample" ? (full ? args_sample_full : args_sample)
                                             : mode == "pdf" ? args_pdf : args_rgb;
             for (int w = 0; w < 3; ++w) CK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
             hipEvent_t e0, e1;

@@ -6,7 +6,11 @@ final [C][N] planes.
   and the in-place case (shard already at its columns) copies nothing;
 * two processes on the box's GPU(s): shards evaluated by the HIP kernels, gathered to
   rank 0, bitwise equal to the whole batch evaluated alone.  With one GPU both ranks
-  share it; if RCCL refuses two ranks on one device the test is skipped with its reason.
+  share it; if RCCL refuses two ranks on one device the test is skipped with its reason;
+* the multi-rank send/recv branch itself on one GPU, 2-4 ranks in one process, with the
+  RCCL entry points served by the test double tests/cpp/fake_rccl.cpp (linked by the
+  test program tests/cpp/gather_double_check): ragged and empty shards, 3 and 11 planes,
+  either root, either call order.
 """
 import ctypes as C
 import os
@@ -91,3 +95,17 @@ def test_two_ranks_rccl_gather_bitwise():
         pytest.skip("RCCL refused this configuration: " + text.strip().splitlines()[-1][:300])
     assert codes == [0, 0], text
     assert "bitwise equal: True" in text
+
+
+def test_multi_rank_gather_through_rccl_double():
+    """sunsky_gather_radiance's grouped ncclSend / ncclRecv branch (csrc/sunsky_comm.cpp) with
+    2, 3 and 4 ranks on one GPU: tests/cpp/gather_double_check links the RCCL test double
+    (tests/cpp/fake_rccl.cpp, soname librccl.so.1) so the product's dlopen finds it."""
+    exe = os.path.join(ROOT, "tests", "cpp", "build", "gather_double_check")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "cpp"), "build/gather_double_check"], check=True,
+                       capture_output=True)
+    p = subprocess.run([exe], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240)
+    print(p.stdout)
+    assert p.returncode == 0, p.stdout
+    assert "48 cases bitwise equal" in p.stdout

@@ -269,8 +269,9 @@ typedef enum sunsky_param {         /* Differentiable traverse() parameters, sun
  * dr::enable_grad(param); dr::set_grad(param, tangent); dr::forward_from(param);
  * dr::grad(eval(si)) computes in the reference's AD variants (exercised by
  * sunsky-testing/traversal_test.py:94-145).  Layout as sunsky_eval; d_out has the
- * planes of out.  The tangent of the staged tables is computed on the host and
- * uploaded (stream-ordered, pinned staging) and the rays processed on `stream`. */
+ * planes of out.  The tangent of the staged tables is staged by a device kernel
+ * (fp64, stream-ordered on `stream`) when the emitter or the tangent changed, then the
+ * rays are processed on `stream`. */
 int sunsky_eval_jvp(const sunsky_emitter *e, int param, const float *tangent, int tangent_count,
                     sunsky_vec3_in wi, const float *wavelengths, int n_wavelengths, size_t wl_stride,
                     const uint8_t *active, size_t n, float *out, float *d_out, size_t out_stride,
@@ -290,6 +291,15 @@ int sunsky_eval_jvp(const sunsky_emitter *e, int param, const float *tangent, in
 int sunsky_eval_vjp(const sunsky_emitter *e, sunsky_vec3_in wi, const float *wavelengths, int n_wavelengths,
                     size_t wl_stride, const uint8_t *active, size_t n, const float *d_out, size_t out_stride,
                     float *grad, void *stream);
+/* The tangent of the staged tables along `tangent` of `param` -- what dr::forward_from(param)
+ * propagates into compute_radiance_params / compute_sun_params (sunsky.h:158-231, 404-419)
+ * before eval: SUNSKY_TANGENT_FLOATS floats, d{A..I, rad} of channel c at c * 10 (+ q), the
+ * local sun direction's tangent at 110..112, the sun table's at 128.  on_device = 1 stages
+ * them with the kernel eval_jvp uses (blocking, on the null stream), 0 on the host (also
+ * for host-only emitters); both compute the same fp64 arithmetic. */
+#define SUNSKY_TANGENT_FLOATS (128 + 3240)
+int sunsky_emitter_tangent_tables(const sunsky_emitter *e, int param, const float *tangent, int tangent_count,
+                                  int on_device, float *out, size_t capacity, size_t *count);
 
 /* --------------------------------------------- dataset I/O (sunsky_v.cpp:16-18) */
 /* array_from_file_d / _f (sunsky.h:516-561): file_dtype 0 = infer, 1 = fp32, 2 = fp64.

@@ -109,6 +109,7 @@ struct DeviceModule {
     hipFunction_t vjp_rgb = nullptr, vjp_spec = nullptr, grad_reduce = nullptr;   // eval_vjp
     hipFunction_t latlong_tables = nullptr;                                     // bake_latlong
     hipFunction_t stage_radiance = nullptr, quad_points = nullptr, quad_finish = nullptr;   // parameters_changed
+    hipFunction_t stage_tangent = nullptr;                                      // eval_jvp / eval_vjp tables
     int cu_count = 256;
 };
 
@@ -138,6 +139,7 @@ DeviceModule* module_for_device(int dev) {
     hip_check(hipModuleGetFunction(&m->vjp_spec, m->module, "sunsky_eval_vjp_spec"), "sunsky_eval_vjp_spec");
     hip_check(hipModuleGetFunction(&m->grad_reduce, m->module, "sunsky_grad_reduce"), "sunsky_grad_reduce");
     hip_check(hipModuleGetFunction(&m->latlong_tables, m->module, "sunsky_latlong_tables"), "sunsky_latlong_tables");
+    hip_check(hipModuleGetFunction(&m->stage_tangent, m->module, "sunsky_stage_tangent"), "sunsky_stage_tangent");
     hip_check(hipModuleGetFunction(&m->stage_radiance, m->module, "sunsky_stage_radiance"), "sunsky_stage_radiance");
     hip_check(hipModuleGetFunction(&m->quad_points, m->module, "sunsky_stage_quad_points"), "sunsky_stage_quad_points");
     hip_check(hipModuleGetFunction(&m->quad_finish, m->module, "sunsky_stage_quad_finish"), "sunsky_stage_quad_finish");
@@ -298,7 +300,6 @@ struct sunsky_emitter {
     mutable float* d_vjp = nullptr;   // eval_vjp basis-tangent tables
     mutable float* d_partials = nullptr;   // eval_vjp per-workgroup gradient partials
     mutable size_t partials_cap = 0;
-    mutable float* h_ad = nullptr;         // pinned staging of the AD tangent tables
     mutable float* d_bake = nullptr;       // bake_latlong angle tables
     mutable size_t bake_cap = 0;
     // AD tangent tables depend only on the emitter state: restaged when `rev` (bumped by
@@ -309,9 +310,10 @@ struct sunsky_emitter {
     uint64_t rev = 0;
     mutable uint64_t vjp_rev = ~0ull, jvp_rev = ~0ull;
     mutable std::vector<float> jvp_key;
-    mutable hipEvent_t ad_done = nullptr, ad_copy_done = nullptr, bake_done = nullptr;
+    mutable hipEvent_t ad_done = nullptr, bake_done = nullptr;
 
-    static constexpr size_t kAdFloats = 576 + kSunRgbTableSize;   // the larger (VJP) tangent block
+    static constexpr int kJvpFloats = kJvpSunOffset + kSunRgbTableSize;   // AD tangent buffers
+    static constexpr int kVjpFloats = kVjpSunOffset + kSunRgbTableSize;
 
     // Allocations of a GPU emitter (once, at creation): state, tables, the raw datasets
     // the staging kernels read, quadrature nodes, scratch, pinned ring, events.
@@ -483,10 +485,9 @@ struct sunsky_emitter {
                         (void*)d_status, (void*)d_jvp, (void*)d_vjp, (void*)d_partials, (void*)d_bake})
             if (p) (void)hipFree(p);
         if (h_ring) (void)hipHostFree(h_ring);
-        if (h_ad) (void)hipHostFree(h_ad);
         for (hipEvent_t ev : ring_ev)
             if (ev) (void)hipEventDestroy(ev);
-        for (hipEvent_t ev : {stage_done, ad_done, ad_copy_done, bake_done})
+        for (hipEvent_t ev : {stage_done, ad_done, bake_done})
             if (ev) (void)hipEventDestroy(ev);
         if (cur >= 0 && cur != device) (void)hipSetDevice(cur);
     }
@@ -497,18 +498,29 @@ struct sunsky_emitter {
         else hip_check(hipStreamWaitEvent(st, ad_done, 0), "hipStreamWaitEvent");
     }
     void ad_end(hipStream_t st) const { hip_check(hipEventRecord(ad_done, st), "hipEventRecord"); }
-    // Stream-ordered upload of host-computed AD tangent tables through a pinned buffer:
-    // the host rewrites the pinned buffer only once the previous copy out of it is done.
-    void ad_upload(float* dst, const std::vector<float>& buf, hipStream_t st) const {
-        if (!h_ad) {
-            hip_check(hipHostMalloc((void**)&h_ad, sizeof(float) * kAdFloats, hipHostMallocDefault), "hipHostMalloc");
-            hip_check(hipEventCreateWithFlags(&ad_copy_done, hipEventDisableTiming), "hipEventCreate");
-        } else {
-            hip_check(hipEventSynchronize(ad_copy_done), "hipEventSynchronize");
-        }
-        std::memcpy(h_ad, buf.data(), sizeof(float) * buf.size());
-        hip_check(hipMemcpyAsync(dst, h_ad, sizeof(float) * buf.size(), hipMemcpyHostToDevice, st), "hipMemcpyAsync");
-        hip_check(hipEventRecord(ad_copy_done, st), "hipEventRecord");
+    // Device tangent staging into an AD table buffer (sunsky_stage_tangent, sunsky_staging.h):
+    // the arguments for `nbasis` bases over this emitter's datasets, then the launch.
+    TangentArgs tangent_args(float* out, int nbasis, int sun_local_off, int sun_local_first, int sun_off,
+                             int total) const {
+        TangentArgs A;
+        std::memset(&A, 0, sizeof(A));
+        A.sky_params_ds = d_sky_params_ds;
+        A.sky_rad_ds = d_sky_rad_ds;
+        A.sun_rad_ds = d_sun_rad_ds;
+        A.out = out;
+        A.nbasis = nbasis;
+        A.sun_local_off = sun_local_off;
+        A.sun_local_first = sun_local_first;
+        A.sun_off = sun_off;
+        A.sun_block = model->variant() == kSpectral ? kSunSpecTableSize : kSunRgbTableSize;
+        A.total = total;
+        return A;
+    }
+    void stage_tangent(TangentArgs& A, hipStream_t st) const {
+        void* args[] = {&A};
+        const unsigned grid = (unsigned)((A.total + 255) / 256);
+        hip_check(hipModuleLaunchKernel(mod->stage_tangent, grid, 1, 1, 256, 1, 1, 0, st, args, nullptr),
+                  "hipModuleLaunchKernel(sunsky_stage_tangent)");
     }
 };
 
@@ -978,20 +990,18 @@ int sunsky_eval_jvp(const sunsky_emitter* e, int param, const float* tangent, in
         std::vector<float> key(tangent, tangent + std::max(0, tangent_count));
         key.push_back((float)param);
         const bool stage = !e->d_jvp || e->jvp_rev != e->rev || key != e->jvp_key;
-        EvalTangent tan;
-        if (stage || n == 0) tan = e->model->eval_tangent(param, tangent, tangent_count);   // validates param / count
+        TangentStage ts;
+        if (stage || n == 0) ts = e->model->tangent_stage(param, tangent, tangent_count);   // validates param / count
         if (n == 0) return;
         require_device(e);
         hipStream_t st = (hipStream_t)stream;
         DeviceScope dev_scope(e->device);
         e->ad_begin(st);   // ordered after the previous AD call (which may read d_jvp), any stream
-        if (stage) {
-            std::vector<float> buf(128 + kSunRgbTableSize, 0.f);
-            std::memcpy(buf.data(), tan.dsky.data(), sizeof(float) * tan.dsky.size());
-            std::memcpy(buf.data() + kNbWavelengths * 10, tan.dsun_local, 3 * sizeof(float));
-            std::memcpy(buf.data() + 128, tan.dsun.data(), sizeof(float) * tan.dsun.size());
-            if (!e->d_jvp) hip_check(hipMalloc(&e->d_jvp, sizeof(float) * buf.size()), "hipMalloc");
-            e->ad_upload(e->d_jvp, buf, st);
+        if (stage) {   // the tangent tables, staged on the device (sunsky_stage_tangent)
+            if (!e->d_jvp) hip_check(hipMalloc(&e->d_jvp, sizeof(float) * sunsky_emitter::kJvpFloats), "hipMalloc");
+            TangentArgs A = e->tangent_args(e->d_jvp, 1, kTanSunLocal, 0, kJvpSunOffset, sunsky_emitter::kJvpFloats);
+            A.st[0] = ts;
+            e->stage_tangent(A, st);
             e->jvp_key = key;
             e->jvp_rev = e->rev;
         }
@@ -1008,6 +1018,37 @@ int sunsky_eval_jvp(const sunsky_emitter* e, int param, const float* tangent, in
             launch(e->mod->jvp_spec, grid_for(e->mod, K_EVAL_SPEC_RAYS_V1, n), (hipStream_t)stream, args);
         }
         e->ad_end(st);
+    });
+}
+
+int sunsky_emitter_tangent_tables(const sunsky_emitter* e, int param, const float* tangent, int tangent_count,
+                                  int on_device, float* out, size_t cap, size_t* count) {
+    if (!e || !count) return fail(SUNSKY_ERROR_INVALID_VALUE, "null argument");
+    if (!tangent) return fail(SUNSKY_ERROR_INVALID_VALUE, "null tangent");
+    return guarded([&] {
+        e->sync_host();
+        const int total = sunsky_emitter::kJvpFloats;
+        static_assert(sunsky_emitter::kJvpFloats == SUNSKY_TANGENT_FLOATS, "tangent buffer layout");
+        std::vector<float> v(total, 0.f);
+        if (on_device) {
+            require_device(e);
+            DeviceScope g(e->device);
+            float* d = nullptr;
+            hip_check(hipMalloc(&d, sizeof(float) * total), "hipMalloc");
+            TangentArgs A = e->tangent_args(d, 1, kTanSunLocal, 0, kJvpSunOffset, total);
+            A.st[0] = e->model->tangent_stage(param, tangent, tangent_count);
+            e->stage_tangent(A, nullptr);
+            hipError_t rc = hipMemcpy(v.data(), d, sizeof(float) * total, hipMemcpyDeviceToHost);
+            (void)hipFree(d);
+            hip_check(rc, "hipMemcpy");
+        } else {
+            const EvalTangent t = e->model->eval_tangent(param, tangent, tangent_count);
+            std::memcpy(v.data(), t.dsky.data(), sizeof(float) * t.dsky.size());
+            std::memcpy(v.data() + kTanSunLocal, t.dsun_local, 3 * sizeof(float));
+            std::memcpy(v.data() + kJvpSunOffset, t.dsun.data(), sizeof(float) * t.dsun.size());
+        }
+        *count = v.size();
+        if (out) std::memcpy(out, v.data(), sizeof(float) * std::min(cap, v.size()));
     });
 }
 
@@ -1030,7 +1071,6 @@ int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam
         // albedo[c] only, so the all-ones tangent is the diagonal), sun_direction x / y / z
         const SunskyModel& M = *e->model;
         const int nch = M.nch();
-        const size_t blk = (size_t)kNbWavelengths * 10;
         // 6 workgroups per CU (the RGB kernel holds 3 per CU at a time, 134 VGPRs): few per-block
         // partials, so the one-workgroup reduce below stays short (16384 partials took 0.3 ms)
         const unsigned grid = (unsigned)std::max<size_t>(
@@ -1048,25 +1088,20 @@ int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam
             hip_check(hipMalloc(&e->d_partials, sizeof(float) * 16 * grid), "hipMalloc");
             e->partials_cap = grid;
         }
-        if (stage) {
-            std::vector<float> buf(576 + kSunRgbTableSize, 0.f);
+        if (stage) {   // the 5 basis tangents, staged on the device (sunsky_stage_tangent)
+            if (!e->d_vjp) hip_check(hipMalloc(&e->d_vjp, sizeof(float) * sunsky_emitter::kVjpFloats), "hipMalloc");
+            const int nb = M.active_record() ? 2 : kVjpBases;   // sun_direction is not exposed in time mode
+            TangentArgs A = e->tangent_args(e->d_vjp, nb, kVjpSunLocal, 2, kVjpSunOffset, sunsky_emitter::kVjpFloats);
             const float one = 1.f;
-            EvalTangent tT = M.eval_tangent(kJvpTurbidity, &one, 1);
-            std::memcpy(buf.data(), tT.dsky.data(), sizeof(float) * tT.dsky.size());
-            std::memcpy(buf.data() + 576, tT.dsun.data(), sizeof(float) * tT.dsun.size());
+            A.st[0] = M.tangent_stage(kJvpTurbidity, &one, 1);
             std::vector<float> ones(nch, 1.f);
-            EvalTangent tA = M.eval_tangent(kJvpAlbedo, ones.data(), nch);
-            std::memcpy(buf.data() + blk, tA.dsky.data(), sizeof(float) * tA.dsky.size());
-            if (!M.active_record())
-                for (int k = 0; k < 3; ++k) {
-                    float axis[3] = {0.f, 0.f, 0.f};
-                    axis[k] = 1.f;
-                    EvalTangent tS = M.eval_tangent(kJvpSunDirection, axis, 3);
-                    std::memcpy(buf.data() + (2 + k) * blk, tS.dsky.data(), sizeof(float) * tS.dsky.size());
-                    std::memcpy(buf.data() + 5 * blk + 3 * k, tS.dsun_local, 3 * sizeof(float));
-                }
-            if (!e->d_vjp) hip_check(hipMalloc(&e->d_vjp, sizeof(float) * buf.size()), "hipMalloc");
-            e->ad_upload(e->d_vjp, buf, st);
+            A.st[1] = M.tangent_stage(kJvpAlbedo, ones.data(), nch);
+            for (int k = 0; k + 2 < nb; ++k) {
+                float axis[3] = {0.f, 0.f, 0.f};
+                axis[k] = 1.f;
+                A.st[2 + k] = M.tangent_stage(kJvpSunDirection, axis, 3);
+            }
+            e->stage_tangent(A, st);
             e->vjp_rev = e->rev;
         }
         const SunskyKArgs* K = e->d_state;

@@ -2059,13 +2059,13 @@ __device__ __forceinline__ void bake_spec_body(const SunskyKArgs& K, LatLong G, 
 // eval_jvp: forward-mode derivative of eval() with respect to one
 // differentiable parameter (turbidity / albedo / sun_direction, sunsky.cpp:
 // 220-240) -- what dr::forward_from(param) + dr::grad(eval(si)) give in the
-// reference.  The host stages the tangent of the tables (SunskyModel::
-// eval_tangent); this kernel carries value and tangent through the reference
-// operation order of eval (sunsky.cpp:303-352, 538-614, 631-650).
+// reference.  sunsky_stage_tangent stages the tangent of the tables on the device
+// (sunsky_staging.h, the same code as SunskyModel::eval_tangent); this kernel carries
+// value and tangent through the reference operation order of eval (sunsky.cpp:303-352,
+// 538-614, 631-650).
 // jvp buffer: [0, 110) d{A..I, rad} x 11 channels, [110, 113) d local sun
-// direction, [128, 128 + sun table size) d sun radiance table.
+// direction, [128, 128 + sun table size) d sun radiance table (kJvpSunOffset).
 // ======================================================================
-constexpr int kJvpSunOffset = 128;
 
 // sky: the channel constants, indexed per lane by the spectral AD kernels (a per-lane
 // index into the kernarg block would gather from memory, 13 loads per channel).
@@ -2295,7 +2295,6 @@ __device__ __forceinline__ void eval_jvp_spec_body(const SunskyKArgs& K, const f
 // (5 x 110), [550, 559) d local sun direction of the 3 sun axes, [576, ...) d sun table (T).
 // ======================================================================
 constexpr int kGradCount = 16;           // 0: T, 1..11: albedo channel, 12..14: sun_direction, 15: pad
-constexpr int kVjpSunOffset = 576;
 
 struct VjpLds {
     SkyChannel sky[kNbWavelengths];   // per-lane channel index in the spectral kernel (see JvpLds)
@@ -2754,6 +2753,14 @@ extern "C" __global__ __launch_bounds__(256) void sunsky_stage_radiance(StageArg
 }
 
 constexpr int kQuadBlock = 256;    // one quadrature row per workgroup, one point per thread
+
+// Tangent tables of eval_jvp / eval_vjp (sunsky_staging.h TangentArgs): one float per
+// thread, fp64 Bezier derivatives of the device-resident datasets, the same code as the
+// host model's eval_tangent.
+extern "C" __global__ __launch_bounds__(256) void sunsky_stage_tangent(TangentArgs A) {
+    for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < A.total; idx += gridDim.x * blockDim.x)
+        A.out[idx] = tangent_buffer_value(A, idx);
+}
 
 struct QuadArgs {                  // mirrors the host-side struct (sunsky_capi.cpp)
     SunskyKArgs* state;

@@ -48,47 +48,6 @@ void compute_radiance_params(const std::vector<float>& ds, int nch, int npar, co
 // (dT, dalbedo[c], deta), in fp64: d/dx of the quintic Bezier, dx/deta of
 // x = cbrt(2 eta / pi), and the derivatives of the turbidity / albedo lerps
 // (floor(T) is piecewise constant, so d t_rem / dT = 1).
-void radiance_params_jvp(const std::vector<float>& ds, int nch, int npar, const std::vector<float>& albedo,
-                         const std::vector<double>& dalbedo, float turbidity, double dT, float eta, double deta,
-                         std::vector<double>* dout) {
-    static const double coefs[kNbSkyCtrlPts] = {1, 5, 10, 10, 5, 1};
-    const int result_size = nch * npar, a_block = kNbSkyCtrlPts * result_size, t_block = kNbAlbedo * a_block;
-    const double x = std::cbrt(2.0 * eta / 3.14159265358979323846);
-    const double dx = x > 0.0 ? (2.0 / (3.0 * 3.14159265358979323846)) / (x * x) * deta : 0.0;
-    const int t_high = (int)std::floor(turbidity), t_low = t_high - 1;
-    const double t_rem = (double)turbidity - t_high;
-    const bool in_range = (0.f <= eta) && (eta <= 0.5f * kPi);
-    dout->assign(result_size, 0.0);
-    if (!in_range) return;
-    for (int e = 0; e < result_size; ++e) {
-        double bez[2][2], dbez[2][2];
-        for (int ti = 0; ti < 2; ++ti) {
-            const int t = ti ? t_high : t_low;
-            for (int a = 0; a < 2; ++a) {
-                double v = 0.0, dv = 0.0;
-                if (t >= 0 && t < kNbTurbidity)
-                    for (int k = 0; k < kNbSkyCtrlPts; ++k) {
-                        const double data = ds[(size_t)t * t_block + a * a_block + k * result_size + e];
-                        const int m = kNbSkyCtrlPts - 1 - k;
-                        v += coefs[k] * std::pow(x, k) * std::pow(1.0 - x, m) * data;
-                        double db = 0.0;
-                        if (k > 0) db += k * std::pow(x, k - 1) * std::pow(1.0 - x, m);
-                        if (m > 0) db -= m * std::pow(x, k) * std::pow(1.0 - x, m - 1);
-                        dv += coefs[k] * db * data;
-                    }
-                bez[ti][a] = v;
-                dbez[ti][a] = dv * dx;
-            }
-        }
-        const double ra_low = bez[0][0] + t_rem * (bez[1][0] - bez[0][0]);
-        const double ra_high = bez[0][1] + t_rem * (bez[1][1] - bez[0][1]);
-        const double dra_low = dbez[0][0] + t_rem * (dbez[1][0] - dbez[0][0]) + (bez[1][0] - bez[0][0]) * dT;
-        const double dra_high = dbez[0][1] + t_rem * (dbez[1][1] - dbez[0][1]) + (bez[1][1] - bez[0][1]) * dT;
-        const double alb = albedo[e / npar];
-        (*dout)[e] = dra_low + alb * (dra_high - dra_low) + (ra_high - ra_low) * dalbedo[e / npar];
-    }
-}
-
 // compute_sun_params, sunsky.h:404-419
 void compute_sun_params(const std::vector<float>& ds, int block, const RadianceStage& rs, std::vector<float>* out) {
     out->assign(block, 0.f);
@@ -661,21 +620,20 @@ void SunskyModel::validate() const {
         if (a < 0.f || a > 1.f) throw std::invalid_argument(fmt("Albedo values must be in [0, 1], got: %f", a));
 }
 
-EvalTangent SunskyModel::eval_tangent(int param, const float* tangent, int count) const {
-    const bool spec = variant_ == kSpectral;
-    double dT = 0.0, deta = 0.0;
-    std::vector<double> dalb(nch_, 0.0);
-    EvalTangent out;
+TangentStage SunskyModel::tangent_stage(int param, const float* tangent, int count) const {
     if (!tangent) throw std::invalid_argument("null tangent");
+    TangentStage s;
+    std::memset(&s, 0, sizeof(s));
+    double deta = 0.0;
     switch (param) {
         case kJvpTurbidity:
             if (count != 1) throw std::invalid_argument("turbidity tangent has 1 value");
-            dT = tangent[0];
+            s.dT = tangent[0];
             break;
         case kJvpAlbedo:
             if (count != 1 && count != nch_)
                 throw std::invalid_argument("albedo tangent has 1 or " + std::to_string(nch_) + " values");
-            for (int c = 0; c < nch_; ++c) dalb[c] = tangent[count == 1 ? 0 : c];
+            for (int c = 0; c < nch_; ++c) s.dalbedo[c] = tangent[count == 1 ? 0 : c];
             break;
         case kJvpSunDirection: {
             if (active_record_) throw std::invalid_argument("sun_direction is not differentiable in time/location mode");
@@ -685,7 +643,7 @@ EvalTangent SunskyModel::eval_tangent(int param, const float* tangent, int count
             for (int r = 0; r < 3; ++r)
                 dl[r] = to_local_d_[r * 3] * tangent[0] + to_local_d_[r * 3 + 1] * tangent[1] +
                         to_local_d_[r * 3 + 2] * tangent[2];
-            for (int r = 0; r < 3; ++r) out.dsun_local[r] = (float)dl[r];
+            for (int r = 0; r < 3; ++r) s.dsun_local[r] = (float)dl[r];
             // theta = unit_angle_z(local) (from_spherical, sunsky.h:84-89); eta = pi/2 - theta
             const double lz = k_.sun_n[2];
             const double w[3] = {k_.sun_n[0], k_.sun_n[1], lz - (std::signbit(lz) ? -1.0 : 1.0)};
@@ -699,26 +657,30 @@ EvalTangent SunskyModel::eval_tangent(int param, const float* tangent, int count
         }
         default: throw std::invalid_argument("unknown differentiable parameter");
     }
+    // the staging scalars of compute_radiance_params (sunsky.h:158-231) and their tangents:
+    // x = cbrt(2 eta / pi), dx = 2 / (3 pi x^2) deta; t_rem = T - floor(T), d t_rem / dT = 1
     const float eta = 0.5f * kPi - k_.sun_theta;
-    std::vector<double> dp, dr;
-    radiance_params_jvp(sky_params_ds_, nch_, kNbSkyParams, albedo_, dalb, turbidity_, dT, eta, deta, &dp);
-    radiance_params_jvp(sky_rad_ds_, nch_, 1, albedo_, dalb, turbidity_, dT, eta, deta, &dr);
+    s.x = std::cbrt(2.0 * eta / 3.14159265358979323846);
+    s.dx = s.x > 0.0 ? (2.0 / (3.0 * 3.14159265358979323846)) / (s.x * s.x) * deta : 0.0;
+    s.t_high = (int)std::floor(turbidity_);
+    s.t_low = s.t_high - 1;
+    s.t_rem = (double)turbidity_ - s.t_high;
+    s.in_range = (0.f <= eta) && (eta <= 0.5f * kPi);
+    s.nch = nch_;
+    for (int c = 0; c < nch_; ++c) s.albedo[c] = albedo_[c];
+    return s;
+}
+
+EvalTangent SunskyModel::eval_tangent(int param, const float* tangent, int count) const {
+    const TangentStage s = tangent_stage(param, tangent, count);
+    EvalTangent out;
     out.dsky.assign((size_t)nch_ * 10, 0.f);
-    for (int c = 0; c < nch_; ++c) {
-        for (int q = 0; q < kNbSkyParams; ++q) out.dsky[c * 10 + q] = (float)dp[c * kNbSkyParams + q];
-        out.dsky[c * 10 + 9] = (float)dr[c];
-    }
+    for (int j = 0; j < nch_ * 10; ++j) out.dsky[j] = tangent_value(sky_params_ds_.data(), sky_rad_ds_.data(), s, j);
+    std::memcpy(out.dsun_local, s.dsun_local, sizeof(out.dsun_local));
     // sun table: lerp over turbidity (compute_sun_params, sunsky.h:404-419)
-    const int block = spec ? kSunSpecTableSize : kSunRgbTableSize;
+    const int block = variant_ == kSpectral ? kSunSpecTableSize : kSunRgbTableSize;
     out.dsun.assign(block, 0.f);
-    if (dT != 0.0) {
-        const int t_high = (int)std::floor(turbidity_), t_low = t_high - 1;
-        for (int i = 0; i < block; ++i) {
-            const double lo = (t_low >= 0 && t_low < kNbTurbidity) ? sun_rad_ds_[(size_t)t_low * block + i] : 0.0;
-            const double hi = (t_high >= 0 && t_high < kNbTurbidity) ? sun_rad_ds_[(size_t)t_high * block + i] : 0.0;
-            out.dsun[i] = (float)((hi - lo) * dT);
-        }
-    }
+    for (int i = 0; i < block; ++i) out.dsun[i] = sun_param_tangent(sun_rad_ds_.data(), block, i, s);
     return out;
 }
 

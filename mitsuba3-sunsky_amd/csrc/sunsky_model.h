@@ -86,6 +86,8 @@ public:
     // Tangent of the eval tables for param (JvpParam) along `tangent`
     // (turbidity: 1 value; albedo: 1 or nch; sun_direction: 3, world space).
     EvalTangent eval_tangent(int param, const float* tangent, int count) const;
+    // The scalars of that tangent (validates param / count), for the device tangent staging
+    TangentStage tangent_stage(int param, const float* tangent, int count) const;
     std::vector<std::string> warnings;
 
 private:

@@ -61,6 +61,119 @@ SS_HD inline float sun_param(const float* ds, int block, int i, const RadianceSt
     return lerpf_(lo, hi, s.t_rem);
 }
 
+// ---------------------------------------------------------------- AD staging
+// Tangent of the staging for one differentiable parameter (traverse(), sunsky.cpp:220-240)
+// at the current (turbidity, eta, albedo): what Dr.Jit's forward mode propagates through
+// compute_radiance_params / compute_sun_params (sunsky.h:158-231, 404-419) before eval.
+// The host fills the few scalars (x = cbrt(2 eta / pi) and dx = dx/deta x deta, t_rem,
+// the albedo tangent); every table entry is then radiance_param_tangent / sun_param_tangent,
+// run by the host model (eval_tangent) and by the device kernel sunsky_stage_tangent in
+// fp64 with integer powers by repeated products: the same bits on both sides.
+struct TangentStage {
+    double x, dx;                 // Bezier abscissa and its tangent
+    double t_rem, dT;             // turbidity lerp factor (d t_rem / dT = 1, floor(T) constant)
+    int t_low, t_high, in_range, nch;
+    double albedo[kNbWavelengths], dalbedo[kNbWavelengths];
+    float dsun_local[3];          // tangent of the local sun direction (sun_direction)
+};
+
+SS_HD inline double powid_(double x, int k) {
+    double r = 1.0;
+    for (int i = 0; i < k; ++i) r *= x;
+    return r;
+}
+
+// d compute_radiance_params entry e of a (nch x npar) result (sunsky.h:158-231): the
+// quintic Bezier and its derivative, the turbidity lerp, the albedo lerp.
+SS_HD inline double radiance_param_tangent(const float* ds, int npar, int e, const TangentStage& s) {
+    SS_NO_CONTRACT
+    const double coefs[kNbSkyCtrlPts] = {1, 5, 10, 10, 5, 1};
+    const int result_size = s.nch * npar, a_block = kNbSkyCtrlPts * result_size, t_block = kNbAlbedo * a_block;
+    if (!s.in_range) return 0.0;
+    double bez[2][2], dbez[2][2];
+    for (int ti = 0; ti < 2; ++ti) {
+        const int t = ti ? s.t_high : s.t_low;
+        for (int a = 0; a < 2; ++a) {
+            double v = 0.0, dv = 0.0;
+            if (t >= 0 && t < kNbTurbidity)
+                for (int k = 0; k < kNbSkyCtrlPts; ++k) {
+                    const double data = ds[(size_t)t * t_block + a * a_block + k * result_size + e];
+                    const int m = kNbSkyCtrlPts - 1 - k;
+                    v += coefs[k] * powid_(s.x, k) * powid_(1.0 - s.x, m) * data;
+                    double db = 0.0;
+                    if (k > 0) db += k * powid_(s.x, k - 1) * powid_(1.0 - s.x, m);
+                    if (m > 0) db -= m * powid_(s.x, k) * powid_(1.0 - s.x, m - 1);
+                    dv += coefs[k] * db * data;
+                }
+            bez[ti][a] = v;
+            dbez[ti][a] = dv * s.dx;
+        }
+    }
+    const double ra_low = bez[0][0] + s.t_rem * (bez[1][0] - bez[0][0]);
+    const double ra_high = bez[0][1] + s.t_rem * (bez[1][1] - bez[0][1]);
+    const double dra_low = dbez[0][0] + s.t_rem * (dbez[1][0] - dbez[0][0]) + (bez[1][0] - bez[0][0]) * s.dT;
+    const double dra_high = dbez[0][1] + s.t_rem * (dbez[1][1] - dbez[0][1]) + (bez[1][1] - bez[0][1]) * s.dT;
+    const int c = e / npar;
+    return dra_low + s.albedo[c] * (dra_high - dra_low) + (ra_high - ra_low) * s.dalbedo[c];
+}
+
+// d compute_sun_params entry i (sunsky.h:404-419): the turbidity lerp's slope times dT
+SS_HD inline float sun_param_tangent(const float* ds, int block, int i, const TangentStage& s) {
+    SS_NO_CONTRACT
+    if (s.dT == 0.0) return 0.f;
+    const double lo = (s.t_low >= 0 && s.t_low < kNbTurbidity) ? ds[(size_t)s.t_low * block + i] : 0.0;
+    const double hi = (s.t_high >= 0 && s.t_high < kNbTurbidity) ? ds[(size_t)s.t_high * block + i] : 0.0;
+    return (float)((hi - lo) * s.dT);
+}
+
+// Layouts of the tangent tables the AD kernels read (sunsky_kernels.hip): per basis a
+// block of kTanBlock floats, d{A..I, rad} of channel c at c * 10 (+ q); the local sun
+// direction's tangent at kTanSunLocal (JVP) or kVjpSunLocal + 3 k (VJP, sun axis k);
+// the sun table's at kJvpSunOffset (JVP) / kVjpSunOffset (VJP, turbidity basis).
+constexpr int kTanBlock = kNbWavelengths * 10;   // 110
+constexpr int kTanSunLocal = kTanBlock;          // JVP: 110..112
+constexpr int kJvpSunOffset = 128;
+constexpr int kVjpBases = 5;                     // turbidity, albedo (diagonal), sun x / y / z
+constexpr int kVjpSunLocal = kVjpBases * kTanBlock;   // 550..558
+constexpr int kVjpSunOffset = 576;
+
+// Sky-channel entry j = c x 10 + q (< nch x 10) of one basis' tangent block: d{A..I}
+// (q < 9) from the sky parameter dataset, d rad (q = 9) from the sky radiance dataset.
+SS_HD inline float tangent_value(const float* sky_params_ds, const float* sky_rad_ds, const TangentStage& s, int j) {
+    const int c = j / 10, q = j % 10;
+    return (float)(q < kNbSkyParams ? radiance_param_tangent(sky_params_ds, kNbSkyParams, c * kNbSkyParams + q, s)
+                                    : radiance_param_tangent(sky_rad_ds, 1, c, s));
+}
+
+// Arguments of the device tangent staging (sunsky_stage_tangent): `nbasis` tangents,
+// basis b's sky block at out + b x kTanBlock, the local sun tangents of bases
+// [sun_local_first, nbasis) at out + sun_local_off (3 each), basis 0's sun-table tangent
+// at out + sun_off; every other float of [0, total) is written 0.
+struct TangentArgs {
+    const float* sky_params_ds;
+    const float* sky_rad_ds;
+    const float* sun_rad_ds;
+    float* out;
+    int nbasis, sun_local_off, sun_local_first, sun_off, sun_block, total;
+    TangentStage st[kVjpBases];
+};
+
+// Float idx of the tangent buffer described by A (the device kernel's per-thread work).
+SS_HD inline float tangent_buffer_value(const TangentArgs& A, int idx) {
+    if (idx < A.nbasis * kTanBlock) {
+        const int b = idx / kTanBlock, j = idx % kTanBlock;
+        return j < A.st[b].nch * 10 ? tangent_value(A.sky_params_ds, A.sky_rad_ds, A.st[b], j) : 0.f;
+    }
+    const int nloc = 3 * (A.nbasis - A.sun_local_first);
+    if (idx >= A.sun_local_off && idx < A.sun_local_off + nloc) {
+        const int k = (idx - A.sun_local_off) / 3, r = (idx - A.sun_local_off) % 3;
+        return A.st[A.sun_local_first + k].dsun_local[r];
+    }
+    if (idx >= A.sun_off && idx < A.sun_off + A.sun_block)
+        return sun_param_tangent(A.sun_rad_ds, A.sun_block, idx - A.sun_off, A.st[0]);
+    return 0.f;
+}
+
 // One staged sky channel from its 9 coefficients and radiance: the reference-order
 // record (render_sky) and the FAST record with the output scale folded in
 // (sky_scale, x MI_CIE_Y_NORMALIZATION for RGB; sunsky.cpp:303-352).

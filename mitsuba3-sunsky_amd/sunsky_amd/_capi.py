@@ -97,6 +97,8 @@ _SIGS = {
     "plugin_name": (C.c_char_p, []),
     "plugin_descr": (C.c_char_p, []),
     "sunsky_eval_vjp": (C.c_int, [vp, Vec3In, vp, C.c_int, C.c_size_t, vp, C.c_size_t, vp, C.c_size_t, vp, vp]),
+    "sunsky_emitter_tangent_tables": (C.c_int, [vp, C.c_int, c_float_p, C.c_int, C.c_int, c_float_p, C.c_size_t,
+                                                C.POINTER(C.c_size_t)]),
     "sunsky_array_from_file": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_double), C.c_size_t,
                                          C.POINTER(C.c_size_t), C.POINTER(C.c_uint64), C.POINTER(C.c_int)]),
     "sunsky_array_to_file": (C.c_int, [C.c_char_p, c_float_p, C.c_size_t, C.POINTER(C.c_uint64), C.c_int]),

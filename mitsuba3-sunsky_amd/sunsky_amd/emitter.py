@@ -385,6 +385,22 @@ class SunskyEmitter:
                                     self._stream()))
         return out, dout
 
+    def tangent_tables(self, param, tangent, on_device=True):
+        """The tangent of the staged tables along `tangent` of `param` (sunsky.h:158-231,
+        404-419): {"dsky": (nch, 10) d{A..I, rad}, "dsun_local": (3,), "dsun": sun table},
+        staged by the device kernel eval_jvp uses, or on the host."""
+        tan = [float(x) for x in np.atleast_1d(np.asarray(tangent, dtype=np.float32))]
+        if param not in PARAMS:
+            raise ValueError(f"'{param}' is not a differentiable parameter ({', '.join(PARAMS)})")
+        buf = (C.c_float * (128 + 3240))()
+        cnt = C.c_size_t()
+        check(lib().sunsky_emitter_tangent_tables(self._h, PARAMS[param], _fa(tan), len(tan), int(on_device), buf,
+                                                  len(buf), C.byref(cnt)))
+        v = np.frombuffer(buf, dtype=np.float32, count=cnt.value).copy()
+        nch = self.info()["nb_channels"]
+        block = 3240 if nch == 3 else 1980
+        return {"dsky": v[: nch * 10].reshape(nch, 10), "dsun_local": v[110:113], "dsun": v[128:128 + block]}
+
     def eval_vjp(self, si, d_out, active=None, grad=None):
         """Reverse mode: accumulate sum(d_out * d eval(si) / d param) into `grad` (a (16,)
         device tensor; zeros if None) and return it together with a dict view

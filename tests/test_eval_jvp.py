@@ -182,3 +182,73 @@ def test_ad_tables_restaged_after_parameter_change(variant):
         g_s, _ = em.eval_vjp(si, cot)
     s.synchronize()
     assert torch.equal(g_s, g_ref)
+
+
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+@pytest.mark.parametrize("param,tangent", [("turbidity", [1.0]), ("albedo", [0.7]),
+                                           ("sun_direction", [0.3, -0.2, 0.5])])
+def test_host_tangent_tables_match_finite_differences_of_the_staging(variant, param, tangent):
+    """CPU: the staging tangent (sunsky_staging.h radiance_param_tangent / sun_param_tangent,
+    through sunsky_emitter_tangent_tables on the host) against central differences of the
+    host-staged tables themselves (compute_radiance_params / compute_sun_params,
+    sunsky.h:158-231, 404-419) at a step of 1e-3 along the tangent."""
+    base = scene(turb=3.4, sun=[math.sin(math.pi / 2 - ETA) * math.cos(0.6), math.sin(math.pi / 2 - ETA) * math.sin(0.6),
+                                math.cos(math.pi / 2 - ETA)])
+    em = ss.SunskyEmitter(base, variant, device="host")
+    t = em.tangent_tables(param, tangent, on_device=False)
+    h = 1e-3
+
+    def staged(sign):
+        # through traverse() + update(), as Dr.Jit differentiates: m_sun_dir is used as set
+        # (parameters_changed, sunsky.cpp:242-285), not renormalised like the constructor's
+        e = ss.SunskyEmitter(base, variant, device="host")
+        p = e.traverse()
+        if param == "turbidity":
+            p["turbidity"] = base["turbidity"] + sign * h * tangent[0]
+        elif param == "albedo":
+            p["albedo"] = base["albedo"] + sign * h * tangent[0]
+        else:
+            p["sun_direction"] = [s + sign * h * v for s, v in zip(np.asarray(p["sun_direction"], np.float64), tangent)]
+        p.update()
+        nch = e.info()["nb_channels"]
+        sky = np.concatenate([e.table("sky_params").reshape(nch, 9), e.table("sky_radiance")[:, None]], axis=1)
+        return sky.astype(np.float64), e.table("sun_radiance").astype(np.float64)
+
+    (sp, up), (sm, um) = staged(1), staged(-1)
+    fd_sky, fd_sun = (sp - sm) / (2 * h), (up - um) / (2 * h)
+    scale = np.abs(fd_sky).max(axis=1, keepdims=True) + 1e-12
+    # fp32 tables differenced at h = 1e-3: ~1e-4 of each channel's largest entry
+    assert np.all(np.abs(t["dsky"] - fd_sky) <= 2e-2 * np.abs(fd_sky) + 2e-3 * scale), \
+        np.max(np.abs(t["dsky"] - fd_sky) / (2e-2 * np.abs(fd_sky) + 2e-3 * scale))
+    assert np.all(np.abs(t["dsun"] - fd_sun) <= 2e-2 * np.abs(fd_sun) + 2e-3 * (np.abs(fd_sun).max() + 1e-12))
+    if param == "sun_direction":
+        assert np.abs(t["dsun_local"]).max() > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+@pytest.mark.parametrize("rotated", [False, True])
+def test_device_tangent_staging_is_the_host_tangent_bitwise(variant, rotated):
+    """f2: the tangent tables eval_jvp / eval_vjp read are staged by the device kernel
+    sunsky_stage_tangent (sunsky_staging.h, fp64), bit for bit the host model's
+    eval_tangent for every differentiable parameter, after a parameter update too."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    d = scene()
+    d["sun_direction"] = [0.4, 0.3, 0.8]
+    if rotated:
+        c, s = math.cos(0.5), math.sin(0.5)
+        d["to_world"] = np.array([[c, -s, 0, 0], [s, c, 0, 0], [0, 0, 1, 0], [0, 0, 0, 1]], np.float32)
+    em = ss.SunskyEmitter(d, variant)
+    cases = [("turbidity", [1.0]), ("turbidity", [-2.5]), ("albedo", [1.0]), ("albedo", [0.3] * em.info()["nb_channels"]),
+             ("sun_direction", [1.0, 0.0, 0.0]), ("sun_direction", [0.1, -0.7, 0.2])]
+    for step in range(2):
+        for param, tan in cases:
+            dev = em.tangent_tables(param, tan, on_device=True)
+            hst = em.tangent_tables(param, tan, on_device=False)
+            for k in dev:
+                assert np.array_equal(dev[k].view(np.uint32), hst[k].view(np.uint32)), (param, tan, k)
+        p = em.traverse()
+        p["turbidity"] = 7.25
+        p["albedo"] = 0.55
+        p.update()

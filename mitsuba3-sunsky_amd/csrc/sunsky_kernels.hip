@@ -516,8 +516,53 @@ __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const float
     eval_rgb_local<FAST>(K, chan_table<FAST>(K), sun_tab, wo, mask, out);
 }
 
-// Spectral sun disc term for channel pair (lo, hi, f): lerp(sun) x limb darkening
-// (sunsky.cpp:341-347); hi = 11 at exactly 720 nm carries weight 0.
+// Powers of the sun disc's polynomial variables, shared by every wavelength of a lane:
+// x^k (render_sun, sunsky.cpp:586-594) and cos psi^j (compute_sun_ld, :631-650), each by
+// repeated products as dr::pow(x, k) / powif_ form them.
+struct SunPowers {
+    float x1, x2, x3;
+    float c[kNbSunLdParams];
+};
+
+__device__ __forceinline__ SunPowers sun_powers(float x, float cpsi) {
+    SunPowers p;
+    p.x1 = x;
+    p.x2 = p.x1 * p.x1;
+    p.x3 = p.x2 * p.x1;
+    p.c[0] = 1.f;
+    p.c[1] = cpsi;
+#pragma unroll
+    for (int j = 2; j < kNbSunLdParams; ++j) p.c[j] = p.c[j - 1] * cpsi;
+    return p;
+}
+
+// render_sun, spectral branch (sunsky.cpp:586-594): sum_k x^k S[pos][c][k] in k order, the
+// 4 control points of (pos, c) in one 16-byte read (the table is 16-byte aligned)
+__device__ __forceinline__ float sun_spec_poly(const float* table, int pos, int c, const SunPowers& p) {
+    const float4 s = *reinterpret_cast<const float4*>(table + (pos * kNbWavelengths + c) * kNbSunCtrlPts);
+    return fmaf(p.x3, s.w, fmaf(p.x2, s.z, fmaf(p.x1, s.y, s.x)));
+}
+
+// Spectral sun disc term for channel pair (lo, lo + 1, f): lerp(sun) x limb darkening
+// (sunsky.cpp:341-347, compute_sun_ld :631-650).  At 720 nm (lo = 10, f = 0) the pair is
+// (10, 10): lerpf_ returns its first operand at f = 0, so the reference's weight-0
+// channel 11 never enters.
+template <bool FAST>
+__device__ __forceinline__ float sun_spec_pair(const SunskyKArgs& K, const float* sun_tab, const float* ld_tab,
+                                               int pos, const SunPowers& p, int lo, float f) {
+    const int hi = lo + 1 < kNbWavelengths ? lo + 1 : lo;
+    const float sun = lerpf_(sun_spec_poly(sun_tab, pos, lo, p), sun_spec_poly(sun_tab, pos, hi, p), f);
+    float ld = 0.f;
+#pragma unroll
+    for (int j = 0; j < kNbSunLdParams; ++j)
+        ld = fmaf(p.c[j], lerpf_(ld_tab[lo * kNbSunLdParams + j], ld_tab[hi * kNbSunLdParams + j], f), ld);
+    return FAST ? K.sun_mul * (sun * ld) : K.sun_scale * sun * ld * K.area_ratio;
+}
+
+// One wavelength's term in the eval kernels, where the disc is rare (~1e-5 of random
+// directions) and the VEC=4 bodies keep 4 directions in registers: the rolled render_sun_spec /
+// sun_limb_darkening loops.  (sun_spec_pair there lets the compiler schedule the 4 directions'
+// table reads together: 70 -> 94 VGPRs in the node kernel, measured statically.)
 template <bool FAST>
 __device__ __forceinline__ float sun_spec_term(const SunskyKArgs& K, const float* sun_tab, const float* ld_tab,
                                                const DirTerms& t, int lo, float f) {
@@ -906,7 +951,7 @@ struct SamplerLds {
     TgmmLds<FAST> tgmm;
     ChanLdsN<FAST, SPEC ? kNbWavelengths : 3> chans;   // spectral: per-lane channel index
     SpecDistLds sdist[SPEC ? 1 : 0];
-    float sun[SPEC ? kSunSpecTableSize : 0];       // spectral: the whole turbidity-lerped table
+    alignas(16) float sun[SPEC ? kSunSpecTableSize : 0];   // spectral: the whole turbidity-lerped table
     SunRowsRgb rows[SPEC ? 0 : 1];                 // RGB: the disc's segments, channels interleaved
     float ld[SPEC ? kNbWavelengths * kNbSunLdParams : 0];
 };
@@ -1285,6 +1330,17 @@ __device__ __forceinline__ void sample_direction_body(
             DirTerms t = dir_terms<FAST>(K, wo, act);
             add_sun_terms<FAST>(K, t);
             const float inv_pd = fdiv<FAST>(1.f, pd);
+            if (nlam == 4) {   // Mitsuba's Spectrum<Float, 4>: the LEAN kernel's eval, same bits
+                const float l4[4] = {lam[i], lam[lstride + i], lam[2 * lstride + i], lam[3 * lstride + i]};
+                float e[4];
+                eval_spec4<FAST>(K, S.chans.c, S.sun, S.ld, t, l4, e);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float w = FAST ? e[k] * inv_pd : e[k] / pd;
+                    weight[(size_t)k * wstride + i] = isfinite(w) ? w : 0.f;
+                }
+                continue;
+            }
             for (int k = 0; k < nlam; ++k) {
                 float e = eval_spec_one<FAST>(K, S.chans.c, S.sun, S.ld, t, lam[(size_t)k * lstride + i]);
                 float w = FAST ? e * inv_pd : e / pd;
@@ -1315,22 +1371,23 @@ __device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const typename 
         lo[k] = c < kNbWavelengths - 2 ? c : kNbWavelengths - 2;
         f[k] = ok[k] ? nw - (float)lo[k] : 0.f;
     }
+#ifndef SS_PROBE_SPEC_NO_SKY   // probe builds (tools/Makefile) only: cost ablations
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         e[k] = lerpf_(sky_eval<FAST>(chans[lo[k]], t, K.sky_scale), sky_eval<FAST>(chans[lo[k] + 1], t, K.sky_scale),
                       f[k]);
-    if (t.hit_sun) {
-#pragma unroll 1
-        for (int k = 0; k < 4; ++k) {
-            const int a = lo[k], b = a + 1;
-            const float sun = lerpf_(render_sun_spec(sun_tab, t.sun_pos, a, t.sun_x),
-                                     render_sun_spec(sun_tab, t.sun_pos, b, t.sun_x), f[k]);
-            float ld = 0.f;
+#else
 #pragma unroll
-            for (int j = 0; j < kNbSunLdParams; ++j)
-                ld += powif_(t.sun_cpsi, j) * lerpf_(ld_tab[a * kNbSunLdParams + j], ld_tab[b * kNbSunLdParams + j], f[k]);
-            e[k] += FAST ? K.sun_mul * (sun * ld) : K.sun_scale * sun * ld * K.area_ratio;
-        }
+    for (int k = 0; k < 4; ++k) e[k] = f[k] * t.r;
+#endif
+#ifndef SS_PROBE_SPEC_NO_SUN
+    if (t.hit_sun) {
+#else
+    if (false) {
+#endif
+        const SunPowers p = sun_powers(t.sun_x, t.sun_cpsi);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[k] += sun_spec_pair<FAST>(K, sun_tab, ld_tab, t.sun_pos, p, lo[k], f[k]);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) e[k] = ok[k] ? e[k] : 0.f;
@@ -1366,11 +1423,19 @@ __device__ __forceinline__ void sample_direction_spec4_body(
         for (int k = 0; k < 4; ++k) l[k] = nl[k];
         if (i + stride < n) load(i + stride);
         const bool pick_sky = sx < K.w_sky;
+#ifndef SS_PROBE_NO_SKY_SAMPLE
         const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
+#else
+        const float3_ sd = sample_sun<FAST>(K, div_exact<FAST>(sx - K.w_sky, w_sun, inv_w_sun), sy);
+#endif
         const bool act = sd.z >= 0.f;
         const float3_ d = to_world(K, sd);
         float skyp, sunp;
+#ifndef SS_PROBE_NO_PDF
         compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+#else
+        skyp = sd.z; sunp = K.sun_pdf;
+#endif
         const float pd = lerpf_(sunp, skyp, K.w_sky);
         store_nt(d.x, dx + i);
         store_nt(d.y, dy + i);

@@ -45,6 +45,9 @@ using namespace sunsky;
 #ifndef SS_RGB_ATTR
 #define SS_RGB_ATTR
 #endif
+#ifndef SS_SPEC_SAMPLE_ATTR
+#define SS_SPEC_SAMPLE_ATTR
+#endif
 constexpr float kLog2e = 1.44269504088896340736f;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -543,19 +546,34 @@ __device__ __forceinline__ float sun_spec_poly(const float* table, int pos, int 
     return fmaf(p.x3, s.w, fmaf(p.x2, s.z, fmaf(p.x1, s.y, s.x)));
 }
 
+// Limb-darkening coefficients of channel c and of c + 1 (c itself for the last channel)
+// interleaved, ldp[c][j] = (ld[c][j], ld[c + 1][j]): a channel pair's 12 coefficients in
+// three 16-byte LDS reads instead of twelve 4-byte ones.
+__device__ __forceinline__ void stage_ld_pairs(const float* ld, float* ldp) {
+    for (int e = threadIdx.x; e < kNbWavelengths * 2 * kNbSunLdParams; e += blockDim.x) {
+        const int c = e / (2 * kNbSunLdParams), j = (e / 2) % kNbSunLdParams, h = e & 1;
+        const int cc = h && c + 1 < kNbWavelengths ? c + 1 : c;
+        ldp[e] = ld[cc * kNbSunLdParams + j];
+    }
+}
+
 // Spectral sun disc term for channel pair (lo, lo + 1, f): lerp(sun) x limb darkening
 // (sunsky.cpp:341-347, compute_sun_ld :631-650).  At 720 nm (lo = 10, f = 0) the pair is
 // (10, 10): lerpf_ returns its first operand at f = 0, so the reference's weight-0
 // channel 11 never enters.
 template <bool FAST>
-__device__ __forceinline__ float sun_spec_pair(const SunskyKArgs& K, const float* sun_tab, const float* ld_tab,
+__device__ __forceinline__ float sun_spec_pair(const SunskyKArgs& K, const float* sun_tab, const float* ldp,
                                                int pos, const SunPowers& p, int lo, float f) {
     const int hi = lo + 1 < kNbWavelengths ? lo + 1 : lo;
     const float sun = lerpf_(sun_spec_poly(sun_tab, pos, lo, p), sun_spec_poly(sun_tab, pos, hi, p), f);
+    const float4* q = reinterpret_cast<const float4*>(ldp + lo * 2 * kNbSunLdParams);
     float ld = 0.f;
 #pragma unroll
-    for (int j = 0; j < kNbSunLdParams; ++j)
-        ld = fmaf(p.c[j], lerpf_(ld_tab[lo * kNbSunLdParams + j], ld_tab[hi * kNbSunLdParams + j], f), ld);
+    for (int h = 0; h < kNbSunLdParams / 2; ++h) {
+        const float4 v = q[h];   // (lo, hi) of coefficients 2h and 2h + 1
+        ld = fmaf(p.c[2 * h], lerpf_(v.x, v.y, f), ld);
+        ld = fmaf(p.c[2 * h + 1], lerpf_(v.z, v.w, f), ld);
+    }
     return FAST ? K.sun_mul * (sun * ld) : K.sun_scale * sun * ld * K.area_ratio;
 }
 
@@ -954,6 +972,7 @@ struct SamplerLds {
     alignas(16) float sun[SPEC ? kSunSpecTableSize : 0];   // spectral: the whole turbidity-lerped table
     SunRowsRgb rows[SPEC ? 0 : 1];                 // RGB: the disc's segments, channels interleaved
     float ld[SPEC ? kNbWavelengths * kNbSunLdParams : 0];
+    alignas(16) float ldp[SPEC ? kNbWavelengths * 2 * kNbSunLdParams : 0];   // spectral: LdPairs layout
 };
 
 template <bool FAST, bool SPEC>
@@ -963,6 +982,7 @@ __device__ __forceinline__ void stage_sampler_lds(const SunskyKArgs& K, SamplerL
     if constexpr (SPEC) {
         stage_spec_dist(K, &s->sdist[0]);
         lds_copy(s->ld, K.sun_ld, kNbWavelengths * kNbSunLdParams);
+        stage_ld_pairs(K.sun_ld, s->ldp);
     }
     if constexpr (SPEC) lds_copy(s->sun, K.sun_table, kSunSpecTableSize);
     else stage_sun_rows(K, s->rows);
@@ -1333,7 +1353,7 @@ __device__ __forceinline__ void sample_direction_body(
             if (nlam == 4) {   // Mitsuba's Spectrum<Float, 4>: the LEAN kernel's eval, same bits
                 const float l4[4] = {lam[i], lam[lstride + i], lam[2 * lstride + i], lam[3 * lstride + i]};
                 float e[4];
-                eval_spec4<FAST>(K, S.chans.c, S.sun, S.ld, t, l4, e);
+                eval_spec4<FAST>(K, S.chans.c, S.sun, S.ldp, t, l4, e);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const float w = FAST ? e[k] * inv_pd : e[k] / pd;
@@ -1358,7 +1378,7 @@ __device__ __forceinline__ void sample_direction_body(
 // terms of the 4 wavelengths run in one branch per lane.
 template <bool FAST>
 __device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
-                                           const float* sun_tab, const float* ld_tab, const DirTerms& t,
+                                           const float* sun_tab, const float* ldp, const DirTerms& t,
                                            const float lam[4], float e[4]) {
     int lo[4];
     float f[4];
@@ -1387,7 +1407,7 @@ __device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const typename 
 #endif
         const SunPowers p = sun_powers(t.sun_x, t.sun_cpsi);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) e[k] += sun_spec_pair<FAST>(K, sun_tab, ld_tab, t.sun_pos, p, lo[k], f[k]);
+        for (int k = 0; k < 4; ++k) e[k] += sun_spec_pair<FAST>(K, sun_tab, ldp, t.sun_pos, p, lo[k], f[k]);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) e[k] = ok[k] ? e[k] : 0.f;
@@ -1444,7 +1464,7 @@ __device__ __forceinline__ void sample_direction_spec4_body(
         DirTerms t = dir_terms<FAST>(K, to_local(K, d), act);
         add_sun_terms<FAST>(K, t);
         float e[4];
-        eval_spec4<FAST>(K, S.chans.c, S.sun, S.ld, t, l, e);
+        eval_spec4<FAST>(K, S.chans.c, S.sun, S.ldp, t, l, e);
         const float inv_pd = fdiv<FAST>(1.f, pd);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1461,15 +1481,27 @@ template <bool FAST>
 __device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const SamplerLds<FAST, false>& S, float sx,
                                                float sy, bool act, float inv_w, float inv_w_sun, float o[7]) {
     const bool pick_sky = sx < K.w_sky;
+#ifndef SS_PROBE_NO_SKY_SAMPLE   // probe builds (tools/Makefile) only: cost ablations
     const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
+#else
+    const float3_ sd = sample_sun<FAST>(K, div_exact<FAST>(sx - K.w_sky, 1.f - K.w_sky, inv_w_sun), sy);
+#endif
     act = act && (sd.z >= 0.f);
     const float3_ d = to_world(K, sd);
     float skyp, sunp;
+#ifndef SS_PROBE_NO_PDF
     compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+#else
+    skyp = sd.z; sunp = K.sun_pdf;
+#endif
     const float pd = lerpf_(sunp, skyp, K.w_sky);
     o[0] = d.x; o[1] = d.y; o[2] = d.z; o[3] = pd;
     float e[3];
+#ifndef SS_PROBE_NO_WEIGHT
     eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, to_local(K, d), act, e, S.rows);
+#else
+    e[0] = d.x; e[1] = d.y; e[2] = d.z;
+#endif
     const float inv_pd = fdiv<FAST>(1.f, pd);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -2627,7 +2659,7 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_plain_fast, true, false, tr
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_plain_ref, false, false, true)
 // LEAN spectral: Mitsuba's 4 wavelengths per sample take the unrolled branchless body
 #define SS_SAMPLE_DIRECTION_SPEC_LEAN(NAME, FAST)                                                              \
-    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_SPEC_SAMPLE_ATTR void NAME(                                               \
         const SunskyKArgs* __restrict__ Kp, const float* ux, const float* uy, const float* px, const float* py, const float* pz,   \
         const float* lam, size_t lstride, int nlam, const uint8_t* active, size_t n, float* dx, float* dy,     \
         float* dz, float* pdf, float* dist, float* opx, float* opy, float* opz, float* weight, size_t wstride) { \

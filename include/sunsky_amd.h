@@ -235,7 +235,8 @@ int sunsky_bake_latlong(const sunsky_emitter *e, int width, int height, float th
  * (src/integrators/path.cpp:176-250; src/bsdfs/diffuse.cpp:100-180): emitter
  * sampling + cosine-hemisphere BSDF sampling combined with the power heuristic, spp
  * samples per point from PCG32Sampler-seeded streams (src/render/sampler.cpp:125-144:
- * sample_tea_32(seed, point index)).
+ * sample_tea_32(seed, point index)), each sample drawing next_2d (emitter), next_1d
+ * (sample_1, unused by this BSDF) and next_2d (BSDF) as path.cpp:216-234 does.
  * normal: unit world-space normals; reflectance: gray per point (NULL = 1).
  * out planes: 3 (RGB) or n_wavelengths <= 4 (spectral, per-point wavelengths).
  * visibility: NULL for unoccluded points, else one byte per (sample s, point i) at
@@ -258,6 +259,31 @@ int sunsky_direct_diffuse(const sunsky_emitter *e, sunsky_vec3_in normal, const 
 int sunsky_direct_diffuse_rays(const sunsky_emitter *e, sunsky_vec3_in normal, uint32_t seed, uint32_t spp,
                                size_t n, sunsky_vec3_out emitter_dir, sunsky_vec3_out bsdf_dir,
                                size_t ray_stride, void *stream);
+
+/* A caller with a glossy vertex: the light a rough conductor (src/bsdfs/roughconductor.cpp,
+ * isotropic Beckmann or GGX, visible-normal sampling, include/mitsuba/render/microfacet.h)
+ * reflects towards wi, gathered as path.cpp:176-250 does at one vertex: per sample the
+ * emitter sample (next_2d) weighted by f cos / pdf and the power heuristic, sample_1
+ * (next_1d, unused by this BSDF), then the BSDF sample (next_2d): reflected direction,
+ * weight F G1(wo), its escaped ray through eval() and pdf_direction().
+ * normal, wi: unit world vectors (wi towards the viewer, si.wi in world space).
+ * eta, k: complex IOR per RGB channel (3 values); spectral emitters use eta[0], k[0]
+ * for every wavelength.  alpha: roughness (clamped to 1e-4 as the reference).
+ * visibility: as sunsky_direct_diffuse, for the rays of sunsky_direct_conductor_rays. */
+#define SUNSKY_MICROFACET_BECKMANN 0
+#define SUNSKY_MICROFACET_GGX 1
+int sunsky_direct_conductor(const sunsky_emitter *e, sunsky_vec3_in normal, sunsky_vec3_in wi, int distribution,
+                            float alpha, const float *eta, const float *k, const float *wavelengths,
+                            int n_wavelengths, size_t wl_stride, uint32_t seed, uint32_t spp,
+                            const uint8_t *visibility, size_t vis_stride, size_t n, float *out,
+                            size_t out_stride, void *stream);
+/* The shadow rays and BSDF rays of sunsky_direct_conductor's samples (same streams and
+ * arithmetic): (0,0,0) where the emitter sample contributes nothing (pdf 0 or f cos = 0)
+ * or the BSDF sample is invalid.  ray_stride >= n; n < 2^32. */
+int sunsky_direct_conductor_rays(const sunsky_emitter *e, sunsky_vec3_in normal, sunsky_vec3_in wi,
+                                 int distribution, float alpha, uint32_t seed, uint32_t spp, size_t n,
+                                 sunsky_vec3_out emitter_dir, sunsky_vec3_out bsdf_dir, size_t ray_stride,
+                                 void *stream);
 
 /* ------------------------------------------------ forward-mode derivatives */
 typedef enum sunsky_param {         /* Differentiable traverse() parameters, sunsky.cpp:220-240 */

@@ -83,7 +83,8 @@ enum KernelId {
     K_EVAL_SPEC_RAYS_V4, K_EVAL_SPEC_RAYS_V1, K_SAMPLE_DIRECTION_RGB, K_SAMPLE_DIRECTION_SPEC, K_PDF_DIRECTION_V4, K_PDF_DIRECTION_V1, K_SAMPLE_WAVELENGTHS_RGB,
     K_SAMPLE_WAVELENGTHS_SPEC, K_SAMPLE_RAY_RGB, K_SAMPLE_RAY_SPEC, K_BAKE_RGB, K_BAKE_SPEC,
     K_DIRECT_DIFFUSE_RGB, K_DIRECT_DIFFUSE_SPEC, K_SAMPLE_DIRECTION_RGB_LEAN, K_SAMPLE_DIRECTION_SPEC_LEAN,
-    K_DIRECT_DIFFUSE_RAYS, K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN, K_COUNT
+    K_DIRECT_DIFFUSE_RAYS, K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN, K_DIRECT_CONDUCTOR_RGB, K_DIRECT_CONDUCTOR_SPEC,
+    K_DIRECT_CONDUCTOR_RAYS, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
@@ -93,7 +94,8 @@ const char* kKernelNames[K_COUNT] = {
     "sunsky_sample_wavelengths_spec", "sunsky_sample_ray_rgb", "sunsky_sample_ray_spec",
     "sunsky_bake_latlong_rgb", "sunsky_bake_latlong_spec", "sunsky_direct_diffuse_rgb", "sunsky_direct_diffuse_spec",
     "sunsky_sample_direction_rgb_lean", "sunsky_sample_direction_spec_lean", "sunsky_direct_diffuse_rays",
-    "sunsky_sample_direction_rgb_lean_plain"};
+    "sunsky_sample_direction_rgb_lean_plain", "sunsky_direct_conductor_rgb", "sunsky_direct_conductor_spec",
+    "sunsky_direct_conductor_rays"};
 
 // eval kernels instantiated twice: eval(si) negates wi at compile time,
 // eval_direction(ds) uses ds.d as is (the "_dir" kernels)
@@ -173,6 +175,7 @@ int blocks_per_cu(KernelId k) {
             return 64;
         case K_BAKE_RGB: case K_BAKE_SPEC: return 64;
         case K_DIRECT_DIFFUSE_RGB: case K_DIRECT_DIFFUSE_SPEC: case K_DIRECT_DIFFUSE_RAYS: return 64;
+        case K_DIRECT_CONDUCTOR_RGB: case K_DIRECT_CONDUCTOR_SPEC: case K_DIRECT_CONDUCTOR_RAYS: return 64;
         case K_EVAL_SPEC_RAYS_V4: case K_EVAL_SPEC_RAYS_V1: return 64;
         default: return 16;
     }
@@ -1223,6 +1226,86 @@ int sunsky_direct_diffuse_rays(const sunsky_emitter* e, sunsky_vec3_in nrm, uint
         void* args[] = {&K, (void*)&nrm.x, (void*)&nrm.y, (void*)&nrm.z, &seed, &spp, &n, &em.x, &em.y, &em.z,
                         &bs.x, &bs.y, &bs.z, &rstride};
         launch(e->fn(K_DIRECT_DIFFUSE_RAYS), grid_for(e->mod, K_DIRECT_DIFFUSE_RAYS, n), (hipStream_t)stream, args);
+    });
+}
+
+// The rough conductor of the glossy caller (mirrors the kernel-side ConductorArgs)
+struct ConductorArgs {
+    int type;
+    float alpha;
+    float eta[4], k[4];
+};
+
+static int conductor_args(const sunsky_emitter* e, int distribution, float alpha, const float* eta, const float* k,
+                          ConductorArgs* c) {
+    if (distribution != SUNSKY_MICROFACET_BECKMANN && distribution != SUNSKY_MICROFACET_GGX)
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "distribution must be SUNSKY_MICROFACET_BECKMANN or _GGX");
+    if (!(alpha > 0.f)) return fail(SUNSKY_ERROR_INVALID_VALUE, "alpha must be > 0");
+    if (!eta || !k) return fail(SUNSKY_ERROR_INVALID_VALUE, "null eta / k");
+    std::memset(c, 0, sizeof(*c));
+    c->type = distribution;
+    // microfacet.h clamps alpha to 1e-4 (MicrofacetDistribution::configure)
+    c->alpha = std::max(alpha, 1e-4f);
+    const int nc = e->kargs.variant == kSpectral ? 1 : 3;
+    for (int i = 0; i < nc; ++i) { c->eta[i] = eta[i]; c->k[i] = k[i]; }
+    return SUNSKY_OK;
+}
+
+int sunsky_direct_conductor(const sunsky_emitter* e, sunsky_vec3_in nrm, sunsky_vec3_in wi, int distribution,
+                            float alpha, const float* eta, const float* k, const float* lam, int nlam, size_t lstride,
+                            uint32_t seed, uint32_t spp, const uint8_t* vis, size_t vstride, size_t n, float* out,
+                            size_t ostride, void* stream) {
+    SUNSKY_PHASE("SamplingIntegratorSample", "direct_conductor");
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    ConductorArgs C;
+    int rc = conductor_args(e, distribution, alpha, eta, k, &C);
+    if (rc != SUNSKY_OK) return rc;
+    if (n == 0) return SUNSKY_OK;
+    const bool spec = e->kargs.variant == kSpectral;
+    if (!nrm.x || !nrm.y || !nrm.z || !wi.x || !wi.y || !wi.z || !out)
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "null normal / view direction / output pointer");
+    if (spp < 1) return fail(SUNSKY_ERROR_INVALID_VALUE, "spp must be >= 1");
+    if (n > 0xffffffffull) return fail(SUNSKY_ERROR_INVALID_VALUE, "more than 2^32 points (the sampler's lane index is 32-bit)");
+    if (spec && (!lam || nlam < 1 || nlam > 4))
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "spectral direct lighting needs 1..4 wavelength planes");
+    if (!spec && (lam || nlam)) return fail(SUNSKY_ERROR_INVALID_VALUE, "RGB direct lighting takes no wavelengths");
+    if (ostride < n || (spec && lstride < n)) return fail(SUNSKY_ERROR_INVALID_VALUE, "stride < n");
+    if (vis && vstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "vis_stride < n");
+    return guarded([&] {
+        require_device(e);
+        DeviceScope dev_scope(e->device);
+        const SunskyKArgs* K = e->d_state;
+        int nl = spec ? nlam : 0;
+        void* args[] = {&K, &C, (void*)&nrm.x, (void*)&nrm.y, (void*)&nrm.z, (void*)&wi.x, (void*)&wi.y, (void*)&wi.z,
+                        &lam, &lstride, &nl, &seed, &spp, &vis, &vstride, &n, &out, &ostride};
+        const KernelId kid = spec ? K_DIRECT_CONDUCTOR_SPEC : K_DIRECT_CONDUCTOR_RGB;
+        launch(e->fn(kid), grid_for(e->mod, kid, n), (hipStream_t)stream, args);
+    });
+}
+
+int sunsky_direct_conductor_rays(const sunsky_emitter* e, sunsky_vec3_in nrm, sunsky_vec3_in wi, int distribution,
+                                 float alpha, uint32_t seed, uint32_t spp, size_t n, sunsky_vec3_out em,
+                                 sunsky_vec3_out bs, size_t rstride, void* stream) {
+    SUNSKY_PHASE("SamplingIntegratorSample", "direct_conductor_rays");
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    const float one[3] = {1.f, 1.f, 1.f};
+    ConductorArgs C;
+    int rc = conductor_args(e, distribution, alpha, one, one, &C);   // the directions do not depend on eta / k
+    if (rc != SUNSKY_OK) return rc;
+    if (n == 0) return SUNSKY_OK;
+    if (!nrm.x || !nrm.y || !nrm.z || !wi.x || !wi.y || !wi.z)
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "null normal / view direction pointer");
+    if (!em.x || !em.y || !em.z || !bs.x || !bs.y || !bs.z) return fail(SUNSKY_ERROR_INVALID_VALUE, "null ray pointer");
+    if (spp < 1) return fail(SUNSKY_ERROR_INVALID_VALUE, "spp must be >= 1");
+    if (n > 0xffffffffull) return fail(SUNSKY_ERROR_INVALID_VALUE, "more than 2^32 points (the sampler's lane index is 32-bit)");
+    if (rstride < n) return fail(SUNSKY_ERROR_INVALID_VALUE, "ray_stride < n");
+    return guarded([&] {
+        require_device(e);
+        DeviceScope dev_scope(e->device);
+        const SunskyKArgs* K = e->d_state;
+        void* args[] = {&K, &C, (void*)&nrm.x, (void*)&nrm.y, (void*)&nrm.z, (void*)&wi.x, (void*)&wi.y, (void*)&wi.z,
+                        &seed, &spp, &n, &em.x, &em.y, &em.z, &bs.x, &bs.y, &bs.z, &rstride};
+        launch(e->fn(K_DIRECT_CONDUCTOR_RAYS), grid_for(e->mod, K_DIRECT_CONDUCTOR_RAYS, n), (hipStream_t)stream, args);
     });
 }
 

@@ -1942,6 +1942,7 @@ __device__ __forceinline__ void direct_diffuse_body(
         for (int c = 0; c < C; ++c) acc[c] = 0.f;
         for (uint32_t smp = 0; smp < spp; ++smp) {
             const float u0 = rng.next_float(), u1 = rng.next_float();
+            (void)rng.next_float();   // sample_1 (path.cpp:233), unused by the diffuse BSDF
             const float u2 = rng.next_float(), u3 = rng.next_float();
             const unsigned v = vis ? (unsigned)vis[(size_t)smp * vstride + i] : 3u;
             if constexpr (!SPEC) {
@@ -2011,6 +2012,308 @@ __device__ __forceinline__ void direct_diffuse_body(
     }
 }
 
+// ======================================================================
+// Caller with a glossy vertex: the rough conductor (src/bsdfs/roughconductor.cpp) with an
+// isotropic Beckmann or GGX microfacet distribution and visible-normal sampling
+// (include/mitsuba/render/microfacet.h), the default Mitsuba configuration.  All in the
+// point's shading frame Frame3f(n) (coordinate_system), fp32 with the libm functions.
+// ======================================================================
+struct ConductorArgs {
+    int type;            // 0 Beckmann, 1 GGX (MicrofacetType)
+    float alpha;         // alpha_u = alpha_v
+    float eta[4], k[4];  // complex IOR per RGB channel (spectral: eta[0], k[0] for every wavelength)
+};
+
+// MicrofacetDistribution::eval (microfacet.h:186-207), isotropic
+__device__ __forceinline__ float mf_eval(const ConductorArgs& c, float3_ m) {
+    const float ct2 = m.z * m.z, a2 = c.alpha * c.alpha;
+    float r;
+    if (c.type == 0) {
+        const float mx = m.x / c.alpha, my = m.y / c.alpha;
+        r = expf(-(mx * mx + my * my) / ct2) / (kPi * a2 * (ct2 * ct2));
+    } else {
+        const float mx = m.x / c.alpha, my = m.y / c.alpha, q = mx * mx + my * my + m.z * m.z;
+        r = 1.f / (kPi * a2 * (q * q));
+    }
+    return r * m.z > 1e-20f ? r : 0.f;
+}
+
+// MicrofacetDistribution::smith_g1 (microfacet.h:330-354)
+__device__ __forceinline__ float mf_smith_g1(const ConductorArgs& c, float3_ v, float3_ m) {
+    const float xy = (c.alpha * v.x) * (c.alpha * v.x) + (c.alpha * v.y) * (c.alpha * v.y);
+    const float t2 = xy / (v.z * v.z);
+    float r;
+    if (c.type == 0) {
+        const float a = 1.f / sqrtf(t2), a2 = a * a;
+        r = a >= 1.6f ? 1.f : (3.535f * a + 2.181f * a2) / (1.f + 2.276f * a + 2.577f * a2);
+    } else {
+        r = 2.f / (1.f + sqrtf(1.f + t2));
+    }
+    if (xy == 0.f) r = 1.f;
+    if (dot3(v, m) * v.z <= 0.f) r = 0.f;
+    return r;
+}
+
+// MicrofacetDistribution::sample_visible_11 (microfacet.h:357-410)
+__device__ __forceinline__ void mf_sample_visible_11(const ConductorArgs& c, float cos_theta_i, float ux, float uy,
+                                                     float* sx, float* sy) {
+    if (c.type == 0) {
+        const float tan_i = sqrtf(fmaxf(fmaf(-cos_theta_i, cos_theta_i, 1.f), 0.f)) / cos_theta_i;
+        const float cot_i = 1.f / tan_i;
+        const float maxval = erff(cot_i);
+        ux = fmaxf(fminf(ux, 1.f - 1e-6f), 1e-6f);
+        uy = fmaxf(fminf(uy, 1.f - 1e-6f), 1e-6f);
+        float x = maxval - (maxval + 1.f) * erff(sqrtf(-logf(ux)));
+        ux *= 1.f + maxval + 0.56418958354775628695f * tan_i * expf(-cot_i * cot_i);
+#pragma unroll 1
+        for (int it = 0; it < 3; ++it) {
+            const float slope = erfinvf_(x);
+            const float value = 1.f + x + 0.56418958354775628695f * tan_i * expf(-slope * slope) - ux;
+            const float deriv = 1.f - slope * tan_i;
+            x -= value / deriv;
+        }
+        *sx = erfinvf_(x);
+        *sy = erfinvf_(fmaf(2.f, uy, -1.f));
+    } else {
+        float px, py;
+        disk_concentric_dev<false>(ux, uy, &px, &py);
+        const float sl = 0.5f * (1.f + cos_theta_i);
+        py = lerpf_(sqrtf(fmaxf(1.f - px * px, 0.f)), py, sl);
+        const float pz = sqrtf(fmaxf(1.f - (px * px + py * py), 0.f));
+        const float sin_i = sqrtf(fmaxf(1.f - cos_theta_i * cos_theta_i, 0.f));
+        const float norm = 1.f / fmaf(sin_i, py, cos_theta_i * pz);
+        *sx = fmaf(cos_theta_i, py, -(sin_i * pz)) * norm;
+        *sy = px * norm;
+    }
+}
+
+// MicrofacetDistribution::sample, visible normals (microfacet.h:293-320): m and its pdf
+__device__ __forceinline__ float3_ mf_sample(const ConductorArgs& c, float3_ wi, float ux, float uy, float* pdf) {
+    float3_ wp = mk3(c.alpha * wi.x, c.alpha * wi.y, wi.z);
+    const float inv = 1.f / sqrtf(dot3(wp, wp));
+    wp = mk3(wp.x * inv, wp.y * inv, wp.z * inv);
+    // Frame3f::sincos_phi (frame.h): sin / cos of the azimuth, (0, 1) at the pole
+    const float st2 = fmaxf(1.f - wp.z * wp.z, 0.f);
+    const float inv_st = 1.f / sqrtf(st2);
+    float sp = wp.y * inv_st, cp = wp.x * inv_st;
+    if (!(st2 > 0.f) || !isfinite(inv_st)) { sp = 0.f; cp = 1.f; }
+    sp = fminf(fmaxf(sp, -1.f), 1.f);
+    cp = fminf(fmaxf(cp, -1.f), 1.f);
+    float slx, sly;
+    mf_sample_visible_11(c, wp.z, ux, uy, &slx, &sly);
+    const float tx = fmaf(cp, slx, -(sp * sly)) * c.alpha, ty = fmaf(sp, slx, cp * sly) * c.alpha;
+    float3_ m = mk3(-tx, -ty, 1.f);
+    const float mi = 1.f / sqrtf(dot3(m, m));
+    m = mk3(m.x * mi, m.y * mi, m.z * mi);
+    *pdf = mf_eval(c, m) * mf_smith_g1(c, wi, m) * fabsf(dot3(wi, m)) / wi.z;
+    return m;
+}
+
+// fresnel_conductor (fresnel.h:93-117)
+__device__ __forceinline__ float fresnel_conductor_dev(float cos_i, float eta, float k) {
+    const float c2 = cos_i * cos_i, s2 = 1.f - c2, s4 = s2 * s2;
+    const float t1 = eta * eta - k * k - s2;
+    const float ab = sqrtf(fmaxf(t1 * t1 + 4.f * k * k * eta * eta, 0.f));
+    const float a = sqrtf(fmaxf(0.5f * (ab + t1), 0.f));
+    const float term1 = ab + c2, term2 = 2.f * cos_i * a;
+    const float rs = (term1 - term2) / (term1 + term2);
+    const float term3 = ab * c2 + s4, term4 = term2 * s2;
+    const float rp = rs * (term3 - term4) / (term3 + term4);
+    return 0.5f * (rs + rp);
+}
+
+// RoughConductor::eval and ::pdf (roughconductor.cpp:308-420) for wi, wo in the shading
+// frame: f cos(theta_o) per channel without the Fresnel factor (returned as D G / (4 cos_i),
+// the caller multiplies F(dot(wi, H)) per channel) and the pdf.
+__device__ __forceinline__ float conductor_eval_pdf(const ConductorArgs& c, float3_ wi, float3_ wo, float* pdf,
+                                                    float* cos_ih) {
+    *pdf = 0.f;
+    *cos_ih = 0.f;
+    if (!(wi.z > 0.f && wo.z > 0.f)) return 0.f;
+    float3_ h = mk3(wo.x + wi.x, wo.y + wi.y, wo.z + wi.z);
+    const float hi = 1.f / sqrtf(dot3(h, h));
+    h = mk3(h.x * hi, h.y * hi, h.z * hi);
+    const float D = mf_eval(c, h);
+    const float g1i = mf_smith_g1(c, wi, h);
+    *cos_ih = dot3(wi, h);
+    if (dot3(wi, h) > 0.f && dot3(wo, h) > 0.f) *pdf = D * g1i / (4.f * wi.z);
+    if (D == 0.f) return 0.f;
+    return D * (g1i * mf_smith_g1(c, wo, h)) / (4.f * wi.z);
+}
+
+// The sky-and-sun lighting a rough-conductor point reflects towards wi (one path vertex,
+// src/integrators/path.cpp:176-250 with src/bsdfs/roughconductor.cpp): per sample the
+// emitter sample (next_2d) weighted by f cos / pdf x MIS, then sample_1 (next_1d, unused by
+// the conductor) and the BSDF sample (next_2d: visible normal, reflection, weight
+// G1(wo) F) whose escaped ray meets eval() x MIS; power heuristic; PCG32Sampler streams.
+// wi: world unit directions towards the viewer (si.wi); visibility as direct_diffuse.
+template <bool FAST, bool SPEC>
+__device__ __forceinline__ void direct_conductor_body(
+    const SunskyKArgs& K, const ConductorArgs C, const float* __restrict__ nx, const float* __restrict__ ny,
+    const float* __restrict__ nz, const float* __restrict__ vx, const float* __restrict__ vy,
+    const float* __restrict__ vz, const float* __restrict__ lam, size_t lstride, int nlam, uint32_t seed,
+    uint32_t spp, const uint8_t* __restrict__ vis, size_t vstride, size_t n, float* __restrict__ out,
+    size_t ostride) {
+    __shared__ SamplerLds<FAST, SPEC> S;
+    stage_sampler_lds<FAST, SPEC>(K, &S);
+    const float w_sun = 1.f - K.w_sky, inv_w = uniform_f(1.f / K.w_sky), inv_w_sun = uniform_f(1.f / w_sun);
+    constexpr int CH = SPEC ? 4 : 3;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float3_ nrm = mk3(nx[i], ny[i], nz[i]);
+        float3_ fs, ft;
+        coordinate_system(nrm, &fs, &ft);
+        const float3_ vw = mk3(vx[i], vy[i], vz[i]);
+        const float3_ wi = mk3(dot3(vw, fs), dot3(vw, ft), dot3(vw, nrm));   // si.to_local(si.wi)
+        uint32_t v0 = seed, v1 = (uint32_t)i;
+        sample_tea_32(&v0, &v1);
+        Pcg32 rng;
+        rng.seed(v0, v1);
+        float wl[CH], eta[CH], kk[CH];
+#pragma unroll
+        for (int c = 0; c < CH; ++c) {
+            wl[c] = (SPEC && c < nlam) ? lam[(size_t)c * lstride + i] : 0.f;
+            eta[c] = SPEC ? C.eta[0] : C.eta[c];
+            kk[c] = SPEC ? C.k[0] : C.k[c];
+        }
+        float acc[CH];
+#pragma unroll
+        for (int c = 0; c < CH; ++c) acc[c] = 0.f;
+        for (uint32_t smp = 0; smp < spp; ++smp) {
+            const float u0 = rng.next_float(), u1 = rng.next_float();
+            (void)rng.next_float();   // sample_1 (path.cpp:233), unused by the conductor
+            const float u2 = rng.next_float(), u3 = rng.next_float();
+            const unsigned v = vis ? (unsigned)vis[(size_t)smp * vstride + i] : 3u;
+            // ---- emitter sampling
+            {
+                const bool pick_sky = u0 < K.w_sky;
+                const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, u0, u1, inv_w, inv_w_sun);
+                const bool act = sd.z >= 0.f;
+                const float3_ d = to_world(K, sd);
+                float skyp, sunp;
+                compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+                const float pd = lerpf_(sunp, skyp, K.w_sky);
+                const float3_ wo = mk3(dot3(d, fs), dot3(d, ft), dot3(d, nrm));
+                float bpdf, cih;
+                const float dg = conductor_eval_pdf(C, wi, wo, &bpdf, &cih);
+                if ((v & 1u) && pd != 0.f && dg != 0.f) {
+                    const float mis = mis_power<FAST>(pd, bpdf);
+                    const float3_ lw = to_local(K, d);
+                    float e[CH];
+                    if constexpr (!SPEC) {
+                        eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, lw, act, e, S.rows);
+                    } else {
+                        DirTerms t = dir_terms<FAST>(K, lw, act);
+                        add_sun_terms<FAST>(K, t);
+#pragma unroll
+                        for (int c = 0; c < CH; ++c) e[c] = c < nlam ? eval_spec_one<FAST>(K, S.chans.c, S.sun, S.ld, t, wl[c]) : 0.f;
+                    }
+#pragma unroll
+                    for (int c = 0; c < CH; ++c) {
+                        float w = e[c] / pd;
+                        w = isfinite(w) ? w : 0.f;
+                        acc[c] = fmaf(dg * fresnel_conductor_dev(cih, eta[c], kk[c]) * w, mis, acc[c]);
+                    }
+                }
+            }
+            // ---- BSDF sampling
+            if (wi.z > 0.f) {
+                float mpdf;
+                const float3_ m = mf_sample(C, wi, u2, u3, &mpdf);
+                const float dwm = dot3(wi, m);
+                const float3_ wo = mk3(fmaf(2.f * dwm, m.x, -wi.x), fmaf(2.f * dwm, m.y, -wi.y), fmaf(2.f * dwm, m.z, -wi.z));
+                const float bpdf = mpdf / (4.f * dot3(wo, m));
+                if ((v & 2u) && bpdf != 0.f && wo.z > 0.f) {
+                    const float g1 = mf_smith_g1(C, wo, m);
+                    const float3_ dw = frame_to_world(fs, ft, nrm, wo);
+                    const float3_ lw = to_local(K, dw);
+                    float bskyp, bsunp;
+                    compute_pdfs<FAST>(K, S.tgmm, lw, true, true, &bskyp, &bsunp);
+                    const float mis = mis_power<FAST>(bpdf, lerpf_(bsunp, bskyp, K.w_sky));
+                    const bool up = lw.z >= 0.f;
+                    float e[CH];
+                    if constexpr (!SPEC) {
+                        eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, lw, up, e, S.rows);
+                    } else {
+                        DirTerms t = dir_terms<FAST>(K, lw, up);
+                        add_sun_terms<FAST>(K, t);
+#pragma unroll
+                        for (int c = 0; c < CH; ++c) e[c] = c < nlam ? eval_spec_one<FAST>(K, S.chans.c, S.sun, S.ld, t, wl[c]) : 0.f;
+                    }
+#pragma unroll
+                    for (int c = 0; c < CH; ++c)   // throughput (F G1) x eval x MIS (path.cpp:184-190)
+                        acc[c] = fmaf(fresnel_conductor_dev(dwm, eta[c], kk[c]) * g1, e[c] * mis, acc[c]);
+                }
+            }
+        }
+        const float r = 1.f / (float)spp;
+        const int nc = SPEC ? nlam : 3;
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+            if (c < nc) __builtin_nontemporal_store(acc[c] * r, out + (size_t)c * ostride + i);
+    }
+}
+
+// The rays of direct_conductor_body's samples, from the same streams and arithmetic (the
+// directions bit for bit): em[s * rstride + i] the emitter sample's world direction, (0, 0,
+// 0) where it contributes nothing (pdf 0, or f cos 0: below either hemisphere or outside
+// the lobe), bs[...] the BSDF sample's reflected world direction, (0, 0, 0) where invalid.
+template <bool FAST>
+__device__ __forceinline__ void direct_conductor_rays_body(
+    const SunskyKArgs& K, const ConductorArgs C, const float* __restrict__ nx, const float* __restrict__ ny,
+    const float* __restrict__ nz, const float* __restrict__ vx, const float* __restrict__ vy,
+    const float* __restrict__ vz, uint32_t seed, uint32_t spp, size_t n, float* __restrict__ ex,
+    float* __restrict__ ey, float* __restrict__ ez, float* __restrict__ bx, float* __restrict__ by,
+    float* __restrict__ bz, size_t rstride) {
+    __shared__ TgmmLds<FAST> T;
+    stage_tgmm<FAST>(K, &T);
+    __syncthreads();
+    const float w_sun = 1.f - K.w_sky, inv_w = uniform_f(1.f / K.w_sky), inv_w_sun = uniform_f(1.f / w_sun);
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float3_ nrm = mk3(nx[i], ny[i], nz[i]);
+        float3_ fs, ft;
+        coordinate_system(nrm, &fs, &ft);
+        const float3_ vw = mk3(vx[i], vy[i], vz[i]);
+        const float3_ wi = mk3(dot3(vw, fs), dot3(vw, ft), dot3(vw, nrm));
+        uint32_t v0 = seed, v1 = (uint32_t)i;
+        sample_tea_32(&v0, &v1);
+        Pcg32 rng;
+        rng.seed(v0, v1);
+        for (uint32_t smp = 0; smp < spp; ++smp) {
+            const float u0 = rng.next_float(), u1 = rng.next_float();
+            (void)rng.next_float();
+            const float u2 = rng.next_float(), u3 = rng.next_float();
+            const bool pick_sky = u0 < K.w_sky;
+            const float3_ sd = sample_sky_or_sun<FAST>(K, T, pick_sky, u0, u1, inv_w, inv_w_sun);
+            const bool act = sd.z >= 0.f;
+            const float3_ d = to_world(K, sd);
+            float skyp, sunp;
+            compute_pdfs<FAST>(K, T, sd, pick_sky, act, &skyp, &sunp);
+            const float pd = lerpf_(sunp, skyp, K.w_sky);
+            const float3_ wo = mk3(dot3(d, fs), dot3(d, ft), dot3(d, nrm));
+            float bpdf, cih;
+            const bool em_ok = pd != 0.f && conductor_eval_pdf(C, wi, wo, &bpdf, &cih) != 0.f;
+            const size_t o = (size_t)smp * rstride + i;
+            ex[o] = em_ok ? d.x : 0.f;
+            ey[o] = em_ok ? d.y : 0.f;
+            ez[o] = em_ok ? d.z : 0.f;
+            float3_ dw = mk3(0.f, 0.f, 0.f);
+            if (wi.z > 0.f) {
+                float mpdf;
+                const float3_ m = mf_sample(C, wi, u2, u3, &mpdf);
+                const float dwm = dot3(wi, m);
+                const float3_ r = mk3(fmaf(2.f * dwm, m.x, -wi.x), fmaf(2.f * dwm, m.y, -wi.y), fmaf(2.f * dwm, m.z, -wi.z));
+                const float p = mpdf / (4.f * dot3(r, m));
+                if (p != 0.f && r.z > 0.f) dw = frame_to_world(fs, ft, nrm, r);
+            }
+            bx[o] = dw.x;
+            by[o] = dw.y;
+            bz[o] = dw.z;
+        }
+    }
+}
+
 // The rays a caller's tracer tests between the two halves of direct_diffuse_body,
 // from the same PCG32 streams and the same arithmetic: for sample s of point i,
 // em[s * rstride + i] is the world direction of the emitter sample (the shadow ray
@@ -2039,6 +2342,7 @@ __device__ __forceinline__ void direct_diffuse_rays_body(
         rng.seed(v0, v1);
         for (uint32_t smp = 0; smp < spp; ++smp) {
             const float u0 = rng.next_float(), u1 = rng.next_float();
+            (void)rng.next_float();   // sample_1 (path.cpp:233), unused by the diffuse BSDF
             const float u2 = rng.next_float(), u3 = rng.next_float();
             const bool pick_sky = u0 < K.w_sky;
             const float3_ sd = sample_sky_or_sun<FAST>(K, T, pick_sky, u0, u1, inv_w, inv_w_sun);
@@ -2743,6 +3047,30 @@ SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_rgb_fast, true, false)
 SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_rgb_ref, false, false)
 SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_spec_fast, true, true)
 SS_DIRECT_DIFFUSE(sunsky_direct_diffuse_spec_ref, false, true)
+
+#define SS_DIRECT_CONDUCTOR(NAME, FAST, SPEC)                                                                 \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                              \
+        const SunskyKArgs* __restrict__ Kp, ConductorArgs C, const float* nx, const float* ny, const float* nz,  \
+        const float* vx, const float* vy, const float* vz, const float* lam, size_t lstride, int nlam, uint32_t seed, \
+        uint32_t spp, const uint8_t* vis, size_t vstride, size_t n, float* out, size_t ostride) {              \
+        direct_conductor_body<FAST, SPEC>(*Kp, C, nx, ny, nz, vx, vy, vz, lam, lstride, nlam, seed, spp, vis,    \
+                                          vstride, n, out, ostride);                                           \
+    }
+SS_DIRECT_CONDUCTOR(sunsky_direct_conductor_rgb_fast, true, false)
+SS_DIRECT_CONDUCTOR(sunsky_direct_conductor_rgb_ref, false, false)
+SS_DIRECT_CONDUCTOR(sunsky_direct_conductor_spec_fast, true, true)
+SS_DIRECT_CONDUCTOR(sunsky_direct_conductor_spec_ref, false, true)
+
+#define SS_DIRECT_CONDUCTOR_RAYS(NAME, FAST)                                                                  \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                              \
+        const SunskyKArgs* __restrict__ Kp, ConductorArgs C, const float* nx, const float* ny, const float* nz,  \
+        const float* vx, const float* vy, const float* vz, uint32_t seed, uint32_t spp, size_t n, float* ex,     \
+        float* ey, float* ez, float* bx, float* by, float* bz, size_t rstride) {                               \
+        direct_conductor_rays_body<FAST>(*Kp, C, nx, ny, nz, vx, vy, vz, seed, spp, n, ex, ey, ez, bx, by, bz,   \
+                                         rstride);                                                             \
+    }
+SS_DIRECT_CONDUCTOR_RAYS(sunsky_direct_conductor_rays_fast, true)
+SS_DIRECT_CONDUCTOR_RAYS(sunsky_direct_conductor_rays_ref, false)
 
 #define SS_DIRECT_DIFFUSE_RAYS(NAME, FAST)                                                                    \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                              \

@@ -497,6 +497,63 @@ class SunskyEmitter:
             Vec3Out(bs[0].data_ptr(), bs[1].data_ptr(), bs[2].data_ptr()), n, self._stream()))
         return em, bs
 
+    def direct_conductor(self, normals, wi, alpha=0.1, distribution="beckmann", eta=0.0, k=1.0, seed=0, spp=1,
+                         wavelengths=None, out=None, visibility=None):
+        """Sun-and-sky light a rough conductor reflects towards wi (sunsky_direct_conductor): one
+        path vertex (path.cpp:176-250) with roughconductor.cpp (isotropic Beckmann / GGX,
+        visible normals; the reference's defaults: Beckmann, alpha 0.1, eta 0, k 1).  normals, wi
+        (3, n) world unit vectors; eta / k: 1 or 3 per-channel values (spectral: the first, for
+        every wavelength) -> (C, n)."""
+        normals, nin = self._vec_in(normals)
+        wi, win = self._vec_in(wi)
+        n = normals.shape[1]
+        if wi.shape[1] != n:
+            raise ValueError("normals and wi must have the same number of points")
+        dist = {"beckmann": 0, "ggx": 1}.get(str(distribution).lower())
+        if dist is None:
+            raise ValueError(f"invalid distribution '{distribution}', must be 'beckmann' or 'ggx'")
+        vis = None
+        if visibility is not None:
+            vis = torch.as_tensor(visibility, device=self.device)
+            if vis.dim() != 2 or tuple(vis.shape) != (int(spp), n):
+                raise ValueError(f"visibility must be a ({int(spp)}, {n}) tensor, got shape {tuple(vis.shape)}")
+            vis = vis.to(torch.uint8).contiguous()
+        if self.is_spectral:
+            if wavelengths is None:
+                raise ValueError("spectral direct lighting needs per-point wavelengths")
+            wl = self._wavelengths(wavelengths, n)
+            if wl.shape[0] > 4:
+                raise ValueError("direct_conductor takes up to 4 wavelengths per point")
+            kk, lam_p, lstride = wl.shape[0], _ptr(wl), wl.stride(0)
+        else:
+            wl, kk, lam_p, lstride = None, 3, None, 0
+        e3 = [float(x) for x in np.broadcast_to(np.asarray(eta, np.float32), (3,))]
+        k3 = [float(x) for x in np.broadcast_to(np.asarray(k, np.float32), (3,))]
+        out = self._out(out, (kk, n))
+        check(lib().sunsky_direct_conductor(self._h, nin, win, dist, float(alpha), _fa(e3), _fa(k3), lam_p,
+                                            kk if self.is_spectral else 0, lstride, int(seed) & 0xFFFFFFFF, int(spp),
+                                            _ptr(vis), n, n, _ptr(out), out.stride(0), self._stream()))
+        return out
+
+    def direct_conductor_rays(self, normals, wi, alpha=0.1, distribution="beckmann", seed=0, spp=1):
+        """The shadow and BSDF rays of direct_conductor's samples -> (emitter_dir, bsdf_dir), each
+        (3, spp, n) world directions, (0, 0, 0) where no ray is needed."""
+        normals, nin = self._vec_in(normals)
+        wi, win = self._vec_in(wi)
+        n = normals.shape[1]
+        dist = {"beckmann": 0, "ggx": 1}.get(str(distribution).lower())
+        if dist is None:
+            raise ValueError(f"invalid distribution '{distribution}', must be 'beckmann' or 'ggx'")
+        if int(spp) < 1:
+            raise ValueError("spp must be >= 1")
+        em = torch.empty((3, int(spp), n), dtype=torch.float32, device=self.device)
+        bs = torch.empty((3, int(spp), n), dtype=torch.float32, device=self.device)
+        check(lib().sunsky_direct_conductor_rays(
+            self._h, nin, win, dist, float(alpha), int(seed) & 0xFFFFFFFF, int(spp), n,
+            Vec3Out(em[0].data_ptr(), em[1].data_ptr(), em[2].data_ptr()),
+            Vec3Out(bs[0].data_ptr(), bs[1].data_ptr(), bs[2].data_ptr()), n, self._stream()))
+        return em, bs
+
     def eval_spectral_broadcast(self, wi, wavelengths, active=None, out=None):
         """Spectral eval of one wavelength list for every direction -> (m, n)."""
         wi, vin = self._vec_in(wi)

@@ -406,13 +406,16 @@ def _mis_power(a, b):
 def _direct_diffuse_samples(em, normals, seed, spp, lam):
     """Per sample of direct_diffuse: the emitter sample (sample_direction result, the
     cosine at the point, whether it contributes) and the cosine-sampled BSDF direction
-    with its pdf, from the PCG32Sampler streams (u_em = next_2d, u_bsdf = next_2d)."""
+    with its pdf, from the PCG32Sampler streams (u_em = next_2d, sample_1 = next_1d -- unused
+    by the diffuse BSDF --, u_bsdf = next_2d; path.cpp:216-234)."""
     normals = np.asarray(normals, dtype=np.float32)
     n = normals.shape[0]
     rng = Pcg32(seed, n)
     s, t = _coordinate_system(normals)
     for _ in range(spp):
-        u0, u1, u2, u3 = rng.next_float(), rng.next_float(), rng.next_float(), rng.next_float()
+        u0, u1 = rng.next_float(), rng.next_float()
+        rng.next_float()
+        u2, u3 = rng.next_float(), rng.next_float()
         # emitter sampling (path.cpp:208-250)
         r = em.sample_direction(np.stack([u0, u1], axis=1), wavelengths=lam)
         cos_em = (normals.astype(np.float64) * r["d"]).sum(axis=1)
@@ -459,4 +462,177 @@ def direct_diffuse_rays(em, normals, seed, spp):
                                                          np.full((1, len(normals)), 500.0, np.float32)):
         em_d.append(np.where(ok[:, None], r["d"], 0.0).astype(np.float32))
         bs_d.append(np.where((bp > 0)[:, None], dw, 0.0).astype(np.float32))
+    return np.stack(em_d), np.stack(bs_d)
+
+
+# ---------------------------------------------------------------- caller: a rough-conductor vertex
+def _mf_eval(distr, a, m):
+    """MicrofacetDistribution::eval, isotropic (include/mitsuba/render/microfacet.h:186-207)."""
+    ct2 = m[:, 2] ** 2
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        if distr == "beckmann":
+            r = np.exp(-((m[:, 0] / a) ** 2 + (m[:, 1] / a) ** 2) / ct2) / (np.pi * a * a * ct2 * ct2)
+        else:
+            r = 1.0 / (np.pi * a * a * ((m[:, 0] / a) ** 2 + (m[:, 1] / a) ** 2 + m[:, 2] ** 2) ** 2)
+    r = np.nan_to_num(r, nan=0.0, posinf=0.0)
+    return np.where(r * m[:, 2] > 1e-20, r, 0.0)
+
+
+def _mf_smith_g1(distr, a, v, m):
+    """MicrofacetDistribution::smith_g1 (microfacet.h:330-354)."""
+    xy = (a * v[:, 0]) ** 2 + (a * v[:, 1]) ** 2
+    with np.errstate(divide="ignore", invalid="ignore"):
+        t2 = xy / v[:, 2] ** 2
+        if distr == "beckmann":
+            q = 1.0 / np.sqrt(t2)
+            r = np.where(q >= 1.6, 1.0, (3.535 * q + 2.181 * q * q) / (1.0 + 2.276 * q + 2.577 * q * q))
+        else:
+            r = 2.0 / (1.0 + np.sqrt(1.0 + t2))
+    r = np.where(xy == 0.0, 1.0, r)
+    return np.where((v * m).sum(axis=1) * v[:, 2] <= 0.0, 0.0, r)
+
+
+def _mf_sample(distr, a, wi, u):
+    """MicrofacetDistribution::sample with visible normals (microfacet.h:293-320, 357-410) -> (m, pdf)."""
+    from scipy.special import erf, erfinv
+    wp = np.stack([a * wi[:, 0], a * wi[:, 1], wi[:, 2]], axis=1)
+    wp /= np.linalg.norm(wp, axis=1, keepdims=True)
+    st2 = np.maximum(1.0 - wp[:, 2] ** 2, 0.0)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = 1.0 / np.sqrt(st2)
+        sp, cp = np.clip(wp[:, 1] * inv, -1, 1), np.clip(wp[:, 0] * inv, -1, 1)
+    pole = ~(st2 > 0) | ~np.isfinite(inv)
+    sp, cp = np.where(pole, 0.0, sp), np.where(pole, 1.0, cp)
+    ct = wp[:, 2]
+    ux, uy = u[:, 0].astype(np.float64), u[:, 1].astype(np.float64)
+    if distr == "beckmann":
+        tan_i = np.sqrt(np.maximum(1.0 - ct * ct, 0.0)) / ct
+        cot_i = 1.0 / tan_i
+        maxval = erf(cot_i)
+        ux = np.clip(ux, 1e-6, 1 - 1e-6)
+        uy = np.clip(uy, 1e-6, 1 - 1e-6)
+        x = maxval - (maxval + 1.0) * erf(np.sqrt(-np.log(ux)))
+        ux = ux * (1.0 + maxval + tan_i * np.exp(-cot_i ** 2) / np.sqrt(np.pi))
+        for _ in range(3):
+            slope = erfinv(x)
+            value = 1.0 + x + tan_i * np.exp(-slope ** 2) / np.sqrt(np.pi) - ux
+            x = x - value / (1.0 - slope * tan_i)
+        sx, sy = erfinv(x), erfinv(2.0 * uy - 1.0)
+    else:
+        px, py = _disk_concentric(u[:, 0], u[:, 1])
+        px, py = px.astype(np.float64), py.astype(np.float64)
+        s = 0.5 * (1.0 + ct)
+        py = np.sqrt(np.maximum(1.0 - px * px, 0.0)) * (1 - s) + py * s
+        pz = np.sqrt(np.maximum(1.0 - (px * px + py * py), 0.0))
+        si = np.sqrt(np.maximum(1.0 - ct * ct, 0.0))
+        norm = 1.0 / (si * py + ct * pz)
+        sx, sy = (ct * py - si * pz) * norm, px * norm
+    tx, ty = (cp * sx - sp * sy) * a, (sp * sx + cp * sy) * a
+    m = np.stack([-tx, -ty, np.ones_like(tx)], axis=1)
+    m /= np.linalg.norm(m, axis=1, keepdims=True)
+    pdf = _mf_eval(distr, a, m) * _mf_smith_g1(distr, a, wi, m) * np.abs((wi * m).sum(axis=1)) / wi[:, 2]
+    return m, pdf
+
+
+def _fresnel_conductor(c, eta, k):
+    """fresnel_conductor (include/mitsuba/render/fresnel.h:93-117)."""
+    c2 = c * c
+    s2 = 1.0 - c2
+    t1 = eta * eta - k * k - s2
+    ab = np.sqrt(np.maximum(t1 * t1 + 4.0 * k * k * eta * eta, 0.0))
+    a = np.sqrt(np.maximum(0.5 * (ab + t1), 0.0))
+    term1, term2 = ab + c2, 2.0 * c * a
+    rs = (term1 - term2) / (term1 + term2)
+    term3, term4 = ab * c2 + s2 * s2, term2 * s2
+    rp = rs * (term3 - term4) / (term3 + term4)
+    return 0.5 * (rs + rp)
+
+
+def _conductor_eval_pdf(distr, a, wi, wo):
+    """RoughConductor::eval (without F) and ::pdf (src/bsdfs/roughconductor.cpp:308-420) -> (D G / 4 cos_i, pdf, cos_ih)."""
+    h = wo + wi
+    with np.errstate(divide="ignore", invalid="ignore"):
+        h = h / np.linalg.norm(h, axis=1, keepdims=True)
+    ok = (wi[:, 2] > 0) & (wo[:, 2] > 0)
+    D = _mf_eval(distr, a, h)
+    g1i = _mf_smith_g1(distr, a, wi, h)
+    cih = (wi * h).sum(axis=1)
+    pdf = np.where(ok & (cih > 0) & ((wo * h).sum(axis=1) > 0), D * g1i / (4.0 * wi[:, 2]), 0.0)
+    val = np.where(ok & (D != 0), D * g1i * _mf_smith_g1(distr, a, wo, h) / (4.0 * wi[:, 2]), 0.0)
+    return np.nan_to_num(val), np.nan_to_num(pdf), cih
+
+
+def _conductor_samples(em, normals, wi_world, distr, alpha, seed, spp, lam):
+    """Per sample of direct_conductor, from the PCG32Sampler streams: u_em = next_2d, sample_1 =
+    next_1d (unused by the conductor), u_bsdf = next_2d (path.cpp:216-234)."""
+    normals = np.asarray(normals, dtype=np.float32)
+    n = normals.shape[0]
+    rng = Pcg32(seed, n)
+    s, t = _coordinate_system(normals)
+    wv = np.asarray(wi_world, dtype=np.float32)
+    wi = np.stack([(wv * s).sum(1), (wv * t).sum(1), (wv * normals).sum(1)], axis=1).astype(np.float64)
+    a = max(float(alpha), 1e-4)
+    for _ in range(spp):
+        u0, u1 = rng.next_float(), rng.next_float()
+        rng.next_float()
+        u2, u3 = rng.next_float(), rng.next_float()
+        r = em.sample_direction(np.stack([u0, u1], axis=1), wavelengths=lam)
+        d = r["d"].astype(np.float64)
+        wo = np.stack([(d * s).sum(1), (d * t).sum(1), (d * normals).sum(1)], axis=1)
+        dg, bpdf, cih = _conductor_eval_pdf(distr, a, wi, wo)
+        em_ok = (r["pdf"] != 0) & (dg != 0)
+        m, mpdf = _mf_sample(distr, a, np.where(wi[:, 2:] > 0, wi, np.array([0.0, 0.0, 1.0])), np.stack([u2, u3], 1))
+        dwm = (wi * m).sum(1)
+        ro = 2.0 * dwm[:, None] * m - wi
+        with np.errstate(divide="ignore", invalid="ignore"):
+            pb = mpdf / (4.0 * (ro * m).sum(1))
+        b_ok = (wi[:, 2] > 0) & (pb != 0) & np.isfinite(pb) & (ro[:, 2] > 0)
+        g1 = _mf_smith_g1(distr, a, ro, m)
+        dw = (s * ro[:, :1] + t * ro[:, 1:2] + normals * ro[:, 2:3]).astype(np.float32)
+        yield r, dg, bpdf, cih, em_ok, dw, pb, b_ok, g1, dwm
+
+
+def direct_conductor(em, normals, wi_world, alpha=0.1, distribution="beckmann", eta=0.0, k=1.0, seed=0, spp=1,
+                     wavelengths=None, vis=None):
+    """Sun-and-sky light a rough conductor reflects towards wi (one vertex of
+    src/integrators/path.cpp:176-250 with src/bsdfs/roughconductor.cpp): emitter sampling
+    (f cos x weight x MIS) + visible-normal BSDF sampling (F G1(wo) x eval x MIS), power
+    heuristic, spp samples.  em: an Oracle; eta / k: 1 or 3 values (spectral: the first).
+    vis: None or (spp, n) uint8 tracer verdicts.  Returns (C, n) fp64."""
+    normals = np.asarray(normals, dtype=np.float32)
+    n = normals.shape[0]
+    c = wavelengths.shape[0] if em.spectral else 3
+    lam = None if not em.spectral else np.asarray(wavelengths, dtype=np.float32)
+    e3 = np.broadcast_to(np.asarray(eta, np.float64), (3,))
+    k3 = np.broadcast_to(np.asarray(k, np.float64), (3,))
+    etas = np.full(c, e3[0]) if em.spectral else e3
+    ks = np.full(c, k3[0]) if em.spectral else k3
+    acc = np.zeros((c, n), dtype=np.float64)
+    for j, (r, dg, bpdf, cih, em_ok, dw, pb, b_ok, g1, dwm) in enumerate(
+            _conductor_samples(em, normals, wi_world, distribution.lower(), alpha, seed, spp, lam)):
+        v = np.full(n, 3, np.uint8) if vis is None else np.asarray(vis[j], dtype=np.uint8)
+        ok = em_ok & ((v & 1) != 0)
+        mis = np.where(ok, _mis_power(r["pdf"], bpdf), 0.0)
+        for ch in range(c):
+            F = _fresnel_conductor(cih, etas[ch], ks[ch])
+            acc[ch] += np.where(ok, F * dg * r["weight"][:, ch] * mis, 0.0)
+        esc = b_ok & ((v & 2) != 0)
+        dws = np.where(esc[:, None], dw, np.array([0, 0, 1], np.float32))
+        mis_b = np.where(esc, _mis_power(pb, em.pdf_direction(dws)), 0.0)
+        e = em.eval(-dws, lam) if em.spectral else em.eval(-dws).T
+        for ch in range(c):
+            F = _fresnel_conductor(dwm, etas[ch], ks[ch])
+            acc[ch] += np.where(esc, F * g1 * e[ch] * mis_b, 0.0)
+    return acc / spp
+
+
+def direct_conductor_rays(em, normals, wi_world, alpha=0.1, distribution="beckmann", seed=0, spp=1):
+    """The rays a tracer tests for direct_conductor: emitter-sample and BSDF directions, each
+    (spp, n, 3) fp32, zero where no ray is needed."""
+    em_d, bs_d = [], []
+    lam = None if not em.spectral else np.full((1, len(normals)), 500.0, np.float32)
+    for r, dg, bpdf, cih, em_ok, dw, pb, b_ok, g1, dwm in _conductor_samples(
+            em, normals, wi_world, distribution.lower(), alpha, seed, spp, lam):
+        em_d.append(np.where(em_ok[:, None], r["d"], 0.0).astype(np.float32))
+        bs_d.append(np.where(b_ok[:, None], dw, 0.0).astype(np.float32))
     return np.stack(em_d), np.stack(bs_d)

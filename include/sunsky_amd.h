@@ -279,11 +279,15 @@ int sunsky_direct_conductor(const sunsky_emitter *e, sunsky_vec3_in normal, suns
                             size_t out_stride, void *stream);
 /* The shadow rays and BSDF rays of sunsky_direct_conductor's samples (same streams and
  * arithmetic): (0,0,0) where the emitter sample contributes nothing (pdf 0 or f cos = 0)
- * or the BSDF sample is invalid.  ray_stride >= n; n < 2^32. */
+ * or the BSDF sample is invalid.  bsdf_weight (NULL to skip; then eta / k may be NULL):
+ * the BSDF sample's weight F(wi.m) G1(wo, m) (roughconductor.cpp sample(), the path
+ * throughput factor of a multi-bounce caller) at bsdf_weight[(c * spp + s) * ray_stride + i]
+ * for c < 3 (RGB) or c < 1 (spectral: eta[0], k[0]), 0 where the sample is invalid.
+ * ray_stride >= n; n < 2^32. */
 int sunsky_direct_conductor_rays(const sunsky_emitter *e, sunsky_vec3_in normal, sunsky_vec3_in wi,
-                                 int distribution, float alpha, uint32_t seed, uint32_t spp, size_t n,
-                                 sunsky_vec3_out emitter_dir, sunsky_vec3_out bsdf_dir, size_t ray_stride,
-                                 void *stream);
+                                 int distribution, float alpha, const float *eta, const float *k, uint32_t seed,
+                                 uint32_t spp, size_t n, sunsky_vec3_out emitter_dir, sunsky_vec3_out bsdf_dir,
+                                 float *bsdf_weight, size_t ray_stride, void *stream);
 
 /* ------------------------------------------------ forward-mode derivatives */
 typedef enum sunsky_param {         /* Differentiable traverse() parameters, sunsky.cpp:220-240 */

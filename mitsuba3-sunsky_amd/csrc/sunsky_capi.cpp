@@ -1284,14 +1284,17 @@ int sunsky_direct_conductor(const sunsky_emitter* e, sunsky_vec3_in nrm, sunsky_
 }
 
 int sunsky_direct_conductor_rays(const sunsky_emitter* e, sunsky_vec3_in nrm, sunsky_vec3_in wi, int distribution,
-                                 float alpha, uint32_t seed, uint32_t spp, size_t n, sunsky_vec3_out em,
-                                 sunsky_vec3_out bs, size_t rstride, void* stream) {
+                                 float alpha, const float* eta, const float* k, uint32_t seed, uint32_t spp, size_t n,
+                                 sunsky_vec3_out em, sunsky_vec3_out bs, float* bw, size_t rstride, void* stream) {
     SUNSKY_PHASE("SamplingIntegratorSample", "direct_conductor_rays");
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (bw && (!eta || !k)) return fail(SUNSKY_ERROR_INVALID_VALUE, "the BSDF weights need eta / k");
     const float one[3] = {1.f, 1.f, 1.f};
     ConductorArgs C;
-    int rc = conductor_args(e, distribution, alpha, one, one, &C);   // the directions do not depend on eta / k
+    // the directions do not depend on eta / k; the weights do
+    int rc = conductor_args(e, distribution, alpha, bw ? eta : one, bw ? k : one, &C);
     if (rc != SUNSKY_OK) return rc;
+    int nw = e->kargs.variant == kSpectral ? 1 : 3;
     if (n == 0) return SUNSKY_OK;
     if (!nrm.x || !nrm.y || !nrm.z || !wi.x || !wi.y || !wi.z)
         return fail(SUNSKY_ERROR_INVALID_VALUE, "null normal / view direction pointer");
@@ -1304,7 +1307,7 @@ int sunsky_direct_conductor_rays(const sunsky_emitter* e, sunsky_vec3_in nrm, su
         DeviceScope dev_scope(e->device);
         const SunskyKArgs* K = e->d_state;
         void* args[] = {&K, &C, (void*)&nrm.x, (void*)&nrm.y, (void*)&nrm.z, (void*)&wi.x, (void*)&wi.y, (void*)&wi.z,
-                        &seed, &spp, &n, &em.x, &em.y, &em.z, &bs.x, &bs.y, &bs.z, &rstride};
+                        &seed, &spp, &n, &em.x, &em.y, &em.z, &bs.x, &bs.y, &bs.z, &rstride, &bw, &nw};
         launch(e->fn(K_DIRECT_CONDUCTOR_RAYS), grid_for(e->mod, K_DIRECT_CONDUCTOR_RAYS, n), (hipStream_t)stream, args);
     });
 }

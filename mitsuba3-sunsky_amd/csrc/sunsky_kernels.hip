@@ -1271,6 +1271,10 @@ __device__ __forceinline__ void sample_wavelengths_one(const SunskyKArgs& K, con
 // LEAN: the host found it_p, ds.dist, ds.p and the active mask all NULL (the common
 // call, u -> d, pdf, weight); the optional pointers and their branches are compiled
 // out, which frees the SGPRs the kernel otherwise spills through v_writelane/v_readlane.
+template <bool FAST>
+__device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
+                                           const float* sun_tab, const float* ldp, const DirTerms& t,
+                                           const float lam[4], float e[4]);
 template <bool FAST, bool SPEC, bool LEAN = false>
 __device__ __forceinline__ void sample_direction_body(
     const SunskyKArgs& K, const float* __restrict__ ux, const float* __restrict__ uy,
@@ -2257,14 +2261,17 @@ __device__ __forceinline__ void direct_conductor_body(
 // The rays of direct_conductor_body's samples, from the same streams and arithmetic (the
 // directions bit for bit): em[s * rstride + i] the emitter sample's world direction, (0, 0,
 // 0) where it contributes nothing (pdf 0, or f cos 0: below either hemisphere or outside
-// the lobe), bs[...] the BSDF sample's reflected world direction, (0, 0, 0) where invalid.
+// the lobe), bs[...] the BSDF sample's reflected world direction, (0, 0, 0) where invalid;
+// bw (if not null) the BSDF sample's weight F(wi.m) G1(wo, m) (roughconductor.cpp:250-262,
+// the caller's path throughput factor) at bw[(c * spp + s) * rstride + i], c < nw, 0 where
+// invalid.
 template <bool FAST>
 __device__ __forceinline__ void direct_conductor_rays_body(
     const SunskyKArgs& K, const ConductorArgs C, const float* __restrict__ nx, const float* __restrict__ ny,
     const float* __restrict__ nz, const float* __restrict__ vx, const float* __restrict__ vy,
     const float* __restrict__ vz, uint32_t seed, uint32_t spp, size_t n, float* __restrict__ ex,
     float* __restrict__ ey, float* __restrict__ ez, float* __restrict__ bx, float* __restrict__ by,
-    float* __restrict__ bz, size_t rstride) {
+    float* __restrict__ bz, size_t rstride, float* __restrict__ bw, int nw) {
     __shared__ TgmmLds<FAST> T;
     stage_tgmm<FAST>(K, &T);
     __syncthreads();
@@ -2299,17 +2306,27 @@ __device__ __forceinline__ void direct_conductor_rays_body(
             ey[o] = em_ok ? d.y : 0.f;
             ez[o] = em_ok ? d.z : 0.f;
             float3_ dw = mk3(0.f, 0.f, 0.f);
+            float g1 = 0.f, dwm = 0.f;
             if (wi.z > 0.f) {
                 float mpdf;
                 const float3_ m = mf_sample(C, wi, u2, u3, &mpdf);
-                const float dwm = dot3(wi, m);
+                dwm = dot3(wi, m);
                 const float3_ r = mk3(fmaf(2.f * dwm, m.x, -wi.x), fmaf(2.f * dwm, m.y, -wi.y), fmaf(2.f * dwm, m.z, -wi.z));
                 const float p = mpdf / (4.f * dot3(r, m));
-                if (p != 0.f && r.z > 0.f) dw = frame_to_world(fs, ft, nrm, r);
+                if (p != 0.f && r.z > 0.f) {
+                    dw = frame_to_world(fs, ft, nrm, r);
+                    g1 = mf_smith_g1(C, r, m);
+                }
             }
             bx[o] = dw.x;
             by[o] = dw.y;
             bz[o] = dw.z;
+            if (bw) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c)
+                    if (c < nw)
+                        bw[((size_t)c * spp + smp) * rstride + i] = g1 != 0.f ? fresnel_conductor_dev(dwm, C.eta[c], C.k[c]) * g1 : 0.f;
+            }
         }
     }
 }
@@ -3065,9 +3082,9 @@ SS_DIRECT_CONDUCTOR(sunsky_direct_conductor_spec_ref, false, true)
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                              \
         const SunskyKArgs* __restrict__ Kp, ConductorArgs C, const float* nx, const float* ny, const float* nz,  \
         const float* vx, const float* vy, const float* vz, uint32_t seed, uint32_t spp, size_t n, float* ex,     \
-        float* ey, float* ez, float* bx, float* by, float* bz, size_t rstride) {                               \
+        float* ey, float* ez, float* bx, float* by, float* bz, size_t rstride, float* bw, int nw) {            \
         direct_conductor_rays_body<FAST>(*Kp, C, nx, ny, nz, vx, vy, vz, seed, spp, n, ex, ey, ez, bx, by, bz,   \
-                                         rstride);                                                             \
+                                         rstride, bw, nw);                                                     \
     }
 SS_DIRECT_CONDUCTOR_RAYS(sunsky_direct_conductor_rays_fast, true)
 SS_DIRECT_CONDUCTOR_RAYS(sunsky_direct_conductor_rays_ref, false)

@@ -535,9 +535,12 @@ class SunskyEmitter:
                                             _ptr(vis), n, n, _ptr(out), out.stride(0), self._stream()))
         return out
 
-    def direct_conductor_rays(self, normals, wi, alpha=0.1, distribution="beckmann", seed=0, spp=1):
+    def direct_conductor_rays(self, normals, wi, alpha=0.1, distribution="beckmann", seed=0, spp=1, eta=None,
+                              k=None):
         """The shadow and BSDF rays of direct_conductor's samples -> (emitter_dir, bsdf_dir), each
-        (3, spp, n) world directions, (0, 0, 0) where no ray is needed."""
+        (3, spp, n) world directions, (0, 0, 0) where no ray is needed.  With eta and k also the
+        BSDF samples' weights F G1 (the throughput of a path continuing along bsdf_dir) ->
+        (emitter_dir, bsdf_dir, bsdf_weight), bsdf_weight (3 | 1, spp, n)."""
         normals, nin = self._vec_in(normals)
         wi, win = self._vec_in(wi)
         n = normals.shape[1]
@@ -546,13 +549,20 @@ class SunskyEmitter:
             raise ValueError(f"invalid distribution '{distribution}', must be 'beckmann' or 'ggx'")
         if int(spp) < 1:
             raise ValueError("spp must be >= 1")
+        if (eta is None) != (k is None):
+            raise ValueError("the BSDF weights need both eta and k")
         em = torch.empty((3, int(spp), n), dtype=torch.float32, device=self.device)
         bs = torch.empty((3, int(spp), n), dtype=torch.float32, device=self.device)
+        bw, e3, k3 = None, None, None
+        if eta is not None:
+            e3 = _fa([float(x) for x in np.broadcast_to(np.asarray(eta, np.float32), (3,))])
+            k3 = _fa([float(x) for x in np.broadcast_to(np.asarray(k, np.float32), (3,))])
+            bw = torch.empty((1 if self.is_spectral else 3, int(spp), n), dtype=torch.float32, device=self.device)
         check(lib().sunsky_direct_conductor_rays(
-            self._h, nin, win, dist, float(alpha), int(seed) & 0xFFFFFFFF, int(spp), n,
+            self._h, nin, win, dist, float(alpha), e3, k3, int(seed) & 0xFFFFFFFF, int(spp), n,
             Vec3Out(em[0].data_ptr(), em[1].data_ptr(), em[2].data_ptr()),
-            Vec3Out(bs[0].data_ptr(), bs[1].data_ptr(), bs[2].data_ptr()), n, self._stream()))
-        return em, bs
+            Vec3Out(bs[0].data_ptr(), bs[1].data_ptr(), bs[2].data_ptr()), _ptr(bw), n, self._stream()))
+        return (em, bs) if bw is None else (em, bs, bw)
 
     def eval_spectral_broadcast(self, wi, wavelengths, active=None, out=None):
         """Spectral eval of one wavelength list for every direction -> (m, n)."""

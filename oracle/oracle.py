@@ -626,13 +626,22 @@ def direct_conductor(em, normals, wi_world, alpha=0.1, distribution="beckmann", 
     return acc / spp
 
 
-def direct_conductor_rays(em, normals, wi_world, alpha=0.1, distribution="beckmann", seed=0, spp=1):
+def direct_conductor_rays(em, normals, wi_world, alpha=0.1, distribution="beckmann", seed=0, spp=1, eta=None,
+                          k=None):
     """The rays a tracer tests for direct_conductor: emitter-sample and BSDF directions, each
-    (spp, n, 3) fp32, zero where no ray is needed."""
-    em_d, bs_d = [], []
+    (spp, n, 3) fp32, zero where no ray is needed; with eta / k also the BSDF samples' weights
+    F(wi.m) G1(wo, m) (roughconductor.cpp sample()), (C, spp, n) fp64 with C = 3 (RGB) or 1."""
+    em_d, bs_d, bw = [], [], []
+    if eta is not None:
+        e3 = np.broadcast_to(np.asarray(eta, np.float64), (3,))[: 1 if em.spectral else 3]
+        k3 = np.broadcast_to(np.asarray(k, np.float64), (3,))[: 1 if em.spectral else 3]
     lam = None if not em.spectral else np.full((1, len(normals)), 500.0, np.float32)
     for r, dg, bpdf, cih, em_ok, dw, pb, b_ok, g1, dwm in _conductor_samples(
             em, normals, wi_world, distribution.lower(), alpha, seed, spp, lam):
         em_d.append(np.where(em_ok[:, None], r["d"], 0.0).astype(np.float32))
         bs_d.append(np.where(b_ok[:, None], dw, 0.0).astype(np.float32))
-    return np.stack(em_d), np.stack(bs_d)
+        if eta is not None:
+            bw.append(np.stack([np.where(b_ok, _fresnel_conductor(dwm, e, kk) * g1, 0.0) for e, kk in zip(e3, k3)]))
+    if eta is None:
+        return np.stack(em_d), np.stack(bs_d)
+    return np.stack(em_d), np.stack(bs_d), np.stack(bw, axis=1)

@@ -271,11 +271,13 @@ def test_direct_conductor_host_errors():
     assert dc(h, v, v, 0, 0.1, one, one, None, 0, 0, 0, 1, None, 0, 0, out, 1, None) == 0        # n = 0
     o3 = ss._capi.Vec3Out(p, p, p)
     rays = L.sunsky_direct_conductor_rays
-    assert rays(h, v, v, 3, 0.1, 0, 1, 1, o3, o3, 1, None) != 0                                  # distribution
-    assert rays(h, v, v, 0, 0.1, 0, 0, 1, o3, o3, 1, None) != 0                                  # spp = 0
-    assert rays(h, v, v, 0, 0.1, 0, 1, 2, o3, o3, 1, None) != 0                                  # ray_stride < n
-    assert rays(h, v, v, 0, 0.1, 0, 1, 1, o3, o3, 1, None) != 0                                  # host-only
-    assert rays(h, v, v, 0, 0.1, 0, 1, 0, o3, o3, 0, None) == 0                                  # n = 0
+    assert rays(h, v, v, 3, 0.1, None, None, 0, 1, 1, o3, o3, None, 1, None) != 0                # distribution
+    assert rays(h, v, v, 0, 0.1, None, None, 0, 0, 1, o3, o3, None, 1, None) != 0                # spp = 0
+    assert rays(h, v, v, 0, 0.1, None, None, 0, 1, 2, o3, o3, None, 1, None) != 0                # ray_stride < n
+    assert rays(h, v, v, 0, 0.1, None, one, 0, 1, 1, o3, o3, out, 1, None) != 0                  # weights, no eta
+    assert b"eta" in L.sunsky_last_error()
+    assert rays(h, v, v, 0, 0.1, None, None, 0, 1, 1, o3, o3, None, 1, None) != 0                # host-only
+    assert rays(h, v, v, 0, 0.1, None, None, 0, 1, 0, o3, o3, None, 0, None) == 0                # n = 0
     L.sunsky_emitter_destroy(h)
     L.sunsky_props_destroy(props)
 
@@ -388,17 +390,26 @@ def test_direct_conductor_rays_parity(precision, distribution):
     2e-6, max < 1e-4); BSDF rays p99.9 < 5e-4, max < 5e-2: fp32 against fp64 visible-normal
     sampling, whose map is ill-conditioned at grazing views (GGX: the denominator
     sin_i p_y + cos_i p_z -> 0; Beckmann: the Newton solve near erfinv's poles) -- measured
-    p99.9 1.2e-4, max 1.0e-2; the same lanes zeroed except on discontinuities (< 1e-3)."""
+    p99.9 1.2e-4, max 1.0e-2; the same lanes zeroed except on discontinuities (< 1e-3).  The
+    BSDF weights F G1 the call returns with eta / k match the oracle's at p99.9 1e-3."""
     em = ss.SunskyEmitter(SCENE, "rgb", precision=precision)
     o32 = O.Oracle(SCENE, "rgb", "jit", "f32")
     o32.override_w_sky(em.sky_sampling_w)
     n, spp, seed, alpha = 1 << 14, 3, 21, 0.2
     normals = _gpu_normals(n, 9)
     wi = _gpu_views(normals, 10)
-    e_g, b_g = em.direct_conductor_rays(_t(normals), _t(wi), alpha, distribution, seed, spp)
+    e_g, b_g, w_g = em.direct_conductor_rays(_t(normals), _t(wi), alpha, distribution, seed, spp, GOLD["eta"],
+                                             GOLD["k"])
     e_g = e_g.permute(1, 2, 0).cpu().numpy()
     b_g = b_g.permute(1, 2, 0).cpu().numpy()
-    e_o, b_o = O.direct_conductor_rays(o32, normals, wi, alpha, distribution, seed, spp)
+    w_g = w_g.cpu().numpy().astype(np.float64)
+    e_o, b_o, w_o = O.direct_conductor_rays(o32, normals, wi, alpha, distribution, seed, spp, GOLD["eta"], GOLD["k"])
+    # the BSDF weights F G1: zero exactly where the direction is, else p99.9 within 1e-3
+    assert np.array_equal(w_g.any(axis=0), b_g.any(axis=2))
+    both = w_g.any(axis=0) & w_o.any(axis=0)
+    wr = (np.abs(w_g - w_o) / np.maximum(w_o, 1e-6)).max(axis=0)[both]
+    assert np.quantile(wr, 0.999) < 1e-3, np.quantile(wr, [0.5, 0.99, 0.999, 1.0])
+    assert np.all((w_g >= 0) & (w_g <= 1))
     for g, o, p999, mx in ((e_g, e_o, 2e-6, 1e-4), (b_g, b_o, 5e-4, 5e-2)):
         zg, zo = ~g.any(axis=2), ~o.any(axis=2)
         assert (zg != zo).mean() < 1e-3, (zg != zo).mean()

@@ -19,6 +19,7 @@ separately; never part of `value`).
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -807,6 +808,12 @@ def main():
             "samples": ns, "achieved_GBps": (8 + 16 + 12 + 4 + 16 + 12 + 4) * ns / ((ms_ss + ms_sq) * 1e-3) / 1e9,
             "note": "spectral emitter, C4 sun: sample_direction with 4 per-sample wavelengths (reads u + 4 lambda, "
                     "writes d, pdf, 4 weights; the unsorted LEAN kernel) + pdf_direction"}
+        vss = valu_floor("sunsky_sample_direction_spec_lean_" + kfx)
+        if vss:
+            sec["sampling_C4_spectral_4lambda"]["valu_roofline"] = {
+                "bound": "valu", "unit": "ms", "sample_direction": dict(vss, achieved_ms=ms_ss, frac=vss["issue_floor_ms"] / ms_ss),
+                "note": "frac = VALU-issue floor (PMC instruction counts x issue cycles / (1024 SIMDs x 2.4 GHz)) / "
+                        "measured launch time"}
         if rank == 0:
             sec["sampling_C4_spectral_4lambda"]["parity"] = parity_c4(
                 smp_sp, dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), u_sp, d_sp, p_sp, w_sp, q_sp, lam=lam_sp)
@@ -839,7 +846,34 @@ def main():
                                            "note": "per sample: sample_direction + eval (emitter sampling), cosine "
                                                    "BSDF sample + pdf_direction + eval (escaped ray), power-heuristic "
                                                    "MIS; C4 sun/sky, random normals; one fused kernel"}
-        del nrm, dd
+        # the glossy vertex: the same points seen from random view directions, a rough conductor
+        # (GGX, alpha 0.2, gold-like eta / k) -- sunsky_direct_conductor, reads 24 B, writes 12 B
+        vw = torch.randn((3, npts), generator=g, device=dev)
+        vw = vw * torch.sign((vw * nrm).sum(0, keepdim=True))
+        vw = (vw / vw.norm(dim=0, keepdim=True)).contiguous()
+        w_in = ss._capi.Vec3In(vw[0].data_ptr(), vw[1].data_ptr(), vw[2].data_ptr())
+        eta3 = (ctypes.c_float * 3)(0.143, 0.374, 1.442)
+        k3 = (ctypes.c_float * 3)(3.983, 2.385, 1.603)
+
+        def conductor_step():
+            rc = lib.sunsky_direct_conductor(smp._h, n_in, w_in, 1, 0.2, eta3, k3, None, 0, 0, 7, spp, None, 0, npts,
+                                             dd.data_ptr(), npts, stream)
+            if rc:
+                raise RuntimeError(lib.sunsky_last_error().decode())
+
+        conductor_step()
+        t_c = KernelTimer()
+        t_c.begin()
+        for _ in range(reps):
+            conductor_step()
+        t_c.end(reps)
+        ms_c = t_c.mean_ms()
+        sec["direct_conductor_16M_x4spp"] = {"samples_per_s": npts * spp / (ms_c * 1e-3), "ms": ms_c,
+                                             "points": npts, "spp": spp,
+                                             "note": "per sample: sample_direction + eval + rough-conductor eval/pdf "
+                                                     "(emitter sampling), GGX visible-normal sample + pdf_direction + "
+                                                     "eval (escaped ray), power-heuristic MIS; one fused kernel"}
+        del nrm, dd, vw
         if rank == 0:
             result["secondary"] = sec
 

@@ -42,7 +42,8 @@
 extern "C" {
 #endif
 
-#define SUNSKY_AMD_ABI_VERSION 3   /* 3: direct_diffuse visibility, direct_diffuse_rays */
+#define SUNSKY_AMD_ABI_VERSION 4   /* 3: direct_diffuse visibility, direct_diffuse_rays; 4: direct_conductor(_rays),
+                                     emitter_tangent_tables, direct_diffuse draws sample_1 (path.cpp:233) */
 
 typedef enum sunsky_status {
     SUNSKY_OK = 0,

@@ -34,6 +34,10 @@ CASES = [
     ("spectral", "scalar", hour_dict(5.2, 9.5, 0.2, 1.0, 1.0)),
     ("rgb", "jit", dict(angles_dict(3.0, 0.5, np.deg2rad(40), 0.3, 1.0, 1.0), sun_aperture=30.0)),
     ("rgb", "jit", angles_dict(1.0, 0.5, np.deg2rad(95), 0.3, 1.0, 1.0)),   # sun below the horizon
+    # configs[3] (C4, the sampling benchmark's emitter): T 3, elevation 30 deg, albedo 0.3
+    ("rgb", "jit", angles_dict(3.0, 0.0, np.deg2rad(60), 0.3, 1.0, 1.0)),
+    ("rgb", "scalar", angles_dict(3.0, 0.0, np.deg2rad(60), 0.3, 1.0, 1.0)),
+    ("spectral", "jit", angles_dict(3.0, 0.0, np.deg2rad(60), 0.3, 1.0, 1.0)),
 ]
 
 

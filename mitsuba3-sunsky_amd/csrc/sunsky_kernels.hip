@@ -48,6 +48,12 @@ using namespace sunsky;
 #ifndef SS_SPEC_SAMPLE_ATTR
 #define SS_SPEC_SAMPLE_ATTR
 #endif
+#ifndef SS_RGB_SORTED_ATTR   // probe builds (tools/build) set occupancy attributes here
+#define SS_RGB_SORTED_ATTR
+#endif
+#ifndef SS_SORT_R            // probe builds: the window of the wave-sorted RGB kernels
+#define SS_SORT_R 4
+#endif
 constexpr float kLog2e = 1.44269504088896340736f;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -2996,7 +3002,7 @@ SS_SAMPLE_DIRECTION_SPEC_LEAN(sunsky_sample_direction_spec_lean_ref, false)
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_loop_fast, true, true, true)
 
 #define SS_SAMPLE_DIRECTION_SORTED(NAME, FAST, R, FULL)                                                           \
-    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_RGB_SORTED_ATTR void NAME(                            \
         const SunskyKArgs* __restrict__ Kp, const float* ux, const float* uy, const float* px, const float* py, const float* pz,   \
         const float* lam, size_t lstride, int nlam, const uint8_t* active, size_t n, float* dx, float* dy,     \
         float* dz, float* pdf, float* dist, float* opx, float* opy, float* opz, float* weight, size_t wstride) { \
@@ -3009,8 +3015,8 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_loop_fast, true, true, tru
 // precisions reproduce the general kernel's bits (test_sample_direction_lean_kernel_bitwise,
 // test_wave_sorted_rgb_kernels_bitwise_vs_unsorted) since the file contracts within
 // expressions only (the pragma at the top).
-SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_fast, true, 4, false)
-SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_ref, false, 4, false)
+SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_fast, true, SS_SORT_R, false)
+SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_ref, false, SS_SORT_R, false)
 // The general call (it.p, ds.dist, ds.p, mask) in the same windows: bitwise the unsorted kernel
 // (test_wave_sorted_rgb_kernels_bitwise_vs_unsorted) but 2 % slower (125 VGPRs and 28 SGPR spills,
 // 4 waves/SIMD; profiles/r02_v13_ab_sample_full.log), so the C ABI keeps the unsorted general kernel.

@@ -6,7 +6,9 @@
 //
 //   kbench <hsaco> <rgb|spec|sample|pdf> <n> <iters> <blocks_per_cu,...> <kernel> [kernel ...]
 // rgb / spec: eval kernels on uniform upper-hemisphere directions (C2 / C3 emitters);
-// sample / pdf: sample_direction (ds.dist, ds.p not requested) / pdf_direction (C4 emitter).
+// sample / pdf: sample_direction (ds.dist, ds.p not requested) / pdf_direction (C4 emitter);
+// conductor: direct_conductor (C4 emitter, GGX alpha 0.2 -- KB_BECKMANN=1 for Beckmann --,
+// gold-like eta / k, 4 spp at random normals and views).
 //
 // Build: make -C tools kbench
 #include <hip/hip_runtime_api.h>
@@ -56,7 +58,8 @@ int main(int argc, char** argv) {
     }
     const bool spec = mode == "spec";
     const bool rays = mode == "rays";   // per-ray spectral eval, 4 random wavelengths per ray (Spectrum<Float, 4>)
-    const bool sampling = mode == "sample" || mode == "pdf";
+    const bool cond = mode == "conductor";
+    const bool sampling = mode == "sample" || mode == "pdf" || cond;
     const char* pack = std::getenv("SUNSKY_AMD_DATASET");
     std::string pack_path = pack ? pack : "mitsuba3-sunsky_amd/data/sunsky_datasets.pack";
 
@@ -93,6 +96,25 @@ int main(int argc, char** argv) {
         hx[i] = -st * std::cos(ph); hy[i] = -st * std::sin(ph); hz[i] = -ct;
     }
     const int nout = spec ? 11 : rays ? 4 : (mode == "pdf" ? 1 : 3);
+    // conductor mode: normals (mostly facing up) and views in their upper hemisphere
+    struct ConductorArgs { int type; float alpha; float eta[4], k[4]; };
+    ConductorArgs cargs = {std::getenv("KB_BECKMANN") ? 0 : 1, 0.2f, {0.143f, 0.374f, 1.442f, 0.f}, {3.983f, 2.385f, 1.603f, 0.f}};
+    float *cnx = nullptr, *cny = nullptr, *cnz = nullptr, *cvx = nullptr, *cvy = nullptr, *cvz = nullptr;
+    if (cond) {
+        std::normal_distribution<float> G(0.f, 1.f);
+        std::vector<float> h(6 * n);
+        for (size_t i = 0; i < n; ++i) {
+            float a[3] = {G(rng), G(rng), std::fabs(G(rng)) + 0.2f}, b[3] = {G(rng), G(rng), G(rng)};
+            float la = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+            float d = a[0] * b[0] + a[1] * b[1] + a[2] * b[2], sg = d < 0 ? -1.f : 1.f;
+            float lb = std::sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]);
+            for (int c = 0; c < 3; ++c) { h[c * n + i] = a[c] / la; h[(3 + c) * n + i] = sg * b[c] / lb; }
+        }
+        float* buf = nullptr;
+        CK(hipMalloc(&buf, 6 * n * 4));
+        CK(hipMemcpy(buf, h.data(), 6 * n * 4, hipMemcpyHostToDevice));
+        cnx = buf; cny = buf + n; cnz = buf + 2 * n; cvx = buf + 3 * n; cvy = buf + 4 * n; cvz = buf + 5 * n;
+    }
     float *wx, *wy, *wz, *out;
     CK(hipMalloc(&wx, n * 4)); CK(hipMalloc(&wy, n * 4)); CK(hipMalloc(&wz, n * 4));
     CK(hipMalloc(&out, n * 4 * nout));
@@ -193,8 +215,11 @@ int main(int argc, char** argv) {
                                         &dd, &ddy, &ddz, &pdf, &fdist, &fox, &foy, &foz, &wgt, &n};
             void* args_pdf[] = {&K, &dd, &ddy, &ddz, &active, &n, &pdf};
             void* args_rays[] = {&K, &wx, &wy, &wz, &lamp, &n, &nl4, &active, &n, &out, &ostride, &sign};
+            uint32_t cseed = 7, cspp = 4;
+            void* args_cond[] = {&K, &cargs, &cnx, &cny, &cnz, &cvx, &cvy, &cvz, &nullf, &zero, &nl0, &cseed, &cspp,
+                                 &active, &zero, &n, &out, &ostride};
             void** args = spec ? args_spec : rays ? args_rays : mode == "sample" ? (full ? args_sample_full : args_sample)
-                                            : mode == "pdf" ? args_pdf : args_rgb;
+                                            : mode == "pdf" ? args_pdf : cond ? args_cond : args_rgb;
             for (int w = 0; w < 3; ++w) CK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
             hipEvent_t e0, e1;
             CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -218,7 +243,7 @@ int main(int argc, char** argv) {
                 CK(hipMemcpy(h.data() + 3 * n, pdf, n * 4, hipMemcpyDeviceToHost));
                 CK(hipMemcpy(h.data() + 4 * n, wgt, 3 * n * 4, hipMemcpyDeviceToHost));
             } else {
-                CK(hipMemcpy(h.data(), sampling ? (mode == "pdf" ? pdf : wgt) : out, h.size() * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(h.data(), sampling && !cond ? (mode == "pdf" ? pdf : wgt) : out, h.size() * 4, hipMemcpyDeviceToHost));
             }
             double maxrel = 0;
             size_t ndiff = 0;

@@ -807,8 +807,8 @@ def main():
             "samples_per_s": ns / ((ms_ss + ms_sq) * 1e-3), "sample_direction_ms": ms_ss, "pdf_direction_ms": ms_sq,
             "samples": ns, "achieved_GBps": (8 + 16 + 12 + 4 + 16 + 12 + 4) * ns / ((ms_ss + ms_sq) * 1e-3) / 1e9,
             "note": "spectral emitter, C4 sun: sample_direction with 4 per-sample wavelengths (reads u + 4 lambda, "
-                    "writes d, pdf, 4 weights; the unsorted LEAN kernel) + pdf_direction"}
-        vss = valu_floor("sunsky_sample_direction_spec_lean_" + kfx)
+                    "writes d, pdf, 4 weights; the wave-sorted LEAN kernel) + pdf_direction"}
+        vss = valu_floor("sunsky_sample_direction_spec_lean4_sorted_" + kfx)
         if vss:
             sec["sampling_C4_spectral_4lambda"]["valu_roofline"] = {
                 "bound": "valu", "unit": "ms", "sample_direction": dict(vss, achieved_ms=ms_ss, frac=vss["issue_floor_ms"] / ms_ss),

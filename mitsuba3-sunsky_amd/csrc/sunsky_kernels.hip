@@ -1487,6 +1487,135 @@ __device__ __forceinline__ void sample_direction_spec4_body(
     }
 }
 
+// Orders a wave's own LDS accesses across the phases of a sorted window: an IR-level
+// wavefront-scope fence (no instruction on gfx950: a wave's LDS operations execute in
+// issue order) plus the scheduling barrier.
+__device__ __forceinline__ void wave_lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+// One spectral sample at 4 wavelengths (u, lambda -> d, pdf, 4 weights): the per-sample
+// work of sample_direction_spec4_body in the same operation order (bitwise its outputs).
+template <bool FAST>
+__device__ __forceinline__ void sample_one_spec4(const SunskyKArgs& K, const SamplerLds<FAST, true>& S, float sx,
+                                                 float sy, const float l[4], float inv_w, float inv_w_sun, float o[8]) {
+    const bool pick_sky = sx < K.w_sky;
+    const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
+    const bool act = sd.z >= 0.f;
+    const float3_ d = to_world(K, sd);
+    float skyp, sunp;
+    compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+    const float pd = lerpf_(sunp, skyp, K.w_sky);
+    o[0] = d.x; o[1] = d.y; o[2] = d.z; o[3] = pd;
+    DirTerms t = dir_terms<FAST>(K, to_local(K, d), act);
+    add_sun_terms<FAST>(K, t);
+    float e[4];
+    eval_spec4<FAST>(K, S.chans.c, S.sun, S.ldp, t, l, e);
+    const float inv_pd = fdiv<FAST>(1.f, pd);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float w = FAST ? e[k] * inv_pd : e[k] / pd;
+        o[4 + k] = isfinite(w) ? w : 0.f;
+    }
+}
+
+// Wave-sorted spectral LEAN sample_direction at Mitsuba's 4 wavelengths per sample, the
+// RGB kernel's windows (sample_direction_sorted_body) for the spectral body: a wave ranks a
+// window of 64 R samples sky picks first, runs R passes over the ranked order (only the
+// pass holding the sky/sun boundary runs both the TGMM sampling branch and the sun-disc
+// terms of 4 wavelengths), and un-sorts the 8 outputs through its LDS rows so the global
+// loads and non-temporal stores stay coalesced in sample order.  The 6 inputs (u, 4 lambda)
+// and the 8 outputs share the rows: pass p reads its columns' inputs, then writes their
+// outputs.  Each sample goes through sample_one_spec4: bitwise the unsorted kernel.
+template <bool FAST, int R>
+__device__ __forceinline__ void sample_direction_spec4_sorted_body(
+    const SunskyKArgs& K, const float* __restrict__ ux, const float* __restrict__ uy, const float* __restrict__ lam,
+    size_t lstride, size_t n, float* __restrict__ dx, float* __restrict__ dy, float* __restrict__ dz,
+    float* __restrict__ pdf, float* __restrict__ weight, size_t wstride) {
+    constexpr int W = 64 * R;
+    __shared__ SamplerLds<FAST, true> S;
+    __shared__ float X[SS_BLOCK / 64][8][W];
+    stage_sampler_lds<FAST, true>(K, &S);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float(*Y)[W] = X[wv];
+    const float inv_w = uniform_f(1.f / K.w_sky), inv_w_sun = uniform_f(1.f / (1.f - K.w_sky));
+    const size_t nwin = (n + W - 1) / W;
+    const size_t wstep = (size_t)gridDim.x * (SS_BLOCK / 64);
+    float na[R], nb[R], nl[4][R];
+    auto load_window = [&](size_t w) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t i = w * W + (size_t)(r * 64 + lane);
+            na[r] = i < n ? ux[i] : 1.f;   // past the end: a sun pick, computed and not stored
+            nb[r] = i < n ? uy[i] : 0.5f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) nl[k][r] = i < n ? lam[(size_t)k * lstride + i] : 500.f;
+        }
+    };
+    size_t w = (size_t)blockIdx.x * (SS_BLOCK / 64) + wv;
+    if (w < nwin) load_window(w);
+    for (; w < nwin; w += wstep) {
+        const size_t base = w * W;
+        int slot[R];
+        {
+            float a[R], b[R], l[4][R];
+            uint64_t m[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                a[r] = na[r];
+                b[r] = nb[r];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) l[k][r] = nl[k][r];
+            }
+            if (w + wstep < nwin) load_window(w + wstep);
+#pragma unroll
+            for (int r = 0; r < R; ++r) m[r] = __ballot(a[r] < K.w_sky);
+            int psun = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) psun += __popcll(m[r]);
+            int psky = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const bool sky = (m[r] >> lane) & 1;
+                slot[r] = sky ? psky + lanes_below(m[r]) : psun + lanes_below(~m[r]);
+                Y[0][slot[r]] = a[r];
+                Y[1][slot[r]] = b[r];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) Y[2 + k][slot[r]] = l[k][r];
+                const int c = __popcll(m[r]);
+                psky += c;
+                psun += 64 - c;
+            }
+        }
+        wave_lds_order();
+#pragma unroll 1
+        for (int p = 0; p < R; ++p) {
+            const int q = p * 64 + lane;
+            const float l4[4] = {Y[2][q], Y[3][q], Y[4][q], Y[5][q]};
+            float o[8];
+            sample_one_spec4<FAST>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) Y[k][q] = o[k];
+        }
+        wave_lds_order();
+        float* const planes[8] = {dx, dy, dz, pdf, weight, weight + wstride, weight + 2 * wstride, weight + 3 * wstride};
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t i = base + (size_t)(r * 64 + lane);
+            if (i < n) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) store_nt(Y[k][slot[r]], planes[k] + i);
+            }
+        }
+        wave_lds_order();
+    }
+}
+
 // One RGB sample (u -> d, pdf, weight), the per-sample work of
 // sample_direction_body<FAST, false, LEAN> in the same operation order; `act` is the
 // caller's mask (true in the LEAN form).
@@ -1521,18 +1650,6 @@ __device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const Sampl
         const float w = FAST ? e[c] * inv_pd : e[c] / pd;
         o[4 + c] = isfinite(w) ? w : 0.f;
     }
-}
-
-// Orders a wave's own LDS accesses across the phases of a sorted window: an IR-level
-// wavefront-scope fence (no instruction on gfx950: a wave's LDS operations execute in
-// issue order) plus the scheduling barrier.
-__device__ __forceinline__ void wave_lds_order() {
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
-
-__device__ __forceinline__ int lanes_below(uint64_t m) {
-    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
 // Wave-sorted RGB sample_direction (sunsky.cpp:399-441).  A wave takes a window of
@@ -3047,6 +3164,26 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_rgb_lean_plain_ref, false, false, tr
     }
 SS_SAMPLE_DIRECTION_SPEC_LEAN(sunsky_sample_direction_spec_lean_fast, true)
 SS_SAMPLE_DIRECTION_SPEC_LEAN(sunsky_sample_direction_spec_lean_ref, false)
+// LEAN spectral sample_direction at 4 wavelengths in wave-sorted windows of SS_SPEC_SORT_R x 64
+// samples (the C ABI's call when nlam == 4): bitwise the unsorted LEAN kernel
+// (test_spectral_sorted_kernel_bitwise_vs_unsorted)
+#ifndef SS_SPEC_SORT_R
+#define SS_SPEC_SORT_R 3
+#endif
+// 4 waves/SIMD (127 VGPRs, 2 spilled; 131 and 3 waves without): interleaved A/B against the
+// unsorted LEAN kernel 0.963 (3 waves: 1.027; R = 2: 0.999, at 4 waves 0.994), profiles/r03_v13_ab_spec_sorted.log
+#ifndef SS_SPEC_SORTED_ATTR
+#define SS_SPEC_SORTED_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+#endif
+#define SS_SAMPLE_DIRECTION_SPEC4_SORTED(NAME, FAST, R)                                                       \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_SPEC_SORTED_ATTR void NAME(                           \
+        const SunskyKArgs* __restrict__ Kp, const float* ux, const float* uy, const float* px, const float* py, const float* pz,   \
+        const float* lam, size_t lstride, int nlam, const uint8_t* active, size_t n, float* dx, float* dy,     \
+        float* dz, float* pdf, float* dist, float* opx, float* opy, float* opz, float* weight, size_t wstride) { \
+        sample_direction_spec4_sorted_body<FAST, R>(*Kp, ux, uy, lam, lstride, n, dx, dy, dz, pdf, weight, wstride); \
+    }
+SS_SAMPLE_DIRECTION_SPEC4_SORTED(sunsky_sample_direction_spec_lean4_sorted_fast, true, SS_SPEC_SORT_R)
+SS_SAMPLE_DIRECTION_SPEC4_SORTED(sunsky_sample_direction_spec_lean4_sorted_ref, false, SS_SPEC_SORT_R)
 // the previous LEAN spectral form (wavelength loop, lambda not prefetched), for A/B timing
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_loop_fast, true, true, true)
 

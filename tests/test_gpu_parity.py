@@ -291,6 +291,51 @@ def test_wave_sorted_rgb_kernels_bitwise_vs_unsorted(precision, monkeypatch):
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)
+def test_spectral_sorted_kernel_bitwise_vs_unsorted(precision, monkeypatch):
+    """The spectral LEAN sample_direction at 4 wavelengths per sample runs in wave-sorted
+    windows of 3 x 64 samples (sky picks first, outputs written back in sample order).
+    Against the unsorted LEAN kernel (SUNSKY_AMD_UNSORTED_SAMPLING=1) d, pdf and the 4
+    weights are bit for bit the same, and both equal the general call's (+ it.p, ds.p,
+    ds.dist), for batch sizes ending inside a window, a pass or a lane, all-sky and all-sun
+    windows, u.x at and next to w_sky, at 0 and 1 - ulp, out-of-range u, wavelengths at the
+    nodes, at 360 / 720 nm and outside [360, 720], and a rotated emitter."""
+    d = angles_dict(3.0, 1.1, np.deg2rad(60), 0.3, 1.0, 1.0)
+    d["to_world"] = np.array([[0, 0, 1, 0], [1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 0, 1]], np.float64)
+    em = ss.SunskyEmitter(d, "spectral", precision=precision)
+    w = np.float32(em.sky_sampling_w)
+    rng = np.random.default_rng(12)
+    special = np.array([w, np.nextafter(w, 0, dtype=np.float32), np.nextafter(w, 1, dtype=np.float32), 0.0,
+                        np.nextafter(np.float32(1), 0, dtype=np.float32)], np.float32)
+    odd = np.array([[np.nan, 0.5], [-0.0, 0.3], [-1e-30, 0.7], [1.0, 0.2], [1.5, 0.9], [np.inf, 0.1],
+                    [0.2, np.nan], [0.9, -0.25], [0.1, 1.0], [0.6, 0.0]], np.float32)
+
+    def run(ut, lam, p, positions):
+        ds, wt = em.sample_direction(ss.Interaction3f(p=p, wavelengths=lam), ut, positions=positions)
+        return [host(x).view(np.uint32).copy() for x in [ds.d, ds.pdf, wt]]
+
+    for n in (1, 5, 63, 64, 65, 191, 192, 193, 1000, 1024, 4097, 65537, (1 << 20) + 1):
+        u = rng.random((n, 2), dtype=np.float32)
+        u[: min(n, 5), 0] = special[: min(n, 5)]
+        lam = rng.uniform(360, 720, (4, n)).astype(np.float32)
+        if n >= 2048:
+            u[192:384, 0] *= w          # an all-sky window
+            u[384:576, 0] = w + (1 - w) * u[384:576, 0]   # an all-sun window
+            u[1000:1010] = odd
+            lam[:, 1100:1111] = np.arange(320, 721, 40, dtype=np.float32)[None, :]
+            lam[:, 1200:1206] = np.array([360, 720, 300, 800, np.nextafter(np.float32(720), 0), 359.9], np.float32)[None, :]
+        ut = soa(u)
+        lt = torch.from_numpy(lam).cuda()
+        p = torch.from_numpy(rng.normal(size=(3, n)).astype(np.float32) * 10).cuda()
+        monkeypatch.delenv("SUNSKY_AMD_UNSORTED_SAMPLING", raising=False)
+        srt = run(ut, lt, None, False)
+        full = run(ut, lt, p, True)
+        monkeypatch.setenv("SUNSKY_AMD_UNSORTED_SAMPLING", "1")
+        plain = run(ut, lt, None, False)
+        for a_, b_, c_ in zip(srt, plain, full):
+            assert np.array_equal(a_, b_) and np.array_equal(a_, c_), n
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
 @pytest.mark.parametrize("elev_deg", [0.1, 0.6, 3.0, 20.0, 60.0, 89.5])
 def test_sun_disc_weights_across_elevations(elev_deg, precision):
     """Sun-picked samples (sunsky.cpp:697-701) at sun elevations whose disc spans one to

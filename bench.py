@@ -81,6 +81,18 @@ class KernelTimer:
         torch.cuda.synchronize()
         return self.t0.elapsed_time(self.t1) / max(self.launches, 1)
 
+    def mean_ms_with_clock(self):
+        """mean_ms, plus the GFX clock (amd-smi, torch.cuda.clock_rate) polled on the host
+        while the burst runs: (ms, median MHz or None)."""
+        clk = []
+        try:
+            while not self.t1.query():
+                clk.append(torch.cuda.clock_rate())
+                time.sleep(0.002)
+        except Exception:   # no SMI access: the timing alone
+            clk = []
+        return self.mean_ms(), (float(np.median(clk)) if clk else None)
+
 
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
@@ -142,6 +154,60 @@ def valu_floor(kernel):
         return None
     return {"valu_wave_insts": rec["valu_wave_insts"], "trans_wave_insts": rec["trans_wave_insts"],
             "issue_floor_ms": rec["valu_issue_floor_ms"], "source": os.path.relpath(files[-1], ROOT)}
+
+
+def sclk_under_valu_load(dev):
+    """GFX clock (MHz, amd-smi through torch.cuda.clock_rate) sampled while every SIMD runs
+    independent FMA chains (tools/clock_probe.hip, built by build(); ~0.3 s of load): the
+    VALU-bound lines scale with the clock the power manager grants, which differs from box
+    to box.  None when the probe's code object is absent."""
+    path = os.path.join(ROOT, "tools", "build", "clock_probe.hsaco")
+    if not os.path.exists(path):
+        return None
+    hip = ctypes.CDLL("libamdhip64.so")
+    mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
+    if hip.hipModuleLoad(ctypes.byref(mod), path.encode()) != 0:
+        return None
+    try:
+        if hip.hipModuleGetFunction(ctypes.byref(fn), mod, b"sunsky_tools_clock_probe") != 0:
+            return None
+        cu = torch.cuda.get_device_properties(dev).multi_processor_count
+        blocks = cu * 8
+        out = torch.zeros(2 * blocks, dtype=torch.int64, device=dev)
+        stream = torch.cuda.current_stream(dev)
+
+        def launch(iters):
+            p_out, it = ctypes.c_void_p(out.data_ptr()), ctypes.c_int(iters)
+            a, b = ctypes.c_float(1.0000001), ctypes.c_float(1e-7)
+            args = (ctypes.c_void_p * 4)(*[ctypes.cast(ctypes.pointer(x), ctypes.c_void_p) for x in (p_out, it, a, b)])
+            rc = hip.hipModuleLaunchKernel(fn, blocks, 1, 1, 256, 1, 1, 0, ctypes.c_void_p(stream.cuda_stream), args,
+                                           None)
+            if rc != 0:
+                raise RuntimeError(f"clock probe launch failed ({rc})")
+        launch(2000)
+        torch.cuda.synchronize(dev)
+        idle = torch.cuda.clock_rate(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        launch(4000000)
+        e1.record(stream)
+        samples = []
+        time.sleep(0.02)
+        while not e1.query():
+            samples.append(torch.cuda.clock_rate(dev))
+            time.sleep(0.005)
+        torch.cuda.synchronize(dev)
+        load_ms = e0.elapsed_time(e1)
+        if not samples:
+            return {"error": "no clock sample during the load", "load_ms": load_ms}
+        return {"gfxclk_mhz_median": float(np.median(samples)), "gfxclk_mhz_min": float(min(samples)),
+                "gfxclk_mhz_max": float(max(samples)), "samples": len(samples), "gfxclk_mhz_idle": float(idle),
+                "load_ms": load_ms,
+                "note": "GFX clock reported by amd-smi (torch.cuda.clock_rate) while every SIMD runs independent FMA "
+                        "chains (tools/clock_probe.hip).  The VALU-bound sampling and caller lines scale with it; the "
+                        "HBM-bound headline does not"}
+    finally:
+        hip.hipModuleUnload(mod)
 
 
 def host_cpu_topology():
@@ -713,10 +779,12 @@ def main():
             for _ in range(reps):
                 pdf_step()
             t_p.end(reps)
-            ms_s, ms_p = t_s.mean_ms(), t_p.mean_ms()
+            ms_s, clk_s = t_s.mean_ms_with_clock()
+            ms_p = t_p.mean_ms()
             ms = ms_s + ms_p
             sec[key] = {"samples_per_s": ns / (ms * 1e-3), "ms": ms, "samples": ns,
                         "sample_direction_ms": ms_s, "pdf_direction_ms": ms_p, "w_sky": smp_s.sky_sampling_w,
+                        "gfxclk_mhz_during_sample_direction": clk_s,
                         "achieved_GBps": BYTES_SAMPLE * ns / (ms * 1e-3) / 1e9,
                         "note": "sample_direction (reads u; writes d, pdf, RGB weight) + pdf_direction "
                                 "(reads d; writes pdf); " + ("JIT semantics, w_sky from the quadrature" if sem == "jit"
@@ -802,9 +870,11 @@ def main():
         for _ in range(reps):
             spec_pdf_step()
         t_sq.end(reps)
-        ms_ss, ms_sq = t_ss.mean_ms(), t_sq.mean_ms()
+        ms_ss, clk_ss = t_ss.mean_ms_with_clock()
+        ms_sq = t_sq.mean_ms()
         sec["sampling_C4_spectral_4lambda"] = {
             "samples_per_s": ns / ((ms_ss + ms_sq) * 1e-3), "sample_direction_ms": ms_ss, "pdf_direction_ms": ms_sq,
+            "gfxclk_mhz_during_sample_direction": clk_ss,
             "samples": ns, "achieved_GBps": (8 + 16 + 12 + 4 + 16 + 12 + 4) * ns / ((ms_ss + ms_sq) * 1e-3) / 1e9,
             "note": "spectral emitter, C4 sun: sample_direction with 4 per-sample wavelengths (reads u + 4 lambda, "
                     "writes d, pdf, 4 weights; the wave-sorted LEAN kernel) + pdf_direction"}
@@ -875,6 +945,10 @@ def main():
                                                      "eval (escaped ray), power-heuristic MIS; one fused kernel"}
         del nrm, dd, vw
         if rank == 0:
+            try:
+                sec["sclk_under_valu_load"] = sclk_under_valu_load(dev)
+            except Exception as exc:   # a diagnostic beside the lines; never fail the bench
+                sec["sclk_under_valu_load"] = {"error": f"{type(exc).__name__}: {exc}"}
             result["secondary"] = sec
 
     # ----------------------------------------------------------- optional gather

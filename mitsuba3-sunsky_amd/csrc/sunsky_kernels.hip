@@ -1308,13 +1308,25 @@ __device__ __forceinline__ void sample_direction_body(
     // A sorted form (a workgroup ranks 256-1024 samples sky-first through LDS so only
     // one 64-lane pass per tile runs both branches, outputs staged in LDS) was 5-25 %
     // slower: profiles/r02_v6_ab_sample_prefetch_sorted.log.
+    // (the general call's it.p and mask are prefetched the same way: they feed ds.p / ds.dist
+    // and the weight after the sample's work)
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    float nx = 0.f, ny = 0.f;
-    if (i < n) { nx = ux[i]; ny = uy[i]; }
+    float nx = 0.f, ny = 0.f, npx = 0.f, npy = 0.f, npz = 0.f;
+    bool nact = true;
+    auto load = [&](size_t j) {
+        nx = ux[j];
+        ny = uy[j];
+        if (active) nact = active[j] != 0;
+        if (px) npx = px[j];
+        if (py) npy = py[j];
+        if (pz) npz = pz[j];
+    };
+    if (i < n) load(i);
     for (; i < n; i += stride) {
-        bool act = active ? active[i] != 0 : true;
+        bool act = nact;
         const float sx = nx, sy = ny;
-        if (i + stride < n) { nx = ux[i + stride]; ny = uy[i + stride]; }
+        const float3_ itp = mk3(npx, npy, npz);
+        if (i + stride < n) load(i + stride);
         const bool pick_sky = sx < K.w_sky;
         // sx / w and the reused sample stay correctly rounded even in FAST: the
         // discrete-distribution reuse divides by the picked gaussian's pmf, so one
@@ -1338,7 +1350,6 @@ __device__ __forceinline__ void sample_direction_body(
         store_nt(d.z, dz + i);
         store_nt(pd, pdf + i);
         if (dist || opx) {
-            float3_ itp = mk3(px ? px[i] : 0.f, py ? py[i] : 0.f, pz ? pz[i] : 0.f);
             float3_ rel = mk3(itp.x - K.bs_center[0], itp.y - K.bs_center[1], itp.z - K.bs_center[2]);
             float dd = 2.f * fmaxf(K.bs_radius, sqrtf(dot3(rel, rel)));
             if (dist) dist[i] = dd;

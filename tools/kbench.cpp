@@ -58,7 +58,7 @@ int main(int argc, char** argv) {
     }
     const bool spec = mode == "spec";
     const bool rays = mode == "rays";   // per-ray spectral eval, 4 random wavelengths per ray (Spectrum<Float, 4>)
-    const bool cond = mode == "conductor";
+    const bool cond = mode == "conductor" || mode == "diffuse";   // the callers (diffuse: the normals only)
     const bool sampling = mode == "sample" || mode == "pdf" || cond;
     const char* pack = std::getenv("SUNSKY_AMD_DATASET");
     std::string pack_path = pack ? pack : "mitsuba3-sunsky_amd/data/sunsky_datasets.pack";
@@ -218,8 +218,11 @@ int main(int argc, char** argv) {
             uint32_t cseed = 7, cspp = 4;
             void* args_cond[] = {&K, &cargs, &cnx, &cny, &cnz, &cvx, &cvy, &cvz, &nullf, &zero, &nl0, &cseed, &cspp,
                                  &active, &zero, &n, &out, &ostride};
+            void* args_diff[] = {&K, &cnx, &cny, &cnz, &nullf, &nullf, &zero, &nl0, &cseed, &cspp, &active, &zero, &n,
+                                 &out, &ostride};
             void** args = spec ? args_spec : rays ? args_rays : mode == "sample" ? (full ? args_sample_full : args_sample)
-                                            : mode == "pdf" ? args_pdf : cond ? args_cond : args_rgb;
+                                            : mode == "pdf" ? args_pdf : mode == "diffuse" ? args_diff
+                                            : cond ? args_cond : args_rgb;
             for (int w = 0; w < 3; ++w) CK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
             hipEvent_t e0, e1;
             CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));

@@ -137,6 +137,30 @@ static int gpu_mode(const std::string& dir) {
     HIPCK(hipDeviceSynchronize());
     std::vector<float> occluded(3 * n);
     HIPCK(hipMemcpy(occluded.data(), d_dd, 3 * n * 4, hipMemcpyDeviceToHost));
+    // a rough-conductor vertex at the same points seen from one view direction: GGX, alpha 0.2,
+    // gold-like eta / k, seed 5, 2 spp; then its rays' BSDF weights (F G1 per channel)
+    float* d_wv;
+    HIPCK(hipMalloc(&d_wv, 3 * n * 4));
+    {
+        std::vector<float> wv(3 * n);
+        const float vx = 0.3f, vy = 0.1f, vz = 0.95f, l = std::sqrt(vx * vx + vy * vy + vz * vz);
+        for (size_t i = 0; i < n; ++i) { wv[i] = vx / l; wv[n + i] = vy / l; wv[2 * n + i] = vz / l; }
+        HIPCK(hipMemcpy(d_wv, wv.data(), 3 * n * 4, hipMemcpyHostToDevice));
+    }
+    const float eta[3] = {0.143f, 0.374f, 1.442f}, kk[3] = {3.983f, 2.385f, 1.603f};
+    em.direct_conductor({d_nrm, d_nrm + n, d_nrm + 2 * n}, {d_wv, d_wv + n, d_wv + 2 * n}, n,
+                        SunskyEmitter::Microfacet::GGX, 0.2f, eta, kk, 5, 2, {d_dd, n});
+    HIPCK(hipDeviceSynchronize());
+    std::vector<float> conductor(3 * n), cweights(3 * 2 * n);
+    HIPCK(hipMemcpy(conductor.data(), d_dd, 3 * n * 4, hipMemcpyDeviceToHost));
+    float* d_bw;
+    HIPCK(hipMalloc(&d_bw, 3 * 2 * n * 4));
+    em.direct_conductor_rays({d_nrm, d_nrm + n, d_nrm + 2 * n}, {d_wv, d_wv + n, d_wv + 2 * n}, n,
+                             SunskyEmitter::Microfacet::GGX, 0.2f, 5, 2, {d_er, d_er + 2 * n, d_er + 4 * n},
+                             {d_br, d_br + 2 * n, d_br + 4 * n}, d_bw, eta, kk);
+    HIPCK(hipDeviceSynchronize());
+    HIPCK(hipMemcpy(cweights.data(), d_bw, cweights.size() * 4, hipMemcpyDeviceToHost));
+    (void)hipFree(d_wv); (void)hipFree(d_bw);
     (void)hipFree(d_nrm); (void)hipFree(d_dd); (void)hipFree(d_er); (void)hipFree(d_br); (void)hipFree(d_vis);
 
     std::vector<float> rgb(3 * n), dd(3 * n), pdf(n), w(3 * n), pdf2(n), djv(3 * n);
@@ -150,7 +174,8 @@ static int gpu_mode(const std::string& dir) {
               write_file(dir + "/d.f32", dd) && write_file(dir + "/pdf.f32", pdf) && write_file(dir + "/w.f32", w) &&
               write_file(dir + "/pdf2.f32", pdf2) && write_file(dir + "/drgb_dturbidity.f32", djv) &&
               write_file(dir + "/direct.f32", direct) && write_file(dir + "/occluded.f32", occluded) &&
-              write_file(dir + "/emitter_rays.f32", er) && write_file(dir + "/vis.u8", vis);
+              write_file(dir + "/emitter_rays.f32", er) && write_file(dir + "/vis.u8", vis) &&
+              write_file(dir + "/conductor.f32", conductor) && write_file(dir + "/conductor_weights.f32", cweights);
     for (float* ptr : {d_wi, d_u, d_rgb, d_d, d_pdf, d_w, d_pdf2, d_jv, d_djv}) (void)hipFree(ptr);
     if (!ok) { std::puts("FAIL writing outputs"); return 1; }
     std::printf("gpu ok w_sky=%.9g\n", em.info().sky_sampling_w);

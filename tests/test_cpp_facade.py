@@ -83,6 +83,22 @@ def test_facade_gpu_mode(exe, tmp_path):
     rel = (np.abs(occ - ref) / np.maximum(np.abs(ref), 1e-3 * np.abs(ref).max())).max(axis=0)
     assert np.quantile(rel, 0.995) < 2e-4
     assert occ.mean() < dd.mean()
+    # the rough-conductor vertex through the facade (GGX 0.2, gold-like IOR, seed 5, 2 spp) vs the
+    # oracle's estimator, and its rays' BSDF weights (test_direct_conductor.py's bounds)
+    up = np.tile(np.array([[0, 0, 1]], np.float32), (n, 1))
+    v = np.array([0.3, 0.1, 0.95], np.float32)
+    wv = np.tile(v / np.linalg.norm(v), (n, 1)).astype(np.float32)
+    eta, kk = (0.143, 0.374, 1.442), (3.983, 2.385, 1.603)
+    cd = load("conductor.f32", 3).T
+    ref = O.direct_conductor(o32, up, wv, 0.2, "ggx", eta, kk, 5, 2)
+    rel = (np.abs(cd - ref) / np.maximum(np.abs(ref), 1e-3 * np.abs(ref).max())).max(axis=0)
+    assert np.quantile(rel, 0.995) < 1e-3, np.quantile(rel, [0.5, 0.995, 1.0])
+    _, _, w_o = O.direct_conductor_rays(o32, up, wv, 0.2, "ggx", 5, 2, eta, kk)
+    w_g = np.fromfile(tmp_path / "conductor_weights.f32", dtype=np.float32).reshape(3, 2, n).astype(np.float64)
+    both = w_g.any(axis=0) & w_o.any(axis=0)
+    assert both.mean() > 0.9
+    wr = (np.abs(w_g - w_o) / np.maximum(w_o, 1e-6)).max(axis=0)[both]
+    assert np.quantile(wr, 0.999) < 1e-3
     # eval_jvp through the facade: d eval / d turbidity vs fp64 central differences
     djv = load("drgb_dturbidity.f32", 3)
     h = 1e-3

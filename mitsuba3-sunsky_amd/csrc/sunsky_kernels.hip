@@ -1260,19 +1260,42 @@ __device__ __forceinline__ float spectral_sample_pdf(const SunskyKArgs& K, const
     return fmaf((float)idx + t, K.spec_interval, 360.f);
 }
 
-// sample_wavelengths, sunsky.cpp:463-480 (spectral: 4 shifted samples, Spectrum<Float, 4>)
+// sample_wavelengths, sunsky.cpp:463-480 (spectral: 4 shifted samples, Spectrum<Float, 4>):
+// the 4 wavelengths drawn, then the eval at all 4 and the weights eval / pdf (FAST: times
+// v_rcp_f32 of the pdf).  EVAL4: one branchless eval (eval_spec4, bitwise eval_spec_one per
+// wavelength; ldp in the LdPairs layout), taken by sample_ray (1.26x faster there, interleaved
+// A/B); the standalone sample_wavelengths kernel keeps the rolled eval_spec_one (ld_tab plain),
+// whose 67 VGPRs hold 7 waves/SIMD (eval_spec4: 121 VGPRs, 7 % slower).
 template <bool FAST>
+__device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
+                                           const float* sun_tab, const float* ldp, const DirTerms& t,
+                                           const float lam[4], float e[4]);
+template <bool FAST, bool EVAL4>
 __device__ __forceinline__ void sample_wavelengths_one(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
                                                        const SpecDistLds& D, const float* sun_tab,
-                                                       const float* ld_tab, const DirTerms& t, float sample,
+                                                       const float* ld, const DirTerms& t, float sample,
                                                        float lam[4], float w[4]) {
+    if constexpr (EVAL4) {
+        float lpdf[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        float s = sample + (float)k / 4.f;   // math::sample_shifted, math.h:408-431
-        s = s > 1.f ? s - 1.f : s;
-        float lpdf;
-        lam[k] = spectral_sample_pdf(K, D, s, &lpdf);
-        w[k] = eval_spec_one<FAST>(K, chans, sun_tab, ld_tab, t, lam[k]) / lpdf;
+        for (int k = 0; k < 4; ++k) {
+            float s = sample + (float)k / 4.f;   // math::sample_shifted, math.h:408-431
+            s = s > 1.f ? s - 1.f : s;
+            lam[k] = spectral_sample_pdf(K, D, s, &lpdf[k]);
+        }
+        float e[4];
+        eval_spec4<FAST>(K, chans, sun_tab, ld, t, lam, e);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[k] = fdiv<FAST>(e[k], lpdf[k]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float s = sample + (float)k / 4.f;
+            s = s > 1.f ? s - 1.f : s;
+            float lpdf;
+            lam[k] = spectral_sample_pdf(K, D, s, &lpdf);
+            w[k] = fdiv<FAST>(eval_spec_one<FAST>(K, chans, sun_tab, ld, t, lam[k]), lpdf);
+        }
     }
 }
 
@@ -1893,7 +1916,7 @@ __device__ __forceinline__ void sample_wavelengths_body(const SunskyKArgs& K, co
             DirTerms t = dir_terms<FAST>(K, wo, act);
             add_sun_terms<FAST>(K, t);
             float lam[4], w[4];
-            sample_wavelengths_one<FAST>(K, S.c, D, K.sun_table, K.sun_ld, t, sample[i], lam, w);
+            sample_wavelengths_one<FAST, false>(K, S.c, D, K.sun_table, K.sun_ld, t, sample[i], lam, w);
             for (int k = 0; k < 4; ++k) {
                 lam_out[(size_t)k * lstride + i] = lam[k];
                 weight[(size_t)k * wstride + i] = w[k];
@@ -1941,7 +1964,7 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
             DirTerms t = dir_terms<FAST>(K, wo, act);
             add_sun_terms<FAST>(K, t);
             float lam[4];
-            sample_wavelengths_one<FAST>(K, S.chans.c, S.sdist[0], S.sun, S.ld, t, wls[i], lam, w);
+            sample_wavelengths_one<FAST, true>(K, S.chans.c, S.sdist[0], S.sun, S.ldp, t, wls[i], lam, w);
             for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = lam[k];
             nw = 4;
         }
@@ -1952,8 +1975,9 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
         oy[i] = K.bs_center[1] + (po.y - dw.y) * K.bs_radius;
         oz[i] = K.bs_center[2] + (po.z - dw.z) * K.bs_radius;
         dxo[i] = dw.x; dyo[i] = dw.y; dzo[i] = dw.z;
+        const float inv_pd = fdiv<FAST>(1.f, pd);
         for (int k = 0; k < nw; ++k) {
-            float v = w[k] / pd;
+            float v = FAST ? w[k] * inv_pd : w[k] / pd;
             weight[(size_t)k * wstride + i] = isfinite(v) ? v : 0.f;
         }
     }

@@ -7,6 +7,7 @@
 //   kbench <hsaco> <rgb|spec|sample|pdf> <n> <iters> <blocks_per_cu,...> <kernel> [kernel ...]
 // rgb / spec: eval kernels on uniform upper-hemisphere directions (C2 / C3 emitters);
 // sample / pdf: sample_direction (ds.dist, ds.p not requested) / pdf_direction (C4 emitter);
+// sray / swl: sample_ray / sample_wavelengths (C4 emitter; KB_SAMPLE_SPEC=1 for spectral);
 // conductor: direct_conductor (C4 emitter, GGX alpha 0.2 -- KB_BECKMANN=1 for Beckmann --,
 // gold-like eta / k, 4 spp at random normals and views).
 //
@@ -59,7 +60,8 @@ int main(int argc, char** argv) {
     const bool spec = mode == "spec";
     const bool rays = mode == "rays";   // per-ray spectral eval, 4 random wavelengths per ray (Spectrum<Float, 4>)
     const bool cond = mode == "conductor" || mode == "diffuse";   // the callers (diffuse: the normals only)
-    const bool sampling = mode == "sample" || mode == "pdf" || cond;
+    const bool sray = mode == "sray", swl = mode == "swl";
+    const bool sampling = mode == "sample" || mode == "pdf" || cond || sray || swl;
     const char* pack = std::getenv("SUNSKY_AMD_DATASET");
     std::string pack_path = pack ? pack : "mitsuba3-sunsky_amd/data/sunsky_datasets.pack";
 
@@ -69,7 +71,7 @@ int main(int argc, char** argv) {
     double th = (90.0 - (sampling ? 30.0 : 45.0)) * M_PI / 180.0;
     props.set_vector3("sun_direction", (float)std::sin(th), 0.f, (float)std::cos(th));
     // KB_SAMPLE_SPEC=1 (sample mode): the spectral emitter, 4 random wavelengths per sample
-    const bool sspec = mode == "sample" && std::getenv("KB_SAMPLE_SPEC") != nullptr;
+    const bool sspec = (mode == "sample" || sray || swl) && std::getenv("KB_SAMPLE_SPEC") != nullptr;
     SunskyModel model(props, spec || sspec || rays ? kSpectral : kRGB, kJit, pack_path);
 
     int cu = 0;
@@ -100,7 +102,7 @@ int main(int argc, char** argv) {
     struct ConductorArgs { int type; float alpha; float eta[4], k[4]; };
     ConductorArgs cargs = {std::getenv("KB_BECKMANN") ? 0 : 1, 0.2f, {0.143f, 0.374f, 1.442f, 0.f}, {3.983f, 2.385f, 1.603f, 0.f}};
     float *cnx = nullptr, *cny = nullptr, *cnz = nullptr, *cvx = nullptr, *cvy = nullptr, *cvz = nullptr;
-    if (cond) {
+    if (cond || swl) {
         std::normal_distribution<float> G(0.f, 1.f);
         std::vector<float> h(6 * n);
         for (size_t i = 0; i < n; ++i) {
@@ -108,7 +110,8 @@ int main(int argc, char** argv) {
             float la = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
             float d = a[0] * b[0] + a[1] * b[1] + a[2] * b[2], sg = d < 0 ? -1.f : 1.f;
             float lb = std::sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]);
-            for (int c = 0; c < 3; ++c) { h[c * n + i] = a[c] / la; h[(3 + c) * n + i] = sg * b[c] / lb; }
+            const float sn = swl ? -1.f : 1.f;   // swl: wi = -normal, so wo = -wi faces the sky
+            for (int c = 0; c < 3; ++c) { h[c * n + i] = sn * a[c] / la; h[(3 + c) * n + i] = sg * b[c] / lb; }
         }
         float* buf = nullptr;
         CK(hipMalloc(&buf, 6 * n * 4));
@@ -220,7 +223,18 @@ int main(int argc, char** argv) {
                                  &active, &zero, &n, &out, &ostride};
             void* args_diff[] = {&K, &cnx, &cny, &cnz, &nullf, &nullf, &zero, &nl0, &cseed, &cspp, &active, &zero, &n,
                                  &out, &ostride};
-            void** args = spec ? args_spec : rays ? args_rays : mode == "sample" ? (full ? args_sample_full : args_sample)
+            // sample_ray: wavelength sample = u.x plane, sample2 = (u.x, u.y), sample3 = (u.y, u.x);
+            // outputs o (3 planes of out), d (dd), lambda (lamo), weight (wgt)
+            static float* lamo = nullptr;
+            if ((sray || swl) && !lamo) CK(hipMalloc(&lamo, 4 * n * 4));
+            static float* rayo = nullptr;
+            if (sray && !rayo) CK(hipMalloc(&rayo, 3 * n * 4));
+            float *ryx = rayo, *ryy = rayo ? rayo + n : nullptr, *ryz = rayo ? rayo + 2 * n : nullptr;
+            void* args_sray[] = {&K, &wx, &wx, &wy, &wy, &wx, &active, &n, &ryx, &ryy, &ryz, &dd, &ddy, &ddz, &lamo, &n,
+                                 &wgt, &n};
+            void* args_swl[] = {&K, &cnx, &cny, &cnz, &wx, &active, &n, &lamo, &n, &wgt, &n};
+            void** args = sray ? args_sray : swl ? args_swl : spec ? args_spec : rays ? args_rays
+                                            : mode == "sample" ? (full ? args_sample_full : args_sample)
                                             : mode == "pdf" ? args_pdf : mode == "diffuse" ? args_diff
                                             : cond ? args_cond : args_rgb;
             for (int w = 0; w < 3; ++w) CK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
@@ -239,7 +253,7 @@ int main(int argc, char** argv) {
             double us = 1e3 * ms / iters;
             // checksum against the first kernel
             // sample mode: d (3 planes), pdf and the weight (3 planes) all enter the check
-            const bool samp7 = mode == "sample";
+            const bool samp7 = mode == "sample" || sray;
             std::vector<float> h((size_t)(samp7 ? 7 : nout) * n);
             if (samp7) {
                 CK(hipMemcpy(h.data(), dd, 3 * n * 4, hipMemcpyDeviceToHost));

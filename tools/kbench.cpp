@@ -71,7 +71,7 @@ int main(int argc, char** argv) {
     double th = (90.0 - (sampling ? 30.0 : 45.0)) * M_PI / 180.0;
     props.set_vector3("sun_direction", (float)std::sin(th), 0.f, (float)std::cos(th));
     // KB_SAMPLE_SPEC=1 (sample mode): the spectral emitter, 4 random wavelengths per sample
-    const bool sspec = (mode == "sample" || sray || swl) && std::getenv("KB_SAMPLE_SPEC") != nullptr;
+    const bool sspec = (mode == "sample" || sray || swl || cond) && std::getenv("KB_SAMPLE_SPEC") != nullptr;
     SunskyModel model(props, spec || sspec || rays ? kSpectral : kRGB, kJit, pack_path);
 
     int cu = 0;
@@ -97,7 +97,7 @@ int main(int argc, char** argv) {
         float ct = U(rng), ph = 2.f * (float)M_PI * U(rng), st = std::sqrt(std::max(0.f, 1 - ct * ct));
         hx[i] = -st * std::cos(ph); hy[i] = -st * std::sin(ph); hz[i] = -ct;
     }
-    const int nout = spec ? 11 : rays ? 4 : (mode == "pdf" ? 1 : 3);
+    const int nout = spec ? 11 : (rays || sspec) ? 4 : (mode == "pdf" ? 1 : 3);
     // conductor mode: normals (mostly facing up) and views in their upper hemisphere
     struct ConductorArgs { int type; float alpha; float eta[4], k[4]; };
     ConductorArgs cargs = {std::getenv("KB_BECKMANN") ? 0 : 1, 0.2f, {0.143f, 0.374f, 1.442f, 0.f}, {3.983f, 2.385f, 1.603f, 0.f}};
@@ -219,10 +219,12 @@ int main(int argc, char** argv) {
             void* args_pdf[] = {&K, &dd, &ddy, &ddz, &active, &n, &pdf};
             void* args_rays[] = {&K, &wx, &wy, &wz, &lamp, &n, &nl4, &active, &n, &out, &ostride, &sign};
             uint32_t cseed = 7, cspp = 4;
-            void* args_cond[] = {&K, &cargs, &cnx, &cny, &cnz, &cvx, &cvy, &cvz, &nullf, &zero, &nl0, &cseed, &cspp,
+            void* args_cond[] = {&K, &cargs, &cnx, &cny, &cnz, &cvx, &cvy, &cvz, sspec ? (void*)&lamp : (void*)&nullf,
+                                 sspec ? (void*)&n : (void*)&zero, sspec ? (void*)&nl4 : (void*)&nl0, &cseed, &cspp,
                                  &active, &zero, &n, &out, &ostride};
-            void* args_diff[] = {&K, &cnx, &cny, &cnz, &nullf, &nullf, &zero, &nl0, &cseed, &cspp, &active, &zero, &n,
-                                 &out, &ostride};
+            void* args_diff[] = {&K, &cnx, &cny, &cnz, &nullf, sspec ? (void*)&lamp : (void*)&nullf,
+                                 sspec ? (void*)&n : (void*)&zero, sspec ? (void*)&nl4 : (void*)&nl0, &cseed, &cspp,
+                                 &active, &zero, &n, &out, &ostride};
             // sample_ray: wavelength sample = u.x plane, sample2 = (u.x, u.y), sample3 = (u.y, u.x);
             // outputs o (3 planes of out), d (dd), lambda (lamo), weight (wgt)
             static float* lamo = nullptr;

@@ -84,7 +84,7 @@ enum KernelId {
     K_SAMPLE_WAVELENGTHS_SPEC, K_SAMPLE_RAY_RGB, K_SAMPLE_RAY_SPEC, K_BAKE_RGB, K_BAKE_SPEC,
     K_DIRECT_DIFFUSE_RGB, K_DIRECT_DIFFUSE_SPEC, K_SAMPLE_DIRECTION_RGB_LEAN, K_SAMPLE_DIRECTION_SPEC_LEAN,
     K_DIRECT_DIFFUSE_RAYS, K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN, K_DIRECT_CONDUCTOR_RGB, K_DIRECT_CONDUCTOR_SPEC,
-    K_DIRECT_CONDUCTOR_RAYS, K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED, K_COUNT
+    K_DIRECT_CONDUCTOR_RAYS, K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED, K_SAMPLE_RAY_RGB_SORTED, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
@@ -95,7 +95,7 @@ const char* kKernelNames[K_COUNT] = {
     "sunsky_bake_latlong_rgb", "sunsky_bake_latlong_spec", "sunsky_direct_diffuse_rgb", "sunsky_direct_diffuse_spec",
     "sunsky_sample_direction_rgb_lean", "sunsky_sample_direction_spec_lean", "sunsky_direct_diffuse_rays",
     "sunsky_sample_direction_rgb_lean_plain", "sunsky_direct_conductor_rgb", "sunsky_direct_conductor_spec",
-    "sunsky_direct_conductor_rays", "sunsky_sample_direction_spec_lean4_sorted"};
+    "sunsky_direct_conductor_rays", "sunsky_sample_direction_spec_lean4_sorted", "sunsky_sample_ray_rgb_sorted"};
 
 // eval kernels instantiated twice: eval(si) negates wi at compile time,
 // eval_direction(ds) uses ds.d as is (the "_dir" kernels)
@@ -172,6 +172,7 @@ int blocks_per_cu(KernelId k) {
         case K_SAMPLE_DIRECTION_RGB: case K_SAMPLE_DIRECTION_SPEC: case K_PDF_DIRECTION_V4: case K_PDF_DIRECTION_V1:
         case K_SAMPLE_DIRECTION_RGB_LEAN: case K_SAMPLE_DIRECTION_SPEC_LEAN:
         case K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN: case K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED:
+        case K_SAMPLE_RAY_RGB_SORTED:
             return 64;
         case K_BAKE_RGB: case K_BAKE_SPEC: return 64;
         case K_DIRECT_DIFFUSE_RGB: case K_DIRECT_DIFFUSE_SPEC: case K_DIRECT_DIFFUSE_RAYS: return 64;
@@ -956,8 +957,14 @@ int sunsky_sample_ray(const sunsky_emitter* e, const float* wls, const float* s2
         const SunskyKArgs* K = e->d_state;
         void* args[] = {&K, &wls, &s2x, &s2y, &s3x, &s3y, &active, &n, &o.x, &o.y, &o.z,
                         &d.x, &d.y, &d.z, &lam, &lstride, &weight, &wstride};
-        const KernelId k = e->kargs.variant == kSpectral ? K_SAMPLE_RAY_SPEC : K_SAMPLE_RAY_RGB;
-        launch(e->fn(k), grid_for(e->mod, k, n), (hipStream_t)stream, args);
+        // RGB without a mask: the wave-sorted kernel (one wave per window of 4 x 64 rays);
+        // SUNSKY_AMD_UNSORTED_SAMPLING=1 keeps the unsorted one (A/B, the bitwise test)
+        const char* uns = std::getenv("SUNSKY_AMD_UNSORTED_SAMPLING");
+        const bool unsorted = uns && uns[0] == '1';
+        const KernelId k = e->kargs.variant == kSpectral ? K_SAMPLE_RAY_SPEC
+                           : (!active && !unsorted) ? K_SAMPLE_RAY_RGB_SORTED : K_SAMPLE_RAY_RGB;
+        launch(e->fn(k), grid_for(e->mod, k, k == K_SAMPLE_RAY_RGB_SORTED ? (n + 3) / 4 : n), (hipStream_t)stream,
+               args);
     });
 }
 

@@ -1983,6 +1983,122 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
     }
 }
 
+// RGB sample_ray without a mask in wave-sorted windows (the RGB sample_direction kernel's
+// windows, sample_direction_sorted_body): a wave ranks 64 R rays by their direction sample
+// (sky picks first), runs R passes computing direction, pdf and weight (sample_ray_body's
+// operations in its order) into 6 LDS rows, and un-sorts them; each lane then forms its
+// rays' origins from its own sample2 (prefetched with sample3) and stores everything in ray
+// order.  Bitwise sample_ray_body<FAST, false>.
+template <bool FAST, int R>
+__device__ __forceinline__ void sample_ray_rgb_sorted_body(
+    const SunskyKArgs& K, const float* __restrict__ s2x, const float* __restrict__ s2y,
+    const float* __restrict__ s3x, const float* __restrict__ s3y, size_t n, float* __restrict__ ox,
+    float* __restrict__ oy, float* __restrict__ oz, float* __restrict__ dxo, float* __restrict__ dyo,
+    float* __restrict__ dzo, float* __restrict__ lam_out, size_t lstride, float* __restrict__ weight,
+    size_t wstride) {
+    constexpr int W = 64 * R;
+    __shared__ SamplerLds<FAST, false> S;
+    __shared__ float X[SS_BLOCK / 64][6][W];
+    stage_sampler_lds<FAST, false>(K, &S);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float(*Y)[W] = X[wv];
+    const float inv_w = uniform_f(1.f / K.w_sky), inv_w_sun = uniform_f(1.f / (1.f - K.w_sky));
+    const size_t nwin = (n + W - 1) / W;
+    const size_t wstep = (size_t)gridDim.x * (SS_BLOCK / 64);
+    float na[R], nb[R], nc[R], nd[R];
+    auto load_window = [&](size_t w) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t i = w * W + (size_t)(r * 64 + lane);
+            na[r] = i < n ? s3x[i] : 1.f;   // past the end: a sun pick, computed and not stored
+            nb[r] = i < n ? s3y[i] : 0.5f;
+            nc[r] = i < n ? s2x[i] : 0.5f;
+            nd[r] = i < n ? s2y[i] : 0.5f;
+        }
+    };
+    size_t w = (size_t)blockIdx.x * (SS_BLOCK / 64) + wv;
+    if (w < nwin) load_window(w);
+    for (; w < nwin; w += wstep) {
+        const size_t base = w * W;
+        int slot[R];
+        float c2[R], d2[R];
+        {
+            float a[R], b[R];
+            uint64_t m[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                a[r] = na[r];
+                b[r] = nb[r];
+                c2[r] = nc[r];
+                d2[r] = nd[r];
+            }
+            if (w + wstep < nwin) load_window(w + wstep);
+#pragma unroll
+            for (int r = 0; r < R; ++r) m[r] = __ballot(a[r] < K.w_sky);
+            int psun = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) psun += __popcll(m[r]);
+            int psky = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const bool sky = (m[r] >> lane) & 1;
+                slot[r] = sky ? psky + lanes_below(m[r]) : psun + lanes_below(~m[r]);
+                Y[0][slot[r]] = a[r];
+                Y[1][slot[r]] = b[r];
+                const int c = __popcll(m[r]);
+                psky += c;
+                psun += 64 - c;
+            }
+        }
+        wave_lds_order();
+#pragma unroll 1
+        for (int p = 0; p < R; ++p) {
+            const int q = p * 64 + lane;
+            const float sx = Y[0][q], sy = Y[1][q];
+            const bool pick_sky = sx < K.w_sky;
+            const float3_ d = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
+            const float3_ dw = to_world(K, mk3(-d.x, -d.y, -d.z));
+            bool act = d.z >= 0.f;
+            float skyp, sunp;
+            compute_pdfs<FAST>(K, S.tgmm, d, pick_sky, act, &skyp, &sunp);
+            float pd = lerpf_(sunp, skyp, K.w_sky);
+            pd *= kInvPi * (1.f / (K.bs_radius * K.bs_radius));
+            act = act && pd > 0.f;
+            float e[3];
+            eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, to_local(K, mk3(-dw.x, -dw.y, -dw.z)), act, e, S.rows);
+            const float inv_pd = fdiv<FAST>(1.f, pd);
+            Y[0][q] = dw.x; Y[1][q] = dw.y; Y[2][q] = dw.z;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float v = FAST ? e[k] * inv_pd : e[k] / pd;
+                Y[3 + k][q] = isfinite(v) ? v : 0.f;
+            }
+        }
+        wave_lds_order();
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const size_t i = base + (size_t)(r * 64 + lane);
+            if (i < n) {
+                const float3_ dw = mk3(Y[0][slot[r]], Y[1][slot[r]], Y[2][slot[r]]);
+                float offx, offy;
+                disk_concentric_dev<FAST>(c2[r], d2[r], &offx, &offy);
+                float3_ fs, ft;
+                coordinate_system(dw, &fs, &ft);
+                const float3_ po = frame_to_world(fs, ft, dw, mk3(offx, offy, 0.f));
+                ox[i] = K.bs_center[0] + (po.x - dw.x) * K.bs_radius;
+                oy[i] = K.bs_center[1] + (po.y - dw.y) * K.bs_radius;
+                oz[i] = K.bs_center[2] + (po.z - dw.z) * K.bs_radius;
+                dxo[i] = dw.x; dyo[i] = dw.y; dzo[i] = dw.z;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = 0.f;
+#pragma unroll
+                for (int k = 0; k < 3; ++k) weight[(size_t)k * wstride + i] = Y[3 + k][slot[r]];
+            }
+        }
+        wave_lds_order();
+    }
+}
+
 // ======================================================================
 // Lat-long bake (a caller of eval: sky -> environment map, as the reference's
 // sunsky-testing/sky_data_test.py:58-79 builds an envmap from eval() over
@@ -3292,6 +3408,26 @@ SS_SAMPLE_WAVELENGTHS(sunsky_sample_wavelengths_spec_ref, false, true)
         sample_ray_body<FAST, SPEC>(*Kp, wls, s2x, s2y, s3x, s3y, active, n, ox, oy, oz, dx, dy, dz, lam,        \
                                     lstride, weight, wstride);                                                 \
     }
+#ifndef SS_RAY_SORT_R
+#define SS_RAY_SORT_R 4
+#endif
+// 4 waves/SIMD (125 VGPRs; 131 and 3 waves without): interleaved A/B against the unsorted
+// kernel 0.922 (3 waves 0.976; R = 3: 0.946, at 4 waves 0.955), profiles/r03_v18_ab_sample_ray_sorted.log
+#ifndef SS_RAY_SORTED_ATTR
+#define SS_RAY_SORTED_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+#endif
+#define SS_SAMPLE_RAY_RGB_SORTED(NAME, FAST, R)                                                               \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_RAY_SORTED_ATTR void NAME(                           \
+        const SunskyKArgs* __restrict__ Kp, const float* wls, const float* s2x, const float* s2y, const float* s3x,                 \
+        const float* s3y, const uint8_t* active, size_t n, float* ox, float* oy, float* oz, float* dx,         \
+        float* dy, float* dz, float* lam, size_t lstride, float* weight, size_t wstride) {                     \
+        sample_ray_rgb_sorted_body<FAST, R>(*Kp, s2x, s2y, s3x, s3y, n, ox, oy, oz, dx, dy, dz, lam, lstride,   \
+                                            weight, wstride);                                                  \
+    }
+// RGB sample_ray without a mask (the C ABI's call then): wave-sorted windows, bitwise the
+// unsorted kernel (test_sample_ray_sorted_bitwise_vs_unsorted)
+SS_SAMPLE_RAY_RGB_SORTED(sunsky_sample_ray_rgb_sorted_fast, true, SS_RAY_SORT_R)
+SS_SAMPLE_RAY_RGB_SORTED(sunsky_sample_ray_rgb_sorted_ref, false, SS_RAY_SORT_R)
 SS_SAMPLE_RAY(sunsky_sample_ray_rgb_fast, true, false)
 SS_SAMPLE_RAY(sunsky_sample_ray_rgb_ref, false, false)
 SS_SAMPLE_RAY(sunsky_sample_ray_spec_fast, true, true)

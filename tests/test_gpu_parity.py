@@ -433,6 +433,52 @@ def test_sample_ray_parity(variant):
     assert np.all(np.isfinite(host(w)))
 
 
+@pytest.mark.parametrize("precision", PRECISIONS)
+def test_sample_ray_sorted_bitwise_vs_unsorted(precision, monkeypatch):
+    """RGB sample_ray without a mask runs in wave-sorted windows of 4 x 64 rays (direction
+    samples ranked sky first; origins formed after the un-sort from each ray's own sample2).
+    Against the unsorted kernel (SUNSKY_AMD_UNSORTED_SAMPLING=1) origins, directions,
+    wavelengths and weights are bit for bit the same, and equal the masked call's where the
+    mask is set, for batch sizes ending inside a window, a pass or a lane, all-sky and
+    all-sun windows, samples at and next to w_sky, at 0 and 1 - ulp, and a rotated emitter
+    with a scene bounding sphere."""
+    d = angles_dict(3.0, 1.1, np.deg2rad(60), 0.3, 1.0, 1.0)
+    d["to_world"] = np.array([[0, 0, 1, 0], [1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 0, 1]], np.float64)
+    em = ss.SunskyEmitter(d, "rgb", precision=precision)
+    em.set_scene([-1, -2, -3], [3, 2, 1])
+    w = np.float32(em.sky_sampling_w)
+    rng = np.random.default_rng(13)
+    special = np.array([w, np.nextafter(w, 0, dtype=np.float32), np.nextafter(w, 1, dtype=np.float32), 0.0,
+                        np.nextafter(np.float32(1), 0, dtype=np.float32)], np.float32)
+
+    def run(s2, s3, mask):
+        ray, wt = em.sample_ray(None, None, s2, s3, active=mask)
+        return [host(x).view(np.uint32).copy() for x in (ray.o, ray.d, ray.wavelengths, wt)]
+
+    for n in (1, 5, 63, 64, 65, 255, 256, 257, 1000, 4097, 65537, (1 << 20) + 1):
+        s2 = rng.random((n, 2), dtype=np.float32)
+        s3 = rng.random((n, 2), dtype=np.float32)
+        s3[: min(n, 5), 0] = special[: min(n, 5)]
+        if n >= 2048:
+            s3[256:512, 0] *= w
+            s3[512:768, 0] = w + (1 - w) * s3[512:768, 0]
+        s2t, s3t = soa(s2), soa(s3)
+        mask = torch.from_numpy(rng.random(n) < 0.8).cuda()
+        monkeypatch.delenv("SUNSKY_AMD_UNSORTED_SAMPLING", raising=False)
+        srt = run(s2t, s3t, None)
+        masked = run(s2t, s3t, mask)
+        monkeypatch.setenv("SUNSKY_AMD_UNSORTED_SAMPLING", "1")
+        plain = run(s2t, s3t, None)
+        for a_, b_ in zip(srt, plain):
+            assert np.array_equal(a_, b_), n
+        mk = host(mask)
+        for a_, m_ in zip(srt, masked):
+            if a_.ndim == 1:
+                assert np.array_equal(a_[mk], m_[mk]), n
+            else:
+                assert np.array_equal(a_[:, mk], m_[:, mk]), n
+
+
 # ---------------------------------------------------------------- edge cases
 def test_ragged_sizes_unaligned_and_masks():
     d = angles_dict(3.0, 0.2, np.deg2rad(50), 0.3, 1.0, 1.0)

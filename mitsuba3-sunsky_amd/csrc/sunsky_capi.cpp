@@ -178,6 +178,9 @@ int blocks_per_cu(KernelId k) {
         case K_DIRECT_DIFFUSE_RGB: case K_DIRECT_DIFFUSE_SPEC: case K_DIRECT_DIFFUSE_RAYS: return 64;
         case K_DIRECT_CONDUCTOR_RGB: case K_DIRECT_CONDUCTOR_SPEC: case K_DIRECT_CONDUCTOR_RAYS: return 64;
         case K_EVAL_SPEC_RAYS_V4: case K_EVAL_SPEC_RAYS_V1: return 64;
+        // kbench sweep over 8/16/32/64 (profiles/r03_v18_kbench_grid_ray_wavelengths.log)
+        case K_SAMPLE_RAY_RGB: case K_SAMPLE_RAY_SPEC: return 32;
+        case K_SAMPLE_WAVELENGTHS_SPEC: return 64;
         default: return 16;
     }
 }

@@ -156,6 +156,15 @@ def valu_floor(kernel):
             "issue_floor_ms": rec["valu_issue_floor_ms"], "source": os.path.relpath(files[-1], ROOT)}
 
 
+def valu_frac(floor, ms, clk_mhz=None):
+    """`floor` (valu_floor) against a measured launch time: frac at the nominal 2.4 GHz, and
+    frac_at_gfxclk with the floor rescaled to the clock sampled during the launches."""
+    out = dict(floor, achieved_ms=ms, frac=floor["issue_floor_ms"] / ms)
+    if clk_mhz:
+        out["frac_at_gfxclk"] = floor["issue_floor_ms"] * (2400.0 / clk_mhz) / ms
+    return out
+
+
 def sclk_under_valu_load(dev):
     """GFX clock (MHz, amd-smi through torch.cuda.clock_rate) sampled while every SIMD runs
     independent FMA chains (tools/clock_probe.hip, built by build(); ~0.3 s of load): the
@@ -793,10 +802,10 @@ def main():
             if sem == "jit" and vs and vp:
                 sec[key]["valu_roofline"] = {
                     "bound": "valu", "unit": "ms",
-                    "sample_direction": dict(vs, achieved_ms=ms_s, frac=vs["issue_floor_ms"] / ms_s),
-                    "pdf_direction": dict(vp, achieved_ms=ms_p, frac=vp["issue_floor_ms"] / ms_p),
+                    "sample_direction": valu_frac(vs, ms_s, clk_s),
+                    "pdf_direction": valu_frac(vp, ms_p),
                     "note": "frac = VALU-issue floor (PMC instruction counts x issue cycles / (1024 SIMDs x 2.4 GHz)) "
-                            "/ measured launch time; HBM frac of the same launches is achieved_GBps / 8000"}
+                            "/ measured launch time (frac_at_gfxclk: the floor at the sampled clock); HBM frac of the same launches is achieved_GBps / 8000"}
             if rank == 0:
                 sec[key]["parity"] = parity_c4(smp_s, dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), u, d,
                                                pdf_s, wgt, pdf_q, semantics=sem)
@@ -881,9 +890,9 @@ def main():
         vss = valu_floor("sunsky_sample_direction_spec_lean4_sorted_" + kfx)
         if vss:
             sec["sampling_C4_spectral_4lambda"]["valu_roofline"] = {
-                "bound": "valu", "unit": "ms", "sample_direction": dict(vss, achieved_ms=ms_ss, frac=vss["issue_floor_ms"] / ms_ss),
+                "bound": "valu", "unit": "ms", "sample_direction": valu_frac(vss, ms_ss, clk_ss),
                 "note": "frac = VALU-issue floor (PMC instruction counts x issue cycles / (1024 SIMDs x 2.4 GHz)) / "
-                        "measured launch time"}
+                        "measured launch time (frac_at_gfxclk: the floor at the sampled clock)"}
         if rank == 0:
             sec["sampling_C4_spectral_4lambda"]["parity"] = parity_c4(
                 smp_sp, dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), u_sp, d_sp, p_sp, w_sp, q_sp, lam=lam_sp)

@@ -432,38 +432,65 @@ __device__ __forceinline__ float render_sun_rgb_compact(const float* table, int 
 }
 
 // RGB sun-table segments [K.sun_row_lo, K.sun_row_lo + kSunRowsStaged) in LDS with
-// the three channels interleaved: r[row][k][j] = (S[c=0], S[c=1], S[c=2], 0) of
-// render_sun's 45x3x4x6 table.  One 16-byte LDS read feeds all three channels'
-// FMAs, in the same Horner order per channel as render_sun_rgb_compact (bitwise
-// the same values).
+// per (row, k) the 18 values S[c][k][j] of render_sun's 45x3x4x6 table: channels 0 and 1
+// interleaved at 2 j + c (the pairs a packed FMA takes), channel 2 at 12 + j, padded to
+// 20 floats (five 16-byte slots).  One k step reads them as 4 ds_read_b128 + 1
+// ds_read_b64 (18 LDS-array cycles) instead of 6 12-byte reads of padded (S0, S1, S2, 0)
+// rows (48 cycles: ds_read_b96 services 8 lanes per cycle).  Same Horner order per
+// channel as render_sun_rgb_compact (bitwise the same values).
+constexpr int kSunRowFloats = 20;
+#ifndef SS_SUN_ROWS_LDS   // probe builds: rows held in LDS (<= kSunRowsStaged; lanes past them read the table)
+#define SS_SUN_ROWS_LDS kSunRowsStaged
+#endif
+constexpr int kSunRowsLds = SS_SUN_ROWS_LDS;
+static_assert(kSunRowsLds <= kSunRowsStaged, "LDS rows");
 struct SunRowsRgb {
-    float4 r[kSunRowsStaged][kNbSunCtrlPts][kNbSunLdParams];
+    float4 r[kSunRowsLds][kNbSunCtrlPts][kSunRowFloats / 4];
 };
 
 __device__ __forceinline__ void stage_sun_rows(const SunskyKArgs& K, SunRowsRgb* s) {
     constexpr int per_row = kNbSunCtrlPts * kNbSunLdParams;
-    for (int e = threadIdx.x; e < kSunRowsStaged * per_row; e += blockDim.x) {
-        const int row = e / per_row, kj = e % per_row;
+    constexpr int per_k = kSunRowFloats;
+    float* dst = reinterpret_cast<float*>(s->r);
+    for (int e = threadIdx.x; e < kSunRowsLds * kNbSunCtrlPts * per_k; e += blockDim.x) {
+        const int row = e / (kNbSunCtrlPts * per_k), k = (e / per_k) % kNbSunCtrlPts, f = e % per_k;
         const int pos = min(K.sun_row_lo + row, kNbSunSegments - 1);
-        const float* src = K.sun_table + pos * 3 * per_row + kj;
-        reinterpret_cast<float4*>(s->r)[e] = make_float4(src[0], src[per_row], src[2 * per_row], 0.f);
+        const int j = f < 12 ? f >> 1 : f - 12, c = f < 12 ? f & 1 : 2;
+        dst[e] = j < kNbSunLdParams ? K.sun_table[pos * 3 * per_row + c * per_row + k * kNbSunLdParams + j] : 0.f;
     }
 }
 
 __device__ __forceinline__ void render_sun_rgb_rows(const SunRowsRgb& R, int row, float x, float cpsi,
                                                     float out[3]) {
+    static_assert(kNbSunLdParams == 6 && kSunRowFloats == 20, "row slots: 12 pair values, 6 channel-2 values, 2 pad");
     float r0 = 0.f, r1 = 0.f, r2 = 0.f;
 #pragma unroll 1
     for (int k = kNbSunCtrlPts - 1; k >= 0; --k) {
         const float4* q = R.r[row][k];
-        const float4 a = q[kNbSunLdParams - 1];
-        float i0 = a.x, i1 = a.y, i2 = a.z;
+        float v[kSunRowFloats];
+        constexpr int J = kNbSunLdParams - 1;
 #pragma unroll
-        for (int j = kNbSunLdParams - 2; j >= 0; --j) {
-            const float4 b = q[j];
-            i0 = fmaf(i0, cpsi, b.x);
-            i1 = fmaf(i1, cpsi, b.y);
-            i2 = fmaf(i2, cpsi, b.z);
+        for (int i = 3; i < kSunRowFloats / 4; ++i) {
+            const float4 b = q[i];
+            v[4 * i] = b.x; v[4 * i + 1] = b.y; v[4 * i + 2] = b.z; v[4 * i + 3] = b.w;
+        }
+        float i2 = v[12 + J];
+#pragma unroll
+        for (int j = J - 1; j >= 0; --j) i2 = fmaf(i2, cpsi, v[12 + j]);
+        // Channel 2 first, then the pairs, with the scheduler held between them: without the
+        // barrier it hoists all five reads (and more around them) and the callers' register
+        // peaks rise (direct_conductor 0 -> 19 spilled VGPRs, the sorted sampler 96 -> 111).
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const float4 b = q[i];
+            v[4 * i] = b.x; v[4 * i + 1] = b.y; v[4 * i + 2] = b.z; v[4 * i + 3] = b.w;
+        }
+        float i0 = v[2 * J], i1 = v[2 * J + 1];
+#pragma unroll
+        for (int j = J - 1; j >= 0; --j) {
+            i0 = fmaf(i0, cpsi, v[2 * j]);
+            i1 = fmaf(i1, cpsi, v[2 * j + 1]);
         }
         r0 = fmaf(r0, x, i0);
         r1 = fmaf(r1, x, i1);
@@ -491,7 +518,7 @@ __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const typen
         if (t.hit_sun) {
             add_sun_terms<true>(K, t);
             const int row = t.sun_pos - K.sun_row_lo;
-            if (rows && row >= 0 && row < kSunRowsStaged) {
+            if (rows && row >= 0 && row < kSunRowsLds) {
                 float sr[3];
                 render_sun_rgb_rows(*rows, row, t.sun_x, t.sun_cpsi, sr);
 #pragma unroll

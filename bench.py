@@ -671,10 +671,10 @@ def main():
         # caller: 8192 x 4096 lat-long RGB bake of the sky (write-only, 12 B per pixel)
         bw, bh = 8192, 4096
         bake_out = torch.empty((3, bh, bw), dtype=torch.float32, device=dev)
-        for _ in range(2):
+        for _ in range(5):
             ems[0].bake_latlong(bw, bh, out=bake_out)
         tm = KernelTimer()
-        reps = max(3, args.steps // 4)
+        reps = max(10, args.steps // 4)
         tm.begin()
         for _ in range(reps):
             ems[0].bake_latlong(bw, bh, out=bake_out)
@@ -691,7 +691,7 @@ def main():
         grad = ems[0].eval_vjp(si_v, d_out)[0]
         ems[0].eval_vjp(si_v, d_out, grad=grad)
         tm = KernelTimer()
-        reps = max(3, args.steps // 4)
+        reps = max(10, args.steps // 4)
         tm.begin()
         for _ in range(reps):
             ems[0].eval_vjp(si_v, d_out, grad=grad)
@@ -706,10 +706,10 @@ def main():
         spec = ss.SunskyEmitter(dict(sun_dict(3.0), albedo=0.3), "spectral", precision=args.precision, device=dev)
         lams = [float(x) for x in range(320, 721, 40)]
         spec_out = torch.empty((11, n), dtype=torch.float32, device=dev)
-        for _ in range(2):
+        for _ in range(5):
             spec.eval_spectral_broadcast(wi, lams, out=spec_out)
         tm = KernelTimer()
-        reps = max(3, args.steps // 4)
+        reps = max(10, args.steps // 4)
         tm.begin()
         for _ in range(reps):
             spec.eval_spectral_broadcast(wi, lams, out=spec_out)
@@ -731,10 +731,10 @@ def main():
             if rc:
                 raise RuntimeError(lib.sunsky_last_error().decode())
 
-        for _ in range(2):
+        for _ in range(5):
             rays_step()
         tm = KernelTimer()
-        reps = max(3, args.steps // 4)
+        reps = max(10, args.steps // 4)
         tm.begin()
         for _ in range(reps):
             rays_step()
@@ -775,10 +775,10 @@ def main():
                 if rc:
                     raise RuntimeError(lib.sunsky_last_error().decode())
 
-            for _ in range(2):
+            for _ in range(5):
                 sample_step()
                 pdf_step()
-            reps = max(3, args.steps // 4)
+            reps = max(10, args.steps // 4)
             t_s, t_p = KernelTimer(), KernelTimer()
             t_s.begin()
             for _ in range(reps):
@@ -868,8 +868,9 @@ def main():
             if rc:
                 raise RuntimeError(lib.sunsky_last_error().decode())
 
-        spec_sample_step()
-        spec_pdf_step()
+        for _ in range(5):
+            spec_sample_step()
+            spec_pdf_step()
         t_ss, t_sq = KernelTimer(), KernelTimer()
         t_ss.begin()
         for _ in range(reps):
@@ -913,7 +914,8 @@ def main():
             if rc:
                 raise RuntimeError(lib.sunsky_last_error().decode())
 
-        direct_step()
+        for _ in range(5):
+            direct_step()
         t_d = KernelTimer()
         t_d.begin()
         for _ in range(reps):
@@ -940,7 +942,8 @@ def main():
             if rc:
                 raise RuntimeError(lib.sunsky_last_error().decode())
 
-        conductor_step()
+        for _ in range(5):
+            conductor_step()
         t_c = KernelTimer()
         t_c.begin()
         for _ in range(reps):

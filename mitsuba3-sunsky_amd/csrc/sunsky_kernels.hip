@@ -1754,14 +1754,16 @@ __device__ __forceinline__ void sample_direction_sorted_body(
     const float inv_w = uniform_f(1.f / K.w_sky), inv_w_sun = uniform_f(1.f / (1.f - K.w_sky));
     const size_t nwin = (n + W - 1) / W;
     const size_t wstep = (size_t)gridDim.x * (SS_BLOCK / 64);
-    // the next window's u is loaded before this window's passes (its HBM latency overlaps them)
-    float na[R], nb[R];
+    // the next window's u (FULL: and mask) is loaded before this window's passes (its HBM
+    // latency overlaps them)
+    float na[R], nb[R], nm[R];
     auto load_window = [&](size_t w) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const size_t i = w * W + (size_t)(r * 64 + lane);
             na[r] = i < n ? ux[i] : 1.f;   // past the end: a sun pick, computed and not stored
             nb[r] = i < n ? uy[i] : 0.5f;
+            if (FULL && active) nm[r] = (i < n && active[i] != 0) ? 1.f : 0.f;
         }
     };
     size_t w = (size_t)blockIdx.x * (SS_BLOCK / 64) + wv;
@@ -1790,13 +1792,22 @@ __device__ __forceinline__ void sample_direction_sorted_body(
                 slot[r] = sky ? psky + lanes_below(m[r]) : psun + lanes_below(~m[r]);
                 Y[0][slot[r]] = a[r];
                 Y[1][slot[r]] = b[r];
-                if (FULL && active) {
-                    const size_t i = base + (size_t)(r * 64 + lane);
-                    Y[2][slot[r]] = (i < n && active[i] != 0) ? 1.f : 0.f;
-                }
+                if (FULL && active) Y[2][slot[r]] = nm[r];
                 const int c = __popcll(m[r]);
                 psky += c;
                 psun += 64 - c;
+            }
+        }
+        // FULL: this window's it.p, loaded before the passes and consumed after them
+        float ipx[FULL ? R : 1], ipy[FULL ? R : 1], ipz[FULL ? R : 1];
+        if constexpr (FULL) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const size_t i = base + (size_t)(r * 64 + lane);
+                const bool in = (dist || opx) && i < n;
+                ipx[r] = in && px ? px[i] : 0.f;
+                ipy[r] = in && py ? py[i] : 0.f;
+                ipz[r] = in && pz ? pz[i] : 0.f;
             }
         }
         wave_lds_order();
@@ -1819,7 +1830,7 @@ __device__ __forceinline__ void sample_direction_sorted_body(
                 for (int k = 0; k < 7; ++k) store_nt(Y[k][slot[r]], planes[k] + i);
                 if (FULL && (dist || opx)) {   // as sample_direction_body: ds.dist, ds.p (sunsky.cpp:417-420)
                     const float3_ d = mk3(Y[0][slot[r]], Y[1][slot[r]], Y[2][slot[r]]);
-                    float3_ itp = mk3(px ? px[i] : 0.f, py ? py[i] : 0.f, pz ? pz[i] : 0.f);
+                    float3_ itp = mk3(ipx[FULL ? r : 0], ipy[FULL ? r : 0], ipz[FULL ? r : 0]);
                     float3_ rel = mk3(itp.x - K.bs_center[0], itp.y - K.bs_center[1], itp.z - K.bs_center[2]);
                     float dd = 2.f * fmaxf(K.bs_radius, sqrtf(dot3(rel, rel)));
                     if (dist) dist[i] = dd;
@@ -3419,8 +3430,10 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_loop_fast, true, true, tru
 SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_fast, true, SS_SORT_R, false)
 SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_ref, false, SS_SORT_R, false)
 // The general call (it.p, ds.dist, ds.p, mask) in the same windows: bitwise the unsorted kernel
-// (test_wave_sorted_rgb_kernels_bitwise_vs_unsorted) but 2 % slower (125 VGPRs and 28 SGPR spills,
-// 4 waves/SIMD; profiles/r02_v13_ab_sample_full.log), so the C ABI keeps the unsorted general kernel.
+// (test_wave_sorted_rgb_kernels_bitwise_vs_unsorted) but slower: 2 % in round 2 (125 VGPRs and 28
+// SGPR spills, profiles/r02_v13_ab_sample_full.log), 14 % against the round-3 unsorted general kernel,
+// 10 % with the mask and it.p prefetched (114 VGPRs, 42 SGPR spills;
+// profiles/r03_v23_ab_sample_full.log), so the C ABI keeps the unsorted general kernel.
 SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_full_sorted_fast, true, 4, true)
 
 

@@ -42,8 +42,9 @@
 extern "C" {
 #endif
 
-#define SUNSKY_AMD_ABI_VERSION 4   /* 3: direct_diffuse visibility, direct_diffuse_rays; 4: direct_conductor(_rays),
-                                     emitter_tangent_tables, direct_diffuse draws sample_1 (path.cpp:233) */
+#define SUNSKY_AMD_ABI_VERSION 5   /* 3: direct_diffuse visibility, direct_diffuse_rays; 4: direct_conductor(_rays),
+                                     emitter_tangent_tables, direct_diffuse draws sample_1 (path.cpp:233);
+                                     5: direct_conductor(_rays)_aniso (alpha_u, alpha_v) */
 
 typedef enum sunsky_status {
     SUNSKY_OK = 0,
@@ -262,7 +263,7 @@ int sunsky_direct_diffuse_rays(const sunsky_emitter *e, sunsky_vec3_in normal, u
                                size_t ray_stride, void *stream);
 
 /* A caller with a glossy vertex: the light a rough conductor (src/bsdfs/roughconductor.cpp,
- * isotropic Beckmann or GGX, visible-normal sampling, include/mitsuba/render/microfacet.h)
+ * Beckmann or GGX, visible-normal sampling, include/mitsuba/render/microfacet.h)
  * reflects towards wi, gathered as path.cpp:176-250 does at one vertex: per sample the
  * emitter sample (next_2d) weighted by f cos / pdf and the power heuristic, sample_1
  * (next_1d, unused by this BSDF), then the BSDF sample (next_2d): reflected direction,
@@ -289,6 +290,21 @@ int sunsky_direct_conductor_rays(const sunsky_emitter *e, sunsky_vec3_in normal,
                                  int distribution, float alpha, const float *eta, const float *k, uint32_t seed,
                                  uint32_t spp, size_t n, sunsky_vec3_out emitter_dir, sunsky_vec3_out bsdf_dir,
                                  float *bsdf_weight, size_t ray_stride, void *stream);
+/* The same two calls with an anisotropic distribution: roughconductor's alpha_u / alpha_v
+ * (microfacet.h:92-95, eval :186-207, smith_g1 :330-354, the visible-normal stretch
+ * :301-316), alpha_u along the shading frame's first tangent (coordinate_system(normal),
+ * include/mitsuba/core/vector.h:116-137) and alpha_v along the second; each clamped to
+ * 1e-4.  alpha_u == alpha_v gives the isotropic calls' results bit for bit. */
+int sunsky_direct_conductor_aniso(const sunsky_emitter *e, sunsky_vec3_in normal, sunsky_vec3_in wi,
+                                  int distribution, float alpha_u, float alpha_v, const float *eta, const float *k,
+                                  const float *wavelengths, int n_wavelengths, size_t wl_stride, uint32_t seed,
+                                  uint32_t spp, const uint8_t *visibility, size_t vis_stride, size_t n, float *out,
+                                  size_t out_stride, void *stream);
+int sunsky_direct_conductor_rays_aniso(const sunsky_emitter *e, sunsky_vec3_in normal, sunsky_vec3_in wi,
+                                       int distribution, float alpha_u, float alpha_v, const float *eta,
+                                       const float *k, uint32_t seed, uint32_t spp, size_t n,
+                                       sunsky_vec3_out emitter_dir, sunsky_vec3_out bsdf_dir, float *bsdf_weight,
+                                       size_t ray_stride, void *stream);
 
 /* ------------------------------------------------ forward-mode derivatives */
 typedef enum sunsky_param {         /* Differentiable traverse() parameters, sunsky.cpp:220-240 */

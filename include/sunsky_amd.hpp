@@ -228,7 +228,8 @@ public:
                                          ray_stride ? ray_stride : n, stream));
     }
     // The same vertex at rough-conductor points (sunsky_direct_conductor): roughconductor.cpp with
-    // an isotropic Beckmann / GGX distribution and visible-normal sampling.  wi: the points'
+    // a Beckmann / GGX distribution and visible-normal sampling (isotropic alpha, or alpha_u /
+    // alpha_v through the _aniso forms).  wi: the points'
     // si.wi in world space; eta / k: complex IOR per RGB channel (spectral: the first).
     enum class Microfacet { Beckmann = SUNSKY_MICROFACET_BECKMANN, GGX = SUNSKY_MICROFACET_GGX };
     void direct_conductor(Vector3 normal, Vector3 wi, size_t n, Microfacet distribution, float alpha,
@@ -240,6 +241,16 @@ public:
                                       visibility, vis_stride ? vis_stride : n, n, out.data,
                                       out.stride ? out.stride : n, stream));
     }
+    void direct_conductor_aniso(Vector3 normal, Vector3 wi, size_t n, Microfacet distribution, float alpha_u,
+                                float alpha_v, const float eta[3], const float k[3], uint32_t seed, uint32_t spp,
+                                SpectrumOut out, Wavelengths wavelengths = {}, void* stream = nullptr,
+                                const uint8_t* visibility = nullptr, size_t vis_stride = 0) const {
+        check(sunsky_direct_conductor_aniso(e_, vin(normal), vin(wi), (int)distribution, alpha_u, alpha_v, eta, k,
+                                            wavelengths.data, wavelengths.count,
+                                            wavelengths.stride ? wavelengths.stride : n, seed, spp, visibility,
+                                            vis_stride ? vis_stride : n, n, out.data, out.stride ? out.stride : n,
+                                            stream));
+    }
     // Its shadow and BSDF rays, and (bsdf_weight not null) the BSDF samples' weights F G1 per
     // channel at bsdf_weight[(c * spp + s) * ray_stride + i] (c < 3 RGB, c < 1 spectral).
     void direct_conductor_rays(Vector3 normal, Vector3 wi, size_t n, Microfacet distribution, float alpha,
@@ -249,6 +260,15 @@ public:
         check(sunsky_direct_conductor_rays(e_, vin(normal), vin(wi), (int)distribution, alpha, eta, k, seed, spp, n,
                                            vout(emitter_dir), vout(bsdf_dir), bsdf_weight,
                                            ray_stride ? ray_stride : n, stream));
+    }
+    void direct_conductor_rays_aniso(Vector3 normal, Vector3 wi, size_t n, Microfacet distribution, float alpha_u,
+                                     float alpha_v, uint32_t seed, uint32_t spp, Vector3Out emitter_dir,
+                                     Vector3Out bsdf_dir, float* bsdf_weight = nullptr, const float eta[3] = nullptr,
+                                     const float k[3] = nullptr, size_t ray_stride = 0,
+                                     void* stream = nullptr) const {
+        check(sunsky_direct_conductor_rays_aniso(e_, vin(normal), vin(wi), (int)distribution, alpha_u, alpha_v, eta, k,
+                                                 seed, spp, n, vout(emitter_dir), vout(bsdf_dir), bsdf_weight,
+                                                 ray_stride ? ray_stride : n, stream));
     }
     // Spectral eval of one wavelength list broadcast to every ray (test_sunsky.py:42-59 layout)
     void eval_spectral_broadcast(Vector3 wi, size_t n, const std::vector<float>& wavelengths, SpectrumOut out,

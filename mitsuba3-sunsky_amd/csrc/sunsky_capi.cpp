@@ -1243,36 +1243,41 @@ int sunsky_direct_diffuse_rays(const sunsky_emitter* e, sunsky_vec3_in nrm, uint
     });
 }
 
-// The rough conductor of the glossy caller (mirrors the kernel-side ConductorArgs)
+// The rough conductor of the glossy caller (mirrors the kernel-side ConductorArgs; alpha_v
+// after the IOR so the isotropic layout's offsets stay)
 struct ConductorArgs {
     int type;
-    float alpha;
+    float alpha_u;
     float eta[4], k[4];
+    float alpha_v;
 };
+static_assert(sizeof(ConductorArgs) == 44 && offsetof(ConductorArgs, alpha_v) == 40, "ConductorArgs layout");
 
-static int conductor_args(const sunsky_emitter* e, int distribution, float alpha, const float* eta, const float* k,
-                          ConductorArgs* c) {
+static int conductor_args(const sunsky_emitter* e, int distribution, float alpha_u, float alpha_v, const float* eta,
+                          const float* k, ConductorArgs* c) {
     if (distribution != SUNSKY_MICROFACET_BECKMANN && distribution != SUNSKY_MICROFACET_GGX)
         return fail(SUNSKY_ERROR_INVALID_VALUE, "distribution must be SUNSKY_MICROFACET_BECKMANN or _GGX");
-    if (!(alpha > 0.f)) return fail(SUNSKY_ERROR_INVALID_VALUE, "alpha must be > 0");
+    if (!(alpha_u > 0.f) || !(alpha_v > 0.f) || std::isinf(alpha_u) || std::isinf(alpha_v))
+        return fail(SUNSKY_ERROR_INVALID_VALUE, "alpha (alpha_u, alpha_v) must be finite and > 0");
     if (!eta || !k) return fail(SUNSKY_ERROR_INVALID_VALUE, "null eta / k");
     std::memset(c, 0, sizeof(*c));
     c->type = distribution;
-    // microfacet.h clamps alpha to 1e-4 (MicrofacetDistribution::configure)
-    c->alpha = std::max(alpha, 1e-4f);
+    // microfacet.h clamps alpha_u, alpha_v to 1e-4 (MicrofacetDistribution::configure, :424-428)
+    c->alpha_u = std::max(alpha_u, 1e-4f);
+    c->alpha_v = std::max(alpha_v, 1e-4f);
     const int nc = e->kargs.variant == kSpectral ? 1 : 3;
     for (int i = 0; i < nc; ++i) { c->eta[i] = eta[i]; c->k[i] = k[i]; }
     return SUNSKY_OK;
 }
 
-int sunsky_direct_conductor(const sunsky_emitter* e, sunsky_vec3_in nrm, sunsky_vec3_in wi, int distribution,
-                            float alpha, const float* eta, const float* k, const float* lam, int nlam, size_t lstride,
-                            uint32_t seed, uint32_t spp, const uint8_t* vis, size_t vstride, size_t n, float* out,
-                            size_t ostride, void* stream) {
+static int direct_conductor_impl(const sunsky_emitter* e, sunsky_vec3_in nrm, sunsky_vec3_in wi, int distribution,
+                                 float alpha_u, float alpha_v, const float* eta, const float* k, const float* lam,
+                                 int nlam, size_t lstride, uint32_t seed, uint32_t spp, const uint8_t* vis,
+                                 size_t vstride, size_t n, float* out, size_t ostride, void* stream) {
     SUNSKY_PHASE("SamplingIntegratorSample", "direct_conductor");
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     ConductorArgs C;
-    int rc = conductor_args(e, distribution, alpha, eta, k, &C);
+    int rc = conductor_args(e, distribution, alpha_u, alpha_v, eta, k, &C);
     if (rc != SUNSKY_OK) return rc;
     if (n == 0) return SUNSKY_OK;
     const bool spec = e->kargs.variant == kSpectral;
@@ -1297,16 +1302,17 @@ int sunsky_direct_conductor(const sunsky_emitter* e, sunsky_vec3_in nrm, sunsky_
     });
 }
 
-int sunsky_direct_conductor_rays(const sunsky_emitter* e, sunsky_vec3_in nrm, sunsky_vec3_in wi, int distribution,
-                                 float alpha, const float* eta, const float* k, uint32_t seed, uint32_t spp, size_t n,
-                                 sunsky_vec3_out em, sunsky_vec3_out bs, float* bw, size_t rstride, void* stream) {
+static int direct_conductor_rays_impl(const sunsky_emitter* e, sunsky_vec3_in nrm, sunsky_vec3_in wi,
+                                      int distribution, float alpha_u, float alpha_v, const float* eta, const float* k,
+                                      uint32_t seed, uint32_t spp, size_t n, sunsky_vec3_out em, sunsky_vec3_out bs,
+                                      float* bw, size_t rstride, void* stream) {
     SUNSKY_PHASE("SamplingIntegratorSample", "direct_conductor_rays");
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     if (bw && (!eta || !k)) return fail(SUNSKY_ERROR_INVALID_VALUE, "the BSDF weights need eta / k");
     const float one[3] = {1.f, 1.f, 1.f};
     ConductorArgs C;
     // the directions do not depend on eta / k; the weights do
-    int rc = conductor_args(e, distribution, alpha, bw ? eta : one, bw ? k : one, &C);
+    int rc = conductor_args(e, distribution, alpha_u, alpha_v, bw ? eta : one, bw ? k : one, &C);
     if (rc != SUNSKY_OK) return rc;
     int nw = e->kargs.variant == kSpectral ? 1 : 3;
     if (n == 0) return SUNSKY_OK;
@@ -1324,6 +1330,37 @@ int sunsky_direct_conductor_rays(const sunsky_emitter* e, sunsky_vec3_in nrm, su
                         &seed, &spp, &n, &em.x, &em.y, &em.z, &bs.x, &bs.y, &bs.z, &rstride, &bw, &nw};
         launch(e->fn(K_DIRECT_CONDUCTOR_RAYS), grid_for(e->mod, K_DIRECT_CONDUCTOR_RAYS, n), (hipStream_t)stream, args);
     });
+}
+
+int sunsky_direct_conductor(const sunsky_emitter* e, sunsky_vec3_in nrm, sunsky_vec3_in wi, int distribution,
+                            float alpha, const float* eta, const float* k, const float* lam, int nlam, size_t lstride,
+                            uint32_t seed, uint32_t spp, const uint8_t* vis, size_t vstride, size_t n, float* out,
+                            size_t ostride, void* stream) {
+    return direct_conductor_impl(e, nrm, wi, distribution, alpha, alpha, eta, k, lam, nlam, lstride, seed, spp, vis,
+                                 vstride, n, out, ostride, stream);
+}
+
+int sunsky_direct_conductor_aniso(const sunsky_emitter* e, sunsky_vec3_in nrm, sunsky_vec3_in wi, int distribution,
+                                  float alpha_u, float alpha_v, const float* eta, const float* k, const float* lam,
+                                  int nlam, size_t lstride, uint32_t seed, uint32_t spp, const uint8_t* vis,
+                                  size_t vstride, size_t n, float* out, size_t ostride, void* stream) {
+    return direct_conductor_impl(e, nrm, wi, distribution, alpha_u, alpha_v, eta, k, lam, nlam, lstride, seed, spp,
+                                 vis, vstride, n, out, ostride, stream);
+}
+
+int sunsky_direct_conductor_rays(const sunsky_emitter* e, sunsky_vec3_in nrm, sunsky_vec3_in wi, int distribution,
+                                 float alpha, const float* eta, const float* k, uint32_t seed, uint32_t spp, size_t n,
+                                 sunsky_vec3_out em, sunsky_vec3_out bs, float* bw, size_t rstride, void* stream) {
+    return direct_conductor_rays_impl(e, nrm, wi, distribution, alpha, alpha, eta, k, seed, spp, n, em, bs, bw, rstride,
+                                      stream);
+}
+
+int sunsky_direct_conductor_rays_aniso(const sunsky_emitter* e, sunsky_vec3_in nrm, sunsky_vec3_in wi,
+                                       int distribution, float alpha_u, float alpha_v, const float* eta,
+                                       const float* k, uint32_t seed, uint32_t spp, size_t n, sunsky_vec3_out em,
+                                       sunsky_vec3_out bs, float* bw, size_t rstride, void* stream) {
+    return direct_conductor_rays_impl(e, nrm, wi, distribution, alpha_u, alpha_v, eta, k, seed, spp, n, em, bs, bw,
+                                      rstride, stream);
 }
 
 int sunsky_sample_position(const sunsky_emitter* e) {

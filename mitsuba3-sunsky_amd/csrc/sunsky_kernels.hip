@@ -2366,25 +2366,27 @@ __device__ __forceinline__ void direct_diffuse_body(
 }
 
 // ======================================================================
-// Caller with a glossy vertex: the rough conductor (src/bsdfs/roughconductor.cpp) with an
-// isotropic Beckmann or GGX microfacet distribution and visible-normal sampling
-// (include/mitsuba/render/microfacet.h), the default Mitsuba configuration.  All in the
-// point's shading frame Frame3f(n) (coordinate_system), fp32 with the libm functions.
+// Caller with a glossy vertex: the rough conductor (src/bsdfs/roughconductor.cpp) with a
+// Beckmann or GGX microfacet distribution, isotropic or anisotropic (alpha_u along the shading
+// frame's s, alpha_v along t), and visible-normal sampling (include/mitsuba/render/microfacet.h),
+// Mitsuba's default sampling.  All in the point's shading frame Frame3f(n) (coordinate_system),
+// fp32 with the libm functions.
 // ======================================================================
 struct ConductorArgs {
     int type;            // 0 Beckmann, 1 GGX (MicrofacetType)
-    float alpha;         // alpha_u = alpha_v
+    float alpha_u;       // roughness along the frame's s (microfacet.h m_alpha_u)
     float eta[4], k[4];  // complex IOR per RGB channel (spectral: eta[0], k[0] for every wavelength)
+    float alpha_v;       // roughness along t (= alpha_u: isotropic)
 };
 
-// MicrofacetDistribution::eval (microfacet.h:186-207), isotropic.  FAST: products with
-// 1 / alpha and v_rcp_f32 / v_exp_f32 in place of the divisions and expf.
+// MicrofacetDistribution::eval (microfacet.h:186-207).  FAST: products with 1 / alpha_u,
+// 1 / alpha_v and v_rcp_f32 / v_exp_f32 in place of the divisions and expf.
 template <bool FAST>
 __device__ __forceinline__ float mf_eval(const ConductorArgs& c, float3_ m) {
-    const float ct2 = m.z * m.z, a2 = c.alpha * c.alpha;
+    const float ct2 = m.z * m.z, a2 = c.alpha_u * c.alpha_v;
     float r;
     if constexpr (FAST) {
-        const float ia = fast_rcp(c.alpha), mx = m.x * ia, my = m.y * ia;
+        const float mx = m.x * fast_rcp(c.alpha_u), my = m.y * fast_rcp(c.alpha_v);
         if (c.type == 0) {
             const float ict2 = fast_rcp(ct2);
             r = fast_exp2(-(mx * mx + my * my) * ict2 * kLog2e) * (fast_rcp(kPi * a2) * (ict2 * ict2));
@@ -2394,10 +2396,10 @@ __device__ __forceinline__ float mf_eval(const ConductorArgs& c, float3_ m) {
         }
     } else {
         if (c.type == 0) {
-            const float mx = m.x / c.alpha, my = m.y / c.alpha;
+            const float mx = m.x / c.alpha_u, my = m.y / c.alpha_v;
             r = expf(-(mx * mx + my * my) / ct2) / (kPi * a2 * (ct2 * ct2));
         } else {
-            const float mx = m.x / c.alpha, my = m.y / c.alpha, q = mx * mx + my * my + m.z * m.z;
+            const float mx = m.x / c.alpha_u, my = m.y / c.alpha_v, q = mx * mx + my * my + m.z * m.z;
             r = 1.f / (kPi * a2 * (q * q));
         }
     }
@@ -2407,7 +2409,7 @@ __device__ __forceinline__ float mf_eval(const ConductorArgs& c, float3_ m) {
 // MicrofacetDistribution::smith_g1 (microfacet.h:330-354)
 template <bool FAST>
 __device__ __forceinline__ float mf_smith_g1(const ConductorArgs& c, float3_ v, float3_ m) {
-    const float xy = (c.alpha * v.x) * (c.alpha * v.x) + (c.alpha * v.y) * (c.alpha * v.y);
+    const float xy = (c.alpha_u * v.x) * (c.alpha_u * v.x) + (c.alpha_v * v.y) * (c.alpha_v * v.y);
     const float t2 = fdiv<FAST>(xy, v.z * v.z);
     float r;
     if (c.type == 0) {
@@ -2434,7 +2436,7 @@ struct MfView {
 template <bool FAST>
 __device__ __forceinline__ MfView mf_view(const ConductorArgs& c, float3_ wi) {
     MfView V;
-    float3_ wp = mk3(c.alpha * wi.x, c.alpha * wi.y, wi.z);
+    float3_ wp = mk3(c.alpha_u * wi.x, c.alpha_v * wi.y, wi.z);
     const float inv = FAST ? fast_rsq(dot3(wp, wp)) : 1.f / sqrtf(dot3(wp, wp));
     wp = mk3(wp.x * inv, wp.y * inv, wp.z * inv);
     const float st2 = fmaxf(1.f - wp.z * wp.z, 0.f);
@@ -2494,7 +2496,7 @@ __device__ __forceinline__ float3_ mf_sample(const ConductorArgs& c, const MfVie
                                              float* pdf) {
     float slx, sly;
     mf_sample_visible_11<FAST>(c, V, ux, uy, &slx, &sly);
-    const float tx = fmaf(V.cp, slx, -(V.sp * sly)) * c.alpha, ty = fmaf(V.sp, slx, V.cp * sly) * c.alpha;
+    const float tx = fmaf(V.cp, slx, -(V.sp * sly)) * c.alpha_u, ty = fmaf(V.sp, slx, V.cp * sly) * c.alpha_v;
     float3_ m = mk3(-tx, -ty, 1.f);
     const float mi = FAST ? fast_rsq(dot3(m, m)) : 1.f / sqrtf(dot3(m, m));
     m = mk3(m.x * mi, m.y * mi, m.z * mi);

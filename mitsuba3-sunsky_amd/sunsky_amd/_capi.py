@@ -98,6 +98,12 @@ _SIGS = {
     "sunsky_direct_conductor_rays": (C.c_int, [vp, Vec3In, Vec3In, C.c_int, C.c_float, c_float_p, c_float_p,
                                                C.c_uint32, C.c_uint32, C.c_size_t, Vec3Out, Vec3Out, vp,
                                                C.c_size_t, vp]),
+    "sunsky_direct_conductor_aniso": (C.c_int, [vp, Vec3In, Vec3In, C.c_int, C.c_float, C.c_float, c_float_p,
+                                                c_float_p, vp, C.c_int, C.c_size_t, C.c_uint32, C.c_uint32, vp,
+                                                C.c_size_t, C.c_size_t, vp, C.c_size_t, vp]),
+    "sunsky_direct_conductor_rays_aniso": (C.c_int, [vp, Vec3In, Vec3In, C.c_int, C.c_float, C.c_float, c_float_p,
+                                                     c_float_p, C.c_uint32, C.c_uint32, C.c_size_t, Vec3Out, Vec3Out,
+                                                     vp, C.c_size_t, vp]),
     "sunsky_hosek_sun_rad": (C.c_int, [C.c_char_p, C.c_double, C.c_double, C.c_double, C.c_double,
                                        C.POINTER(C.c_double)]),
     "plugin_name": (C.c_char_p, []),

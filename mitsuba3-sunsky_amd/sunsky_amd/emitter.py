@@ -23,6 +23,16 @@ _SEMANTICS = {"jit": _capi.SEMANTICS_JIT, "scalar": _capi.SEMANTICS_SCALAR}
 _PRECISION = {"fast": _capi.PRECISION_FAST, "reference": _capi.PRECISION_REFERENCE}
 
 
+def _alpha_uv(alpha):
+    """roughconductor's alpha: a float (isotropic) or (alpha_u, alpha_v) -> two floats."""
+    if np.ndim(alpha) == 0:
+        return float(alpha), float(alpha)
+    a = [float(x) for x in alpha]
+    if len(a) != 2:
+        raise ValueError("alpha must be a float or (alpha_u, alpha_v)")
+    return a[0], a[1]
+
+
 def _fa(values):
     arr = (C.c_float * len(values))(*[float(v) for v in values])
     return arr
@@ -500,10 +510,12 @@ class SunskyEmitter:
     def direct_conductor(self, normals, wi, alpha=0.1, distribution="beckmann", eta=0.0, k=1.0, seed=0, spp=1,
                          wavelengths=None, out=None, visibility=None):
         """Sun-and-sky light a rough conductor reflects towards wi (sunsky_direct_conductor): one
-        path vertex (path.cpp:176-250) with roughconductor.cpp (isotropic Beckmann / GGX,
-        visible normals; the reference's defaults: Beckmann, alpha 0.1, eta 0, k 1).  normals, wi
-        (3, n) world unit vectors; eta / k: 1 or 3 per-channel values (spectral: the first, for
-        every wavelength) -> (C, n)."""
+        path vertex (path.cpp:176-250) with roughconductor.cpp (Beckmann / GGX, visible normals;
+        the reference's defaults: Beckmann, alpha 0.1, eta 0, k 1).  alpha: a float, or
+        (alpha_u, alpha_v) for an anisotropic distribution (sunsky_direct_conductor_aniso; alpha_u
+        along the first tangent of coordinate_system(normal)).  normals, wi (3, n) world unit
+        vectors; eta / k: 1 or 3 per-channel values (spectral: the first, for every
+        wavelength) -> (C, n)."""
         normals, nin = self._vec_in(normals)
         wi, win = self._vec_in(wi)
         n = normals.shape[1]
@@ -530,15 +542,19 @@ class SunskyEmitter:
         e3 = [float(x) for x in np.broadcast_to(np.asarray(eta, np.float32), (3,))]
         k3 = [float(x) for x in np.broadcast_to(np.asarray(k, np.float32), (3,))]
         out = self._out(out, (kk, n))
-        check(lib().sunsky_direct_conductor(self._h, nin, win, dist, float(alpha), _fa(e3), _fa(k3), lam_p,
-                                            kk if self.is_spectral else 0, lstride, int(seed) & 0xFFFFFFFF, int(spp),
-                                            _ptr(vis), n, n, _ptr(out), out.stride(0), self._stream()))
+        tail = (_fa(e3), _fa(k3), lam_p, kk if self.is_spectral else 0, lstride, int(seed) & 0xFFFFFFFF, int(spp),
+                _ptr(vis), n, n, _ptr(out), out.stride(0), self._stream())
+        au, av = _alpha_uv(alpha)
+        if au == av:
+            check(lib().sunsky_direct_conductor(self._h, nin, win, dist, au, *tail))
+        else:
+            check(lib().sunsky_direct_conductor_aniso(self._h, nin, win, dist, au, av, *tail))
         return out
 
     def direct_conductor_rays(self, normals, wi, alpha=0.1, distribution="beckmann", seed=0, spp=1, eta=None,
                               k=None):
         """The shadow and BSDF rays of direct_conductor's samples -> (emitter_dir, bsdf_dir), each
-        (3, spp, n) world directions, (0, 0, 0) where no ray is needed.  With eta and k also the
+        (3, spp, n) world directions, (0, 0, 0) where no ray is needed; alpha as direct_conductor.  With eta and k also the
         BSDF samples' weights F G1 (the throughput of a path continuing along bsdf_dir) ->
         (emitter_dir, bsdf_dir, bsdf_weight), bsdf_weight (3 | 1, spp, n)."""
         normals, nin = self._vec_in(normals)
@@ -558,10 +574,13 @@ class SunskyEmitter:
             e3 = _fa([float(x) for x in np.broadcast_to(np.asarray(eta, np.float32), (3,))])
             k3 = _fa([float(x) for x in np.broadcast_to(np.asarray(k, np.float32), (3,))])
             bw = torch.empty((1 if self.is_spectral else 3, int(spp), n), dtype=torch.float32, device=self.device)
-        check(lib().sunsky_direct_conductor_rays(
-            self._h, nin, win, dist, float(alpha), e3, k3, int(seed) & 0xFFFFFFFF, int(spp), n,
-            Vec3Out(em[0].data_ptr(), em[1].data_ptr(), em[2].data_ptr()),
-            Vec3Out(bs[0].data_ptr(), bs[1].data_ptr(), bs[2].data_ptr()), _ptr(bw), n, self._stream()))
+        tail = (e3, k3, int(seed) & 0xFFFFFFFF, int(spp), n, Vec3Out(em[0].data_ptr(), em[1].data_ptr(), em[2].data_ptr()),
+                Vec3Out(bs[0].data_ptr(), bs[1].data_ptr(), bs[2].data_ptr()), _ptr(bw), n, self._stream())
+        au, av = _alpha_uv(alpha)
+        if au == av:
+            check(lib().sunsky_direct_conductor_rays(self._h, nin, win, dist, au, *tail))
+        else:
+            check(lib().sunsky_direct_conductor_rays_aniso(self._h, nin, win, dist, au, av, *tail))
         return (em, bs) if bw is None else (em, bs, bw)
 
     def eval_spectral_broadcast(self, wi, wavelengths, active=None, out=None):

@@ -466,21 +466,32 @@ def direct_diffuse_rays(em, normals, seed, spp):
 
 
 # ---------------------------------------------------------------- caller: a rough-conductor vertex
+def _auv(a):
+    """alpha as (alpha_u, alpha_v): a float is isotropic (microfacet.h:75-78)."""
+    if np.ndim(a) == 0:
+        return float(a), float(a)
+    au, av = a
+    return float(au), float(av)
+
+
 def _mf_eval(distr, a, m):
-    """MicrofacetDistribution::eval, isotropic (include/mitsuba/render/microfacet.h:186-207)."""
+    """MicrofacetDistribution::eval (include/mitsuba/render/microfacet.h:186-207); a = alpha or
+    (alpha_u, alpha_v)."""
+    au, av = _auv(a)
     ct2 = m[:, 2] ** 2
     with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
         if distr == "beckmann":
-            r = np.exp(-((m[:, 0] / a) ** 2 + (m[:, 1] / a) ** 2) / ct2) / (np.pi * a * a * ct2 * ct2)
+            r = np.exp(-((m[:, 0] / au) ** 2 + (m[:, 1] / av) ** 2) / ct2) / (np.pi * au * av * ct2 * ct2)
         else:
-            r = 1.0 / (np.pi * a * a * ((m[:, 0] / a) ** 2 + (m[:, 1] / a) ** 2 + m[:, 2] ** 2) ** 2)
+            r = 1.0 / (np.pi * au * av * ((m[:, 0] / au) ** 2 + (m[:, 1] / av) ** 2 + m[:, 2] ** 2) ** 2)
     r = np.nan_to_num(r, nan=0.0, posinf=0.0)
     return np.where(r * m[:, 2] > 1e-20, r, 0.0)
 
 
 def _mf_smith_g1(distr, a, v, m):
     """MicrofacetDistribution::smith_g1 (microfacet.h:330-354)."""
-    xy = (a * v[:, 0]) ** 2 + (a * v[:, 1]) ** 2
+    au, av = _auv(a)
+    xy = (au * v[:, 0]) ** 2 + (av * v[:, 1]) ** 2
     with np.errstate(divide="ignore", invalid="ignore"):
         t2 = xy / v[:, 2] ** 2
         if distr == "beckmann":
@@ -495,7 +506,8 @@ def _mf_smith_g1(distr, a, v, m):
 def _mf_sample(distr, a, wi, u):
     """MicrofacetDistribution::sample with visible normals (microfacet.h:293-320, 357-410) -> (m, pdf)."""
     from scipy.special import erf, erfinv
-    wp = np.stack([a * wi[:, 0], a * wi[:, 1], wi[:, 2]], axis=1)
+    au, av = _auv(a)
+    wp = np.stack([au * wi[:, 0], av * wi[:, 1], wi[:, 2]], axis=1)
     wp /= np.linalg.norm(wp, axis=1, keepdims=True)
     st2 = np.maximum(1.0 - wp[:, 2] ** 2, 0.0)
     with np.errstate(divide="ignore", invalid="ignore"):
@@ -507,7 +519,8 @@ def _mf_sample(distr, a, wi, u):
     ux, uy = u[:, 0].astype(np.float64), u[:, 1].astype(np.float64)
     if distr == "beckmann":
         tan_i = np.sqrt(np.maximum(1.0 - ct * ct, 0.0)) / ct
-        cot_i = 1.0 / tan_i
+        with np.errstate(divide="ignore"):
+            cot_i = 1.0 / tan_i          # normal incidence: inf, erf(inf) = 1 as dr::rcp gives
         maxval = erf(cot_i)
         ux = np.clip(ux, 1e-6, 1 - 1e-6)
         uy = np.clip(uy, 1e-6, 1 - 1e-6)
@@ -527,7 +540,7 @@ def _mf_sample(distr, a, wi, u):
         si = np.sqrt(np.maximum(1.0 - ct * ct, 0.0))
         norm = 1.0 / (si * py + ct * pz)
         sx, sy = (ct * py - si * pz) * norm, px * norm
-    tx, ty = (cp * sx - sp * sy) * a, (sp * sx + cp * sy) * a
+    tx, ty = (cp * sx - sp * sy) * au, (sp * sx + cp * sy) * av
     m = np.stack([-tx, -ty, np.ones_like(tx)], axis=1)
     m /= np.linalg.norm(m, axis=1, keepdims=True)
     pdf = _mf_eval(distr, a, m) * _mf_smith_g1(distr, a, wi, m) * np.abs((wi * m).sum(axis=1)) / wi[:, 2]
@@ -571,7 +584,8 @@ def _conductor_samples(em, normals, wi_world, distr, alpha, seed, spp, lam):
     s, t = _coordinate_system(normals)
     wv = np.asarray(wi_world, dtype=np.float32)
     wi = np.stack([(wv * s).sum(1), (wv * t).sum(1), (wv * normals).sum(1)], axis=1).astype(np.float64)
-    a = max(float(alpha), 1e-4)
+    au, av = _auv(alpha)
+    a = (max(au, 1e-4), max(av, 1e-4))   # MicrofacetDistribution::configure, microfacet.h:424-428
     for _ in range(spp):
         u0, u1 = rng.next_float(), rng.next_float()
         rng.next_float()
@@ -595,7 +609,8 @@ def _conductor_samples(em, normals, wi_world, distr, alpha, seed, spp, lam):
 def direct_conductor(em, normals, wi_world, alpha=0.1, distribution="beckmann", eta=0.0, k=1.0, seed=0, spp=1,
                      wavelengths=None, vis=None):
     """Sun-and-sky light a rough conductor reflects towards wi (one vertex of
-    src/integrators/path.cpp:176-250 with src/bsdfs/roughconductor.cpp): emitter sampling
+    src/integrators/path.cpp:176-250 with src/bsdfs/roughconductor.cpp; alpha = a float or
+    (alpha_u, alpha_v)): emitter sampling
     (f cos x weight x MIS) + visible-normal BSDF sampling (F G1(wo) x eval x MIS), power
     heuristic, spp samples.  em: an Oracle; eta / k: 1 or 3 values (spectral: the first).
     vis: None or (spp, n) uint8 tracer verdicts.  Returns (C, n) fp64."""

@@ -80,6 +80,42 @@ def test_microfacet_matches_reference_test_vectors():
     assert np.allclose(O._mf_smith_g1("ggx", 0.1, v, z), 0.46130955, rtol=1e-5)
 
 
+def test_microfacet_anisotropic_matches_reference_test_vectors():
+    """src/render/tests/test_microfacet.py, anisotropic rows (alpha_u 0.1, alpha_v 0.3): Beckmann
+    eval over theta in linspace(0, pi, 20) at phi = pi/2 and over phi at theta = 0.1; Beckmann
+    and GGX smith_g1 (m = +z) over theta in linspace(pi/3, pi/2, 20) at phi = pi/2 and over phi
+    at theta = 0.98 pi/2 (dr.allclose: rtol 1e-5, atol 1e-8, or the rows' atol 1e-5)."""
+    steps, a = 20, (0.1, 0.3)
+    v = _sph(np.linspace(0, np.pi, steps), np.full(steps, np.pi / 2))
+    ref = np.zeros(steps)
+    ref[:7] = [1.06103287e+01, 8.22650051e+00, 3.57923722e+00, 6.84863329e-01, 3.26460004e-02, 1.01964230e-04,
+               5.87322635e-10]
+    assert np.allclose(O._mf_eval("beckmann", a, v), ref, rtol=1e-5, atol=1e-8)
+    v = _sph(np.full(steps, 0.1), np.linspace(0, 2 * np.pi, steps))
+    half = [3.95569706, 4.34706259, 5.54415846, 7.4061389, 9.17129803, 9.62056446, 8.37803268, 6.42071199,
+            4.84459257, 4.05276537]
+    assert np.allclose(O._mf_eval("beckmann", a, v), half + half[::-1], rtol=1e-5, atol=1e-8)
+    z = np.tile([0.0, 0.0, 1.0], (steps, 1))
+    v = _sph(np.linspace(np.pi / 3, np.pi / 2, steps), np.full(steps, np.pi / 2))
+    g_beck = [1.0000000e+00, 1.0000000e+00, 1.0000000e+00, 1.0000523e+00, 9.9941480e-01, 9.9757767e-01,
+              9.9420297e-01, 9.8884594e-01, 9.8091525e-01, 9.6961778e-01, 9.5387781e-01, 9.3222123e-01,
+              9.0260512e-01, 8.6216795e-01, 8.0686140e-01, 7.3091686e-01, 6.2609726e-01, 4.8074335e-01,
+              2.7883825e-01, 1.9197471e-06]
+    g_ggx = [9.4031686e-01, 9.3310797e-01, 9.2485082e-01, 9.1534841e-01, 9.0435863e-01, 8.9158219e-01,
+             8.7664890e-01, 8.5909742e-01, 8.3835226e-01, 8.1369340e-01, 7.8421932e-01, 7.4880326e-01,
+             7.0604056e-01, 6.5419233e-01, 5.9112519e-01, 5.1425743e-01, 4.2051861e-01, 3.0633566e-01,
+             1.6765384e-01, 1.0861372e-06]
+    assert np.allclose(O._mf_smith_g1("beckmann", a, v, z), g_beck, rtol=1e-5, atol=1e-5)
+    assert np.allclose(O._mf_smith_g1("ggx", a, v, z), g_ggx, rtol=1e-5, atol=1e-5)
+    v = _sph(np.full(steps, np.pi / 2 * 0.98), np.linspace(0, 2 * np.pi, steps))
+    half_b = [0.67333597, 0.56164336, 0.42798978, 0.35298213, 0.31838724, 0.31201753, 0.33166203, 0.38421196,
+              0.48717275, 0.63746351]
+    half_g = [0.46130955, 0.36801264, 0.26822716, 0.21645154, 0.19341162, 0.18922243, 0.20219423, 0.23769052,
+              0.31108665, 0.43013984]
+    assert np.allclose(O._mf_smith_g1("beckmann", a, v, z), half_b + half_b[::-1], rtol=1e-5)
+    assert np.allclose(O._mf_smith_g1("ggx", a, v, z), half_g + half_g[::-1], rtol=1e-5)
+
+
 def _fresnel_dielectric(c, eta):
     """Unpolarised Fresnel reflectance of a real interface (1 if totally reflected)."""
     s2t = (1 - c * c) / (eta * eta)
@@ -99,7 +135,7 @@ def test_fresnel_conductor_is_dielectric_for_a_real_ior():
     assert np.allclose(O._fresnel_conductor(c, 0.0, 1.0), 1.0)
 
 
-def visible_normalisation(distribution, alpha, theta_i):
+def visible_normalisation(distribution, alpha, theta_i, phi_i=0.0):
     """int D(m) G1(wi, m) max(0, wi.m) dm / cos(theta_i) by quadrature."""
     mu, wmu = _gl(512, 0.0, 1.0)
     phi = (np.arange(1024) + 0.5) * (2 * np.pi / 1024)
@@ -107,7 +143,8 @@ def visible_normalisation(distribution, alpha, theta_i):
     st = np.sqrt(1 - M * M)
     m = np.stack([st * np.cos(P), st * np.sin(P), M], axis=-1).reshape(-1, 3)
     wt = (wmu[:, None] * np.full(1024, 2 * np.pi / 1024)[None, :]).reshape(-1)
-    wi = np.tile([math.sin(theta_i), 0.0, math.cos(theta_i)], (m.shape[0], 1))
+    wi = np.tile([math.sin(theta_i) * math.cos(phi_i), math.sin(theta_i) * math.sin(phi_i), math.cos(theta_i)],
+                 (m.shape[0], 1))
     f = O._mf_eval(distribution, alpha, m) * O._mf_smith_g1(distribution, alpha, wi, m) * np.maximum((wi * m).sum(1), 0)
     return (f * wt).sum() / wi[0, 2]
 
@@ -116,28 +153,43 @@ def expected_range(q, distribution, alpha, normal, wi):
     """The estimator's expectation lies between q and q / N, N = visible_normalisation: the
     sampler draws exact visible normals but reports D G1_fit |wi.m| / cos = N x their density
     (G1_fit / G1_exact depends on wi only), which scales the BSDF-sampled half by 1 / N."""
-    th = math.acos(float(np.clip(np.dot(normal, wi) / np.linalg.norm(normal), -1, 1)))
-    r = 1.0 / visible_normalisation(distribution, alpha, th)
+    x, y, z = _shading_frame(normal)
+    th = math.acos(float(np.clip(np.dot(z, wi), -1, 1)))
+    r = 1.0 / visible_normalisation(distribution, alpha, th, math.atan2(np.dot(y, wi), np.dot(x, wi)))
     return q * min(1.0, r), q * max(1.0, r)
+
+
+def _shading_frame(normal):
+    """The product's shading frame of a normal: coordinate_system (vector.h:116-137), whose
+    first tangent carries alpha_u."""
+    nf = np.asarray(normal, np.float32)[None]
+    s, t = O._coordinate_system(nf)
+    return s[0].astype(np.float64), t[0].astype(np.float64), nf[0].astype(np.float64)
 
 
 @pytest.mark.parametrize("distribution", ["beckmann", "ggx"])
 @pytest.mark.parametrize("theta_i", [0.2, 1.2])
-def test_visible_normal_pdf_is_normalised(distribution, theta_i):
+@pytest.mark.parametrize("alpha", [0.3, (0.1, 0.4)])
+def test_visible_normal_pdf_is_normalised(distribution, theta_i, alpha):
     """int D(m) G1(wi, m) max(0, wi.m) / cos(theta_i) dm = 1 (the visible-normal density the
     sampler reports): exact for GGX's G1; Beckmann's G1 is a rational fit (microfacet.h:
     340-345), off by 3.1e-3 at theta_i = 1.2 -- the reference's own sampled density (exact
-    Beckmann visible normals) and reported pdf differ by as much."""
-    tot = visible_normalisation(distribution, 0.3, theta_i)
+    Beckmann visible normals) and reported pdf differ by as much.  Anisotropic: wi at azimuth
+    0.7, where alpha_u != alpha_v matters."""
+    tot = visible_normalisation(distribution, alpha, theta_i, 0.0 if np.ndim(alpha) == 0 else 0.7)
     assert abs(tot - 1) < (1e-4 if distribution == "ggx" else 4e-3), tot
 
 
 @pytest.mark.parametrize("distribution", ["beckmann", "ggx"])
-def test_visible_normal_samples_follow_their_pdf(distribution):
+@pytest.mark.parametrize("a", [0.3, (0.1, 0.4)])
+def test_visible_normal_samples_follow_their_pdf(distribution, a):
     """The sampled normals' density is the reported pdf: moments of m under 2^18 samples
-    (Beckmann's 3 Newton steps included) equal their quadrature against the pdf."""
-    a, theta_i, n = 0.3, 0.9, 1 << 18
-    wi = np.tile([math.sin(theta_i), 0.0, math.cos(theta_i)], (n, 1))
+    (Beckmann's 3 Newton steps included) equal their quadrature against the pdf; anisotropic
+    with wi at azimuth 0.7 (the stretch by (alpha_u, alpha_v), microfacet.h:301-316)."""
+    theta_i, n = 0.9, 1 << 18
+    phi_i = 0.0 if np.ndim(a) == 0 else 0.7
+    wi = np.tile([math.sin(theta_i) * math.cos(phi_i), math.sin(theta_i) * math.sin(phi_i), math.cos(theta_i)],
+                 (n, 1))
     u = np.random.default_rng(5).random((n, 2)).astype(np.float32)
     m, pdf = O._mf_sample(distribution, a, wi, u)
     ref = O._mf_eval(distribution, a, m) * O._mf_smith_g1(distribution, a, wi, m) * np.abs((wi * m).sum(1)) / wi[:, 2]
@@ -151,7 +203,8 @@ def test_visible_normal_samples_follow_their_pdf(distribution):
     wq = np.tile(wi[0], (q.shape[0], 1))
     dens = O._mf_eval(distribution, a, q) * O._mf_smith_g1(distribution, a, wq, q) * np.maximum((wq * q).sum(1), 0) / wq[0, 2]
     dens = dens / (dens * wt).sum()       # the Beckmann fit's 1e-3 normalisation aside
-    for g in (lambda v: v[:, 0], lambda v: v[:, 2], lambda v: v[:, 0] ** 2, lambda v: v[:, 1] ** 2):
+    for g in (lambda v: v[:, 0], lambda v: v[:, 1], lambda v: v[:, 2], lambda v: v[:, 0] ** 2,
+              lambda v: v[:, 1] ** 2, lambda v: v[:, 0] * v[:, 1]):
         est, se = g(m).mean(), g(m).std() / math.sqrt(n)
         assert abs(est - (g(q) * dens * wt).sum()) < 5 * se, (est, (g(q) * dens * wt).sum(), se)
 
@@ -169,12 +222,12 @@ def _cap(axis, mu0, n_mu, n_phi):
 
 def _lobe_integral(em, w, wt, normal, wi_world, distribution, alpha, eta, k, lam):
     """sum over quadrature nodes w of L(w) f(wi, w) cos(n, w): f cos from the oracle's
-    roughconductor restatement in a frame of the normal (isotropic, so any frame)."""
-    x, y, z = _frame(normal)
+    roughconductor restatement in the product's shading frame (alpha_u along its first tangent)."""
+    x, y, z = _shading_frame(normal)
     to_l = lambda v: np.stack([v @ x, v @ y, v @ z], axis=1)   # noqa: E731
     wo = to_l(w)
     wi = np.tile(to_l(np.asarray(wi_world, np.float64)[None])[0], (w.shape[0], 1))
-    val, _, cih = O._conductor_eval_pdf(distribution, max(alpha, 1e-4), wi, wo)
+    val, _, cih = O._conductor_eval_pdf(distribution, alpha, wi, wo)
     lw = (-w).astype(np.float32)
     if em.spectral:
         L = np.stack([em.eval(lw, np.full(lw.shape[0], lam_, np.float32)) for lam_ in lam])
@@ -278,6 +331,19 @@ def test_direct_conductor_host_errors():
     assert b"eta" in L.sunsky_last_error()
     assert rays(h, v, v, 0, 0.1, None, None, 0, 1, 1, o3, o3, None, 1, None) != 0                # host-only
     assert rays(h, v, v, 0, 0.1, None, None, 0, 1, 0, o3, o3, None, 0, None) == 0                # n = 0
+    # the anisotropic forms validate both alphas (finite, > 0) before any device work
+    da, ra = L.sunsky_direct_conductor_aniso, L.sunsky_direct_conductor_rays_aniso
+    for au, av in ((0.1, 0.0), (0.0, 0.1), (0.1, float("nan")), (float("inf"), 0.1)):
+        assert da(h, v, v, 0, au, av, one, one, None, 0, 0, 0, 1, None, 0, 1, out, 1, None) != 0
+        assert b"alpha" in L.sunsky_last_error()
+        assert ra(h, v, v, 1, au, av, None, None, 0, 1, 1, o3, o3, None, 1, None) != 0
+    assert da(h, v, v, 0, 0.1, 0.3, one, one, None, 0, 0, 0, 1, None, 0, 1, out, 1, None) != 0   # host-only
+    assert b"host-only" in L.sunsky_last_error()
+    assert da(h, v, v, 1, 0.1, 0.3, one, one, None, 0, 0, 0, 1, None, 0, 0, out, 1, None) == 0   # n = 0
+    from sunsky_amd.emitter import _alpha_uv
+    assert _alpha_uv(0.2) == (0.2, 0.2) and _alpha_uv((0.1, 0.3)) == (0.1, 0.3)
+    with pytest.raises(ValueError):
+        _alpha_uv((0.1, 0.2, 0.3))
     L.sunsky_emitter_destroy(h)
     L.sunsky_props_destroy(props)
 
@@ -313,15 +379,17 @@ Q, TOL = 0.995, 1e-3
 @pytest.mark.parametrize("variant", ["rgb", "spectral"])
 @pytest.mark.parametrize("precision", ["fast", "reference"])
 @pytest.mark.parametrize("distribution", ["beckmann", "ggx"])
-def test_direct_conductor_parity(variant, precision, distribution):
+@pytest.mark.parametrize("alpha", [0.25, (0.08, 0.35)])
+def test_direct_conductor_parity(variant, precision, distribution, alpha):
     """Per point the GPU kernel equals oracle.direct_conductor on the same PCG32 streams (the
-    oracle adopts the product's staged w_sky), 2^14 points x 4 spp, rough (0.25) lobes."""
+    oracle adopts the product's staged w_sky), 2^14 points x 4 spp, rough (0.25) lobes and an
+    anisotropic (alpha_u 0.08, alpha_v 0.35) one (sunsky_direct_conductor_aniso)."""
     import torch
     scene = dict(SCENE, to_world=_rot_x(0.35)) if precision == "reference" else SCENE
     em = ss.SunskyEmitter(scene, variant, precision=precision)
     o32 = O.Oracle(scene, variant, "jit", "f32")
     o32.override_w_sky(em.sky_sampling_w)
-    n, spp, seed, alpha = 1 << 14, 4, 11, 0.25
+    n, spp, seed = 1 << 14, 4, 11
     normals = _gpu_normals(n, 3)
     wi = _gpu_views(normals, 4)
     rng = np.random.default_rng(4)
@@ -361,14 +429,15 @@ def test_direct_conductor_glossy_parity(distribution):
 @pytest.mark.parametrize("variant", ["rgb", "spectral"])
 @pytest.mark.parametrize("distribution", ["beckmann", "ggx"])
 @pytest.mark.parametrize("view", list(VIEWS))
-def test_direct_conductor_unbiased(variant, distribution, view):
+@pytest.mark.parametrize("alpha", [0.3, (0.12, 0.4)])
+def test_direct_conductor_unbiased(variant, distribution, view, alpha):
     """2^20 points x 16 spp: the GPU estimate matches the quadrature within 5 standard errors
     + 1.5e-3 (the fp32 sun-cone edge loss test_direct_diffuse_unbiased documents) of the range
     expected_range allows.  Measured: Beckmann at the grazing view (theta_i 1.35, N = 0.99818)
     sits +0.19 % above q, the reference estimator's own 1 / N - 1 = +0.18 %."""
     import torch
     em = ss.SunskyEmitter(SCENE, variant)
-    n, spp, alpha = 1 << 20, 16, 0.3
+    n, spp = 1 << 20, 16
     wi = view_dir(view)
     nrm = _t(np.tile(NORMAL.astype(np.float32), (n, 1)))
     wis = _t(np.tile(wi.astype(np.float32), (n, 1)))
@@ -384,7 +453,8 @@ def test_direct_conductor_unbiased(variant, distribution, view):
 @pytest.mark.gpu
 @pytest.mark.parametrize("precision", ["fast", "reference"])
 @pytest.mark.parametrize("distribution", ["beckmann", "ggx"])
-def test_direct_conductor_rays_parity(precision, distribution):
+@pytest.mark.parametrize("alpha", [0.2, (0.1, 0.3)])
+def test_direct_conductor_rays_parity(precision, distribution, alpha):
     """sunsky_direct_conductor_rays writes the directions oracle.direct_conductor_rays draws
     on the same streams: emitter rays at the sampling bounds of test_gpu_parity.py (p99.9 <
     2e-6, max < 1e-4); BSDF rays p99.9 < 5e-4, max < 5e-2: fp32 against fp64 visible-normal
@@ -395,7 +465,7 @@ def test_direct_conductor_rays_parity(precision, distribution):
     em = ss.SunskyEmitter(SCENE, "rgb", precision=precision)
     o32 = O.Oracle(SCENE, "rgb", "jit", "f32")
     o32.override_w_sky(em.sky_sampling_w)
-    n, spp, seed, alpha = 1 << 14, 3, 21, 0.2
+    n, spp, seed = 1 << 14, 3, 21
     normals = _gpu_normals(n, 9)
     wi = _gpu_views(normals, 10)
     e_g, b_g, w_g = em.direct_conductor_rays(_t(normals), _t(wi), alpha, distribution, seed, spp, GOLD["eta"],
@@ -490,3 +560,37 @@ def test_direct_conductor_visibility_all_and_none_and_seeded():
     assert torch.allclose(run(vis=full(1)) + run(vis=full(2)), free, rtol=1e-5, atol=1e-6 * float(free.abs().max()))
     with pytest.raises(ValueError):
         run(vis=torch.zeros((spp + 1, n), dtype=torch.uint8, device="cuda"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+def test_direct_conductor_aniso_entry_with_equal_alphas_is_the_isotropic_call(variant):
+    """sunsky_direct_conductor_aniso(alpha, alpha) and sunsky_direct_conductor(alpha) give the
+    same bits (one kernel, alpha_u = alpha_v), estimates and rays."""
+    import torch
+    from sunsky_amd import _capi
+    from sunsky_amd.emitter import _fa, _ptr
+    em = ss.SunskyEmitter(SCENE, variant)
+    n, spp, seed, a = 4099, 2, 3, 0.17
+    normals, wi = _gpu_normals(n, 5), None
+    wi = _gpu_views(normals, 6)
+    nt, wt = _t(normals), _t(wi)
+    lam = torch.from_numpy(np.random.default_rng(2).uniform(360, 720, (4, n)).astype(np.float32)).cuda() \
+        if variant == "spectral" else None
+    iso = em.direct_conductor(nt, wt, a, "ggx", GOLD["eta"], GOLD["k"], seed, spp, lam)
+    nin, win = em._vec_in(nt)[1], em._vec_in(wt)[1]
+    out = torch.empty_like(iso)
+    kk = iso.shape[0]
+    rc = ss.lib().sunsky_direct_conductor_aniso(
+        em._h, nin, win, 1, a, a, _fa(list(GOLD["eta"])), _fa(list(GOLD["k"])), _ptr(lam),
+        kk if variant == "spectral" else 0, n if lam is not None else 0, seed, spp, None, n, n, _ptr(out), n,
+        em._stream())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.equal(iso, out)
+    r_iso = em.direct_conductor_rays(nt, wt, a, "beckmann", seed, spp, GOLD["eta"], GOLD["k"])
+    r_an = em.direct_conductor_rays(nt, wt, (a, a + 0.0), "beckmann", seed, spp, GOLD["eta"], GOLD["k"])
+    assert all(torch.equal(x, y) for x, y in zip(r_iso, r_an))
+    r_an2 = em.direct_conductor_rays(nt, wt, (a, 0.3), "beckmann", seed, spp, GOLD["eta"], GOLD["k"])
+    assert not torch.equal(r_iso[1], r_an2[1])   # alpha_v reaches the sampler
+

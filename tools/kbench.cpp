@@ -99,8 +99,9 @@ int main(int argc, char** argv) {
     }
     const int nout = spec ? 11 : (rays || sspec) ? 4 : (mode == "pdf" ? 1 : 3);
     // conductor mode: normals (mostly facing up) and views in their upper hemisphere
-    struct ConductorArgs { int type; float alpha; float eta[4], k[4]; };
-    ConductorArgs cargs = {std::getenv("KB_BECKMANN") ? 0 : 1, 0.2f, {0.143f, 0.374f, 1.442f, 0.f}, {3.983f, 2.385f, 1.603f, 0.f}};
+    struct ConductorArgs { int type; float alpha_u; float eta[4], k[4]; float alpha_v; };
+    ConductorArgs cargs = {std::getenv("KB_BECKMANN") ? 0 : 1, 0.2f, {0.143f, 0.374f, 1.442f, 0.f}, {3.983f, 2.385f, 1.603f, 0.f},
+                           0.2f};
     float *cnx = nullptr, *cny = nullptr, *cnz = nullptr, *cvx = nullptr, *cvy = nullptr, *cvz = nullptr;
     if (cond || swl) {
         std::normal_distribution<float> G(0.f, 1.f);

@@ -430,6 +430,32 @@ def parity_c4(em, d_scene, u, d, pdf_s, wgt, pdf_q, n_check=1 << 19, semantics="
             "bounds": "dir p99.9 < 2e-6, max < 1e-4; pdf 1e-5 rel; weights 2e-5 (sky vs o32, sun vs o64)"}
 
 
+def parity_caller(kind, em, d_scene, nrm, out, seed, spp, vw=None, n_check=4096):
+    """Caller parity on the first n_check points (PCG32 streams by point index, so the first
+    points are the oracle's points 0..n_check-1): per point the GPU estimate vs
+    oracle.direct_diffuse / direct_conductor (GGX 0.2, the bench's eta / k) with the product's
+    staged w_sky; the bounds of tests/test_direct_diffuse.py and test_direct_conductor.py
+    (p99.5 of the per-point max channel error relative to max(|ref|, 1e-3 max|ref|))."""
+    O = _oracle()
+    torch.cuda.synchronize()            # the caller kernels ran on the bench's own stream
+    o32 = O.Oracle(d_scene, "rgb", "jit", "f32")
+    o32.override_w_sky(em.sky_sampling_w)
+    nh = nrm[:, :n_check].T.cpu().numpy()
+    got = out[:, :n_check].cpu().numpy().astype(np.float64)
+    if kind == "diffuse":
+        ref, bound = O.direct_diffuse(o32, nh, seed, spp), 2e-4
+    else:
+        ref = O.direct_conductor(o32, nh, vw[:, :n_check].T.cpu().numpy(), 0.2, "ggx", (0.143, 0.374, 1.442),
+                                 (3.983, 2.385, 1.603), seed, spp)
+        bound = 1e-3
+    rel = (np.abs(got - ref) / np.maximum(np.abs(ref), 1e-3 * np.abs(ref).max())).max(axis=0)
+    q = np.quantile(rel, [0.5, 0.995, 1.0])
+    return {"checked_points": n_check, "spp": spp, "rel_p50": float(q[0]), "rel_p995": float(q[1]),
+            "rel_max": float(q[2]), "mean_rel_delta": float(abs(got.mean() - ref.mean()) / abs(ref.mean())),
+            "pass": bool(q[1] < bound and np.all(np.isfinite(got))),
+            "bounds": f"per-point p99.5 < {bound:g} (tests' bound; fp32 vs the oracle's fp64 BSDF / MIS terms)"}
+
+
 def run_c5(args, world, rank, dev, coll_dev, rehearsal):
     """configs[4]: a --c5-dirs spectral batch per GPU (11 model
     wavelengths, the C3 node kernel), then the gather of every rank's (11, n) radiance
@@ -927,6 +953,9 @@ def main():
                                            "note": "per sample: sample_direction + eval (emitter sampling), cosine "
                                                    "BSDF sample + pdf_direction + eval (escaped ray), power-heuristic "
                                                    "MIS; C4 sun/sky, random normals; one fused kernel"}
+        if rank == 0:
+            sec["direct_diffuse_16M_x4spp"]["parity"] = parity_caller(
+                "diffuse", smp, dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), nrm, dd, 7, spp)
         # the glossy vertex: the same points seen from random view directions, a rough conductor
         # (GGX, alpha 0.2, gold-like eta / k) -- sunsky_direct_conductor, reads 24 B, writes 12 B
         vw = torch.randn((3, npts), generator=g, device=dev)
@@ -955,6 +984,9 @@ def main():
                                              "note": "per sample: sample_direction + eval + rough-conductor eval/pdf "
                                                      "(emitter sampling), GGX visible-normal sample + pdf_direction + "
                                                      "eval (escaped ray), power-heuristic MIS; one fused kernel"}
+        if rank == 0:
+            sec["direct_conductor_16M_x4spp"]["parity"] = parity_caller(
+                "conductor", smp, dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), nrm, dd, 7, spp, vw=vw)
         del nrm, dd, vw
         if rank == 0:
             try:

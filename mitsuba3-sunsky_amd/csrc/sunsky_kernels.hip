@@ -3435,8 +3435,10 @@ SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_ref, false, SS_SORT_
 // (test_wave_sorted_rgb_kernels_bitwise_vs_unsorted) but slower: 2 % in round 2 (125 VGPRs and 28
 // SGPR spills, profiles/r02_v13_ab_sample_full.log), 14 % against the round-3 unsorted general kernel,
 // 10 % with the mask and it.p prefetched (114 VGPRs, 42 SGPR spills;
-// profiles/r03_v23_ab_sample_full.log), so the C ABI keeps the unsorted general kernel.
+// profiles/r03_v23_ab_sample_full.log), so the C ABI keeps the unsorted general kernel and takes this one
+// only with SUNSKY_AMD_SORTED_GENERAL_SAMPLING=1 (test_wave_sorted_rgb_kernels_bitwise_vs_unsorted).
 SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_full_sorted_fast, true, 4, true)
+SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_full_sorted_ref, false, 4, true)
 
 
 #define SS_PDF_DIRECTION(NAME, VEC, FAST)                                                                     \

@@ -288,6 +288,15 @@ def test_wave_sorted_rgb_kernels_bitwise_vs_unsorted(precision, monkeypatch):
         mk = host(mask)
         assert np.all(masked[2][:, ~mk] == 0) and np.array_equal(masked[2][:, mk], lean[2][:, mk]), n
         assert np.array_equal(masked[0], lean[0]), n
+        # the general call through the wave-sorted kernel (mask prefetched with u, it.p before
+        # the passes): the unsorted general kernel's bits, with and without the mask
+        monkeypatch.delenv("SUNSKY_AMD_UNSORTED_SAMPLING", raising=False)
+        monkeypatch.setenv("SUNSKY_AMD_SORTED_GENERAL_SAMPLING", "1")
+        for a_, b_ in zip(run(ut, ss.Interaction3f(p=p), None, True), full):
+            assert np.array_equal(a_, b_), n
+        for a_, b_ in zip(run(ut, ss.Interaction3f(p=p), mask, True), masked):
+            assert np.array_equal(a_, b_), n
+        monkeypatch.delenv("SUNSKY_AMD_SORTED_GENERAL_SAMPLING", raising=False)
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)

@@ -1124,6 +1124,13 @@ int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam
                 axis[k] = 1.f;
                 A.st[2 + k] = M.tangent_stage(kJvpSunDirection, axis, 3);
             }
+            if (nb == kVjpBases) {
+                // the sky tables of sun axis k are d eta_k times those of a unit elevation
+                // tangent: basis 2 holds the latter and the kernels scale by d eta_k
+                // (kVjpSunEta), one sky tangent per channel for the 3 axes instead of 3
+                A.eta_off = kVjpSunEta;
+                A.st[2].dx = A.st[2].dx_per_eta;
+            }
             e->stage_tangent(A, st);
             e->vjp_rev = e->rev;
         }

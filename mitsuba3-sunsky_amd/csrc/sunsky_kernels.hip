@@ -2932,6 +2932,15 @@ __device__ __forceinline__ float sky_tan(const SkyChannel& k, const float* dk, c
     return (dc1 * s.c2 + s.c1 * dc2) * k.rad + s.c1 * s.c2 * dk[9];
 }
 
+// sky_tan along d gamma = 1 with d params = 0 (the gamma part of a sun-axis tangent)
+__device__ __forceinline__ float sky_tan_gamma(const SkyChannel& k, const DirTerms& t, const SkyVal& s, float sg) {
+    const float cg = t.cg, dcg = -sg;
+    const float db = -2.f * k.I * dcg;
+    const float dchi = 2.f * cg * dcg * s.inv_pb - 1.5f * s.chi * db * s.inv_b;
+    const float dc2 = k.D * s.e2 * k.E + k.F * 2.f * cg * dcg + k.G * dchi;
+    return s.c1 * dc2 * k.rad;
+}
+
 // unit_angle_tangent split for several tangents da of one (a, b): the per-direction part
 // (the chord v and 1 / (2 h sqrt(1 - h^2)) with the branch sign) once, then one dot per tangent.
 struct UnitAngleTan { float3_ v; float f, sd; };
@@ -3109,15 +3118,21 @@ __device__ __forceinline__ void eval_jvp_spec_body(const SunskyKArgs& K, const f
 // per workgroup in a fixed order (wave shuffles, then LDS) into per-block
 // partials, which sunsky_grad_reduce adds to grad in block order --
 // deterministic, no float atomics.
-// vjp buffer: [0, 550) dsky for T / albedo-diagonal / sun x / sun y / sun z
-// (5 x 110), [550, 559) d local sun direction of the 3 sun axes, [576, ...) d sun table (T).
+// vjp buffer: [0, 330) dsky for T / albedo-diagonal / unit sun elevation (3 x 110; 330..549
+// the per-axis tables, not read), [550, 559) d local sun direction of the 3 sun axes,
+// [559, 562) d eta of the 3 sun axes, [576, ...) d sun table (T).
+// The sky parameters depend on the sun only through its elevation eta, and the sky tangent
+// is linear in (d params, d gamma): along sun axis k it is d eta_k x (unit-eta tangent at
+// d gamma = 0) + d gamma_k x (the gamma part).  Each ray accumulates the first, summed over
+// rays, in g[15] (scaled by d eta_k per lane before the reduction) and the second per axis.
 // ======================================================================
-constexpr int kGradCount = 16;           // 0: T, 1..11: albedo channel, 12..14: sun_direction, 15: pad
+constexpr int kGradCount = 16;           // 0: T, 1..11: albedo channel, 12..14: sun_direction, 15: per-lane unit-elevation sum (0 in the partials)
 
 struct VjpLds {
     SkyChannel sky[kNbWavelengths];   // per-lane channel index in the spectral kernel (see JvpLds)
-    float dsky[5][kNbWavelengths * 10];
+    float dsky[3][kNbWavelengths * 10];
     float dlocal[3][3];
+    float deta[3];
     float red[SS_BLOCK / 64][kGradCount];
 };
 
@@ -3128,8 +3143,11 @@ __device__ __forceinline__ float wave_sum(float v) {
 }
 
 // Per-workgroup reduction of the per-lane gradient accumulators -> partials[block][16]
-__device__ __forceinline__ void block_reduce_grad(VjpLds& L, const float g[kGradCount], float* partials) {
+__device__ __forceinline__ void block_reduce_grad(VjpLds& L, float g[kGradCount], float* partials) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) g[12 + k] += L.deta[k] * g[15];   // the unit-elevation sums
+    g[15] = 0.f;
 #pragma unroll
     for (int p = 0; p < kGradCount; ++p) {
         float w = wave_sum(g[p]);
@@ -3145,8 +3163,9 @@ __device__ __forceinline__ void block_reduce_grad(VjpLds& L, const float g[kGrad
 
 __device__ __forceinline__ void stage_vjp(const SunskyKArgs& K, const float* vjp, VjpLds* L) {
     lds_copy(L->sky, K.sky, kNbWavelengths);
-    for (int i = threadIdx.x; i < 5 * kNbWavelengths * 10; i += blockDim.x) (&L->dsky[0][0])[i] = vjp[i];
-    if (threadIdx.x < 9) (&L->dlocal[0][0])[threadIdx.x] = vjp[5 * kNbWavelengths * 10 + threadIdx.x];
+    for (int i = threadIdx.x; i < 3 * kNbWavelengths * 10; i += blockDim.x) (&L->dsky[0][0])[i] = vjp[i];
+    if (threadIdx.x < 9) (&L->dlocal[0][0])[threadIdx.x] = vjp[kVjpSunLocal + threadIdx.x];
+    if (threadIdx.x < 3) L->deta[threadIdx.x] = vjp[kVjpSunEta + threadIdx.x];
     __syncthreads();
 }
 
@@ -3190,8 +3209,10 @@ __device__ __forceinline__ void eval_vjp_rgb_body(const SunskyKArgs& K, const fl
             const float cs = cot * K.sky_scale;
             g[0] += cs * sky_tan(kc, L.dsky[0] + c * 10, t, sv, 0.f, sg);
             g[1 + c] += cs * sky_tan(kc, L.dsky[1] + c * 10, t, sv, 0.f, sg);
+            g[15] += cs * sky_tan(kc, L.dsky[2] + c * 10, t, sv, 0.f, sg);   // unit elevation
+            const float gam = sky_tan_gamma(kc, t, sv, sg);
 #pragma unroll
-            for (int k = 0; k < 3; ++k) g[12 + k] += cs * sky_tan(kc, L.dsky[2 + k] + c * 10, t, sv, dgs[k], sg);
+            for (int k = 0; k < 3; ++k) g[12 + k] += cs * gam * dgs[k];
             if (t.hit_sun) {
                 const float* S = K.sun_table + pos * (3 * kNbSunCtrlPts * kNbSunLdParams) + c * (kNbSunCtrlPts * kNbSunLdParams);
                 const float* dS = dsun_tab + pos * (3 * kNbSunCtrlPts * kNbSunLdParams) + c * (kNbSunCtrlPts * kNbSunLdParams);
@@ -3270,13 +3291,16 @@ __device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const f
                 db = sky_tan(khi, L.dsky[1] + hi * 10, t, shi, 0.f, sg);
                 g[1 + hi] += cot * K.sky_scale * whi * db;
             }
+            db = 0.f;
+            da = sky_tan(klo, L.dsky[2] + lo * 10, t, slo, 0.f, sg);   // unit elevation
+            if (has_hi) db = sky_tan(khi, L.dsky[2] + hi * 10, t, shi, 0.f, sg);
+            g[15] += cot * K.sky_scale * (wlo * da + whi * db);
+            db = 0.f;
+            da = sky_tan_gamma(klo, t, slo, sg);
+            if (has_hi) db = sky_tan_gamma(khi, t, shi, sg);
+            const float gam = cot * K.sky_scale * (wlo * da + whi * db);
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                db = 0.f;
-                da = sky_tan(klo, L.dsky[2 + k] + lo * 10, t, slo, dgs[k], sg);
-                if (has_hi) db = sky_tan(khi, L.dsky[2 + k] + hi * 10, t, shi, dgs[k], sg);
-                g[12 + k] += cot * K.sky_scale * (wlo * da + whi * db);
-            }
+            for (int k = 0; k < 3; ++k) g[12 + k] += gam * dgs[k];
             if (t.hit_sun) {
                 float sa = render_sun_spec(K.sun_table, pos, lo, xs), dsa = render_sun_spec(dsun_tab, pos, lo, xs);
                 float sun = sa, dsun = dsa;

@@ -661,7 +661,9 @@ TangentStage SunskyModel::tangent_stage(int param, const float* tangent, int cou
     // x = cbrt(2 eta / pi), dx = 2 / (3 pi x^2) deta; t_rem = T - floor(T), d t_rem / dT = 1
     const float eta = 0.5f * kPi - k_.sun_theta;
     s.x = std::cbrt(2.0 * eta / 3.14159265358979323846);
-    s.dx = s.x > 0.0 ? (2.0 / (3.0 * 3.14159265358979323846)) / (s.x * s.x) * deta : 0.0;
+    s.deta = deta;
+    s.dx_per_eta = s.x > 0.0 ? (2.0 / (3.0 * 3.14159265358979323846)) / (s.x * s.x) : 0.0;
+    s.dx = s.x > 0.0 ? s.dx_per_eta * deta : 0.0;
     s.t_high = (int)std::floor(turbidity_);
     s.t_low = s.t_high - 1;
     s.t_rem = (double)turbidity_ - s.t_high;

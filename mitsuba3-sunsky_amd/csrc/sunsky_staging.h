@@ -75,6 +75,7 @@ struct TangentStage {
     int t_low, t_high, in_range, nch;
     double albedo[kNbWavelengths], dalbedo[kNbWavelengths];
     float dsun_local[3];          // tangent of the local sun direction (sun_direction)
+    double deta, dx_per_eta;      // the sun elevation's tangent; dx = dx_per_eta * deta
 };
 
 SS_HD inline double powid_(double x, int k) {
@@ -135,7 +136,11 @@ constexpr int kTanSunLocal = kTanBlock;          // JVP: 110..112
 constexpr int kJvpSunOffset = 128;
 constexpr int kVjpBases = 5;                     // turbidity, albedo (diagonal), sun x / y / z
 constexpr int kVjpSunLocal = kVjpBases * kTanBlock;   // 550..558
+// VJP: d eta of the 3 sun axes (559..561).  The sky tables of a sun axis are d eta times
+// those of a unit elevation tangent, which the VJP stages as its basis 2 (eval_vjp_*_body)
+constexpr int kVjpSunEta = kVjpSunLocal + 9;
 constexpr int kVjpSunOffset = 576;
+static_assert(kVjpSunEta + 3 <= kVjpSunOffset, "VJP buffer layout");
 
 // Sky-channel entry j = c x 10 + q (< nch x 10) of one basis' tangent block: d{A..I}
 // (q < 9) from the sky parameter dataset, d rad (q = 9) from the sky radiance dataset.
@@ -156,6 +161,7 @@ struct TangentArgs {
     float* out;
     int nbasis, sun_local_off, sun_local_first, sun_off, sun_block, total;
     TangentStage st[kVjpBases];
+    int eta_off;   // > 0: d eta of bases [sun_local_first, nbasis) at out + eta_off (VJP)
 };
 
 // Float idx of the tangent buffer described by A (the device kernel's per-thread work).
@@ -165,6 +171,8 @@ SS_HD inline float tangent_buffer_value(const TangentArgs& A, int idx) {
         return j < A.st[b].nch * 10 ? tangent_value(A.sky_params_ds, A.sky_rad_ds, A.st[b], j) : 0.f;
     }
     const int nloc = 3 * (A.nbasis - A.sun_local_first);
+    if (A.eta_off > 0 && idx >= A.eta_off && idx < A.eta_off + nloc / 3)
+        return (float)A.st[A.sun_local_first + (idx - A.eta_off)].deta;
     if (idx >= A.sun_local_off && idx < A.sun_local_off + nloc) {
         const int k = (idx - A.sun_local_off) / 3, r = (idx - A.sun_local_off) % 3;
         return A.st[A.sun_local_first + k].dsun_local[r];

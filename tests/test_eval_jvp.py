@@ -113,7 +113,19 @@ def test_eval_jvp_matches_finite_differences(variant, param):
 def test_eval_vjp_matches_jvp_contractions(variant):
     """Reverse mode (sunsky_eval_vjp) against the forward mode: for a random cotangent,
     grad[p] = sum(d_out * jvp(e_p)) for every basis parameter; deterministic and accumulating."""
-    d = scene()
+    grad, cot, si, view, em = _vjp_vs_jvp(scene(), variant)
+    # deterministic, and accumulating into a given buffer
+    grad2, _ = em.eval_vjp(si, cot)
+    assert torch.equal(grad, grad2)
+    em.eval_vjp(si, cot, grad=grad2)
+    assert torch.allclose(grad2, 2 * grad, rtol=1e-6, atol=0)
+    assert view["albedo"].numel() == (11 if variant == "spectral" else 3)
+
+
+def _vjp_vs_jvp(d, variant, sun_axes=True):
+    """eval_vjp's 15 gradients against the contractions of eval_jvp along each basis tangent
+    (1e-4 of the contraction's magnitude); without sun axes (time/location mode) the three
+    sun_direction gradients must be 0."""
     em = ss.load_dict(d, variant=variant)
     o32 = O.Oracle(d, variant, "jit", "f32")
     wo = rays(o32)
@@ -134,16 +146,37 @@ def test_eval_vjp_matches_jvp_contractions(variant):
 
     checks = [(0, "turbidity", [1.0])]
     checks += [(1 + ch, "albedo", list(np.eye(nch)[ch])) for ch in range(nch)]
-    checks += [(12 + ax, "sun_direction", list(np.eye(3)[ax])) for ax in range(3)]
+    if sun_axes:
+        checks += [(12 + ax, "sun_direction", list(np.eye(3)[ax])) for ax in range(3)]
+    else:
+        assert np.all(g[12:15] == 0.0), g[12:15]
     for idx, param, tangent in checks:
         ref, mag = contract(param, tangent)
         assert abs(g[idx] - ref) <= 1e-4 * mag + 1e-12, (param, tangent, g[idx], ref, mag)
-    # deterministic, and accumulating into a given buffer
-    grad2, _ = em.eval_vjp(si, cot)
-    assert torch.equal(grad, grad2)
-    em.eval_vjp(si, cot, grad=grad2)
-    assert torch.allclose(grad2, 2 * grad, rtol=1e-6, atol=0)
-    assert view["albedo"].numel() == nch
+    return grad, cot, si, view, em
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+@pytest.mark.parametrize("case", ["low_sun", "high_sun", "rotated", "time_mode"])
+def test_eval_vjp_sun_axes_across_elevations_and_frames(variant, case):
+    """The VJP reaches the sun axes through one unit-elevation sky tangent scaled by d eta_k
+    plus the gamma part (sunsky_kernels.hip eval_vjp_*_body): the same contractions as the
+    forward mode near the horizon, near the zenith, under a rotated to_world, and with no
+    sun axes at all in time/location mode (sunsky.cpp:220-240: sun_direction is not exposed)."""
+    if case == "time_mode":
+        d = {"type": "sunsky", "hour": 15.5, "turbidity": 4.2, "albedo": 0.25}
+        _vjp_vs_jvp(d, variant, sun_axes=False)
+        return
+    if case == "low_sun":
+        d = scene(sun=[0.8 * math.cos(math.radians(4)), 0.6 * math.cos(math.radians(4)), math.sin(math.radians(4))])
+    elif case == "high_sun":
+        d = scene(sun=[0.3 * math.cos(math.radians(82)), -0.95 * math.cos(math.radians(82)), math.sin(math.radians(82))])
+    else:
+        d = scene(sun=[0.4, 0.3, 0.8])
+        c, s = math.cos(0.7), math.sin(0.7)
+        d["to_world"] = np.array([[1, 0, 0, 0], [0, c, -s, 0], [0, s, c, 0], [0, 0, 0, 1]], np.float32)
+    _vjp_vs_jvp(d, variant)
 
 
 @pytest.mark.gpu

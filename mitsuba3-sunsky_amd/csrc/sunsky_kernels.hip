@@ -3169,6 +3169,50 @@ __device__ __forceinline__ void stage_vjp(const SunskyKArgs& K, const float* vjp
     __syncthreads();
 }
 
+// The d gamma = 0 sky tangent is linear in d{A..I, rad}: sky_tan(dk) = sum_p W_p dk_p with
+// weights that depend on the ray and the channel only.  The reverse-mode kernels form W once
+// per channel and take the turbidity, albedo and unit-elevation tangents as 10-term dot
+// products (the same sums as sky_tan, reassociated).
+struct SkyTanW { float w[10]; };
+
+__device__ __forceinline__ SkyTanW sky_tan_weights(const SkyChannel& k, const DirTerms& t, const SkyVal& s) {
+    SkyTanW W;
+    const float c2r = s.c2 * k.rad, q = s.c1 * k.rad;
+    W.w[0] = c2r * s.e1;
+    W.w[1] = c2r * (k.A * s.e1 * t.r);
+    W.w[2] = q;
+    W.w[3] = q * s.e2;
+    W.w[4] = q * (k.D * s.e2 * t.gamma);
+    W.w[5] = q * t.cg2;
+    W.w[6] = q * s.chi;
+    W.w[7] = q * t.sq;
+    W.w[8] = q * (k.G * (-1.5f * s.chi * s.inv_b) * (2.f * k.I - 2.f * t.cg));   // d chi through d I
+    W.w[9] = s.c1 * s.c2;
+    return W;
+}
+
+__device__ __forceinline__ float sky_dot(const SkyTanW& W, const float* dk) {
+    float acc = W.w[0] * dk[0];
+#pragma unroll
+    for (int p = 1; p < 10; ++p) acc = fmaf(W.w[p], dk[p], acc);
+    return acc;
+}
+
+// One sky channel's reverse-mode terms: the tangents along turbidity, albedo and the unit
+// elevation (d gamma = 0), and the gamma part of the sun axes
+struct SkySide { float t, a, e, gm; };
+
+__device__ __forceinline__ SkySide sky_side(const SkyChannel& k, const VjpLds& L, int ch, const DirTerms& t, float sg) {
+    const SkyVal s = sky_val(k, t);
+    const SkyTanW W = sky_tan_weights(k, t, s);
+    SkySide r;
+    r.t = sky_dot(W, L.dsky[0] + ch * 10);
+    r.a = sky_dot(W, L.dsky[1] + ch * 10);
+    r.e = sky_dot(W, L.dsky[2] + ch * 10);
+    r.gm = sky_tan_gamma(k, t, s, sg);
+    return r;
+}
+
 __device__ __forceinline__ void eval_vjp_rgb_body(const SunskyKArgs& K, const float* __restrict__ vjp,
                                                   const float* __restrict__ wx, const float* __restrict__ wy,
                                                   const float* __restrict__ wz, const uint8_t* __restrict__ active,
@@ -3204,13 +3248,12 @@ __device__ __forceinline__ void eval_vjp_rgb_body(const SunskyKArgs& K, const fl
 #pragma unroll 1
         for (int c = 0; c < 3; ++c) {
             const float cot = dout[(size_t)c * ostride + i] * cie;
-            const SkyChannel& kc = K.sky[c];
-            const SkyVal sv = sky_val(kc, t);   // once for the 5 tangents
+            const SkySide S = sky_side(K.sky[c], L, c, t, sg);   // value terms once for the 5 tangents
             const float cs = cot * K.sky_scale;
-            g[0] += cs * sky_tan(kc, L.dsky[0] + c * 10, t, sv, 0.f, sg);
-            g[1 + c] += cs * sky_tan(kc, L.dsky[1] + c * 10, t, sv, 0.f, sg);
-            g[15] += cs * sky_tan(kc, L.dsky[2] + c * 10, t, sv, 0.f, sg);   // unit elevation
-            const float gam = sky_tan_gamma(kc, t, sv, sg);
+            g[0] += cs * S.t;
+            g[1 + c] += cs * S.a;
+            g[15] += cs * S.e;   // unit elevation
+            const float gam = S.gm;
 #pragma unroll
             for (int k = 0; k < 3; ++k) g[12 + k] += cs * gam * dgs[k];
             if (t.hit_sun) {
@@ -3275,30 +3318,20 @@ __device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const f
             float f = nw - (float)lo;
             const bool has_hi = f != 0.f && hi < kNbWavelengths;
             const float wlo = f != 0.f ? 1.f - f : 1.f, whi = f;   // lerp weights (f = 0: low channel only)
-            float da, db = 0.f;
             // turbidity, albedo (diagonal), sun axes: each lerped over the two channels; the
             // value terms of each channel once for its 5 tangents
-            const SkyChannel &klo = L.sky[lo], &khi = L.sky[has_hi ? hi : lo];
-            const SkyVal slo = sky_val(klo, t);
-            SkyVal shi = slo;
-            if (has_hi) shi = sky_val(khi, t);
-            da = sky_tan(klo, L.dsky[0] + lo * 10, t, slo, 0.f, sg);
-            if (has_hi) db = sky_tan(khi, L.dsky[0] + hi * 10, t, shi, 0.f, sg);
-            g[0] += cot * K.sky_scale * (wlo * da + whi * db);
-            da = sky_tan(klo, L.dsky[1] + lo * 10, t, slo, 0.f, sg);
-            g[1 + lo] += cot * K.sky_scale * wlo * da;
-            if (has_hi) {
-                db = sky_tan(khi, L.dsky[1] + hi * 10, t, shi, 0.f, sg);
-                g[1 + hi] += cot * K.sky_scale * whi * db;
-            }
-            db = 0.f;
-            da = sky_tan(klo, L.dsky[2] + lo * 10, t, slo, 0.f, sg);   // unit elevation
-            if (has_hi) db = sky_tan(khi, L.dsky[2] + hi * 10, t, shi, 0.f, sg);
-            g[15] += cot * K.sky_scale * (wlo * da + whi * db);
-            db = 0.f;
-            da = sky_tan_gamma(klo, t, slo, sg);
-            if (has_hi) db = sky_tan_gamma(khi, t, shi, sg);
-            const float gam = cot * K.sky_scale * (wlo * da + whi * db);
+            const SkySide A = sky_side(L.sky[lo], L, lo, t, sg);
+            // the two sides one after the other: hoisting the second side's table reads over
+            // the first holds both sets of weights and reads live (164 VGPRs, 3 waves/SIMD)
+            __builtin_amdgcn_sched_barrier(0);
+            SkySide B = {0.f, 0.f, 0.f, 0.f};
+            if (has_hi) B = sky_side(L.sky[hi], L, hi, t, sg);
+            const float cs = cot * K.sky_scale;
+            g[0] += cs * (wlo * A.t + whi * B.t);
+            g[1 + lo] += cs * wlo * A.a;
+            if (has_hi) g[1 + hi] += cs * whi * B.a;
+            g[15] += cs * (wlo * A.e + whi * B.e);   // unit elevation
+            const float gam = cs * (wlo * A.gm + whi * B.gm);
 #pragma unroll
             for (int k = 0; k < 3; ++k) g[12 + k] += gam * dgs[k];
             if (t.hit_sun) {
@@ -3587,7 +3620,10 @@ extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_vjp_rgb(
     size_t n, const float* dout, size_t ostride, float sign, float* partials) {
     eval_vjp_rgb_body(*Kp, vjp, wx, wy, wz, active, n, dout, ostride, sign, partials);
 }
-extern "C" __global__ __launch_bounds__(SS_BLOCK) void sunsky_eval_vjp_spec(
+#ifndef SS_VJP_SPEC_ATTR
+#define SS_VJP_SPEC_ATTR
+#endif
+extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_VJP_SPEC_ATTR void sunsky_eval_vjp_spec(
     const SunskyKArgs* __restrict__ Kp, const float* vjp, const float* wx, const float* wy, const float* wz, const float* lam,
     size_t lstride, int nlam, const uint8_t* active, size_t n, const float* dout, size_t ostride, float sign,
     float* partials) {

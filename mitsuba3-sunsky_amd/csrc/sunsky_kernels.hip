@@ -3640,7 +3640,18 @@ extern "C" __global__ __launch_bounds__(256) void sunsky_grad_reduce(const float
     __shared__ float seg[kSeg][kGradCount];
     const int p = threadIdx.x % kGradCount, sgi = threadIdx.x / kGradCount;
     float acc = 0.f;
-    for (unsigned b = sgi; b < nblocks; b += kSeg) acc += partials[(size_t)b * kGradCount + p];
+    // 16 loads in flight per thread, then the adds in block order (the summation order of
+    // the one-load-per-step loop, which waited out a load latency per block: 26 us per call)
+    constexpr unsigned kU = 16;
+    unsigned b = sgi;
+    for (; b + (kU - 1) * kSeg < nblocks; b += kU * kSeg) {
+        float v[kU];
+#pragma unroll
+        for (unsigned u = 0; u < kU; ++u) v[u] = partials[(size_t)(b + u * kSeg) * kGradCount + p];
+#pragma unroll
+        for (unsigned u = 0; u < kU; ++u) acc += v[u];
+    }
+    for (; b < nblocks; b += kSeg) acc += partials[(size_t)b * kGradCount + p];
     seg[sgi][p] = acc;
     __syncthreads();
     if (threadIdx.x < kGradCount) {

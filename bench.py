@@ -456,15 +456,55 @@ def parity_caller(kind, em, d_scene, nrm, out, seed, spp, vw=None, n_check=4096)
             "bounds": f"per-point p99.5 < {bound:g} (tests' bound; fp32 vs the oracle's fp64 BSDF / MIS terms)"}
 
 
+C5_SEED = 4321            # rank k's configs[4] batch: hemisphere_dirs(seed = C5_SEED + k)
+
+
+def c5_scene():
+    return dict(sun_dict(3.0), albedo=0.3)
+
+
+def parity_c5(planes, n5, world, dev, per_rank=1 << 14):
+    """configs[4] output parity on rank 0: for every rank k, a strided sample of per_rank
+    directions of k's batch plus every sun-disc direction in it (regenerated here from k's
+    seed), read from k's columns of the gathered (11, n5 * world) planes and compared with
+    the oracle at the DESIGN.md §6 bars.  A gather that put a shard at the wrong column
+    range or plane would fail here (the sampled columns would hold another rank's rays)."""
+    O = _oracle()
+    lams = np.arange(320, 721, 40, dtype=np.float32)
+    o32, o64 = O.Oracle(c5_scene(), "spectral", "jit", "f32"), O.Oracle(c5_scene(), "spectral", "jit", "f64")
+    inf = o32.info()
+    s = torch.tensor(inf["sun_dir_local"], dtype=torch.float32, device=dev)
+    parts, checked = [], 0
+    for k in range(world):
+        wi_k = -hemisphere_dirs(n5, seed=C5_SEED + k, device=dev)
+        disc = ((s[:, None] * -wi_k).sum(0) >= inf["cos_cutoff"]) & (wi_k[2] <= 0)
+        idx = torch.unique(torch.cat([torch.arange(0, n5, max(1, n5 // per_rank), device=dev),
+                                      disc.nonzero().flatten()]))
+        w = wi_k[:, idx].T.cpu().numpy()
+        got = planes[:, k * n5 + idx.to(planes.device)].T.cpu().numpy()
+        del wi_k, disc
+        lam = np.repeat(lams[:, None], w.shape[0], 1)
+        sun = (-w @ inf["sun_dir_local"] >= inf["cos_cutoff"]) & (w[:, 2] <= 0)
+        parts.append(lane_stats(got, o32.eval(w, lam).T, o64.eval(w, lam).T, sun))
+        checked += w.shape[0]
+    return dict(merge_stats(parts), checked_dirs=checked, ranks_checked=world,
+                sample=f"per rank: every {max(1, n5 // per_rank)}th direction + every sun-disc direction, "
+                       "x 11 nodes, read from that rank's columns of the gathered planes",
+                bound=f"sky: |gpu-o32| <= 1e-5|o32| + |o32-o64|; sun disc: |gpu-o64| <= 1e-5|o64| + "
+                      f"{SUN_SLACK[0]:g}|o32-o64|")
+
+
 def run_c5(args, world, rank, dev, coll_dev, rehearsal):
     """configs[4]: a --c5-dirs spectral batch per GPU (11 model
     wavelengths, the C3 node kernel), then the gather of every rank's (11, n) radiance
-    planes into rank 0's (11, N) planes.  Per-GPU eval time (max over ranks), whole-job
-    evals/s, gather time and GB/s; rank 0's own shard checked bitwise after the gather.
-    Returns the report on rank 0, None elsewhere."""
+    planes into rank 0's (11, N) planes through the C ABI (sunsky_gather_radiance; at one
+    rank the copy of the rank's own shard into the output planes).  Per-GPU eval time (max
+    over ranks), whole-job evals/s, gather time and GB/s; on rank 0 the own shard checked
+    bitwise after the gather and every rank's columns sampled against the oracle
+    (parity_c5).  Returns the report on rank 0, None elsewhere."""
     n5 = args.c5_dirs
-    wi5 = -hemisphere_dirs(n5, seed=4321 + rank, device=dev)
-    spec5 = ss.SunskyEmitter(dict(sun_dict(3.0), albedo=0.3), "spectral", precision=args.precision, device=dev)
+    wi5 = -hemisphere_dirs(n5, seed=C5_SEED + rank, device=dev)
+    spec5 = ss.SunskyEmitter(c5_scene(), "spectral", precision=args.precision, device=dev)
     lams = [float(x) for x in range(320, 721, 40)]
     out5 = torch.empty((11, n5), dtype=torch.float32, device=dev)
     for _ in range(2):
@@ -473,68 +513,112 @@ def run_c5(args, world, rank, dev, coll_dev, rehearsal):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    tm = KernelTimer()
     t0 = time.perf_counter()
+    tm.begin()
     for _ in range(reps):
         spec5.eval_spectral_broadcast(wi5, lams, out=out5)
+    tm.end(reps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     te = (time.perf_counter() - t0) / reps
-    tg, tcat, own_ok, gpath = 0.0, 0.0, True, None
+    kernel_ms = tm.mean_ms()
+    del wi5
+    tg, tcat, own_ok, gpath, full = 0.0, 0.0, True, None, None
     if world > 1:
-        from sunsky_amd.sharding import RadianceComm, gather_shards, shard_sizes
         t = torch.tensor([te], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         te = float(t.item())
-        tgs = []
-        if not rehearsal:
-            # C ABI gather (grouped RCCL send/recv) straight into rank 0's final planes
-            gpath = "sunsky_gather_radiance: RCCL send/recv into rank 0's (11, N) planes, no padding / concat"
-            comm = RadianceComm(device=dev)
-            full = torch.empty((11, n5 * world), dtype=torch.float32, device=dev) if rank == 0 else None
-            comm.gather(out5, n5 * world, out=full)         # untimed: connection setup
-            for _ in range(3):
-                torch.cuda.synchronize()
+    tgs = []
+    if not rehearsal:
+        # C ABI gather (grouped RCCL send/recv) straight into rank 0's final planes; one
+        # rank (no torch.distributed): its own shard copied into the output planes
+        from sunsky_amd.sharding import RadianceComm
+        gpath = ("sunsky_gather_radiance: RCCL send/recv into rank 0's (11, N) planes, no padding / concat"
+                 if world > 1 else "sunsky_gather_radiance, one rank: the shard copied into the (11, N) planes")
+        comm = RadianceComm(device=dev)
+        full = torch.empty((11, n5 * world), dtype=torch.float32, device=dev) if rank == 0 else None
+        comm.gather(out5, n5 * world, out=full)         # untimed: connection setup
+        for _ in range(3):
+            torch.cuda.synchronize()
+            if world > 1:
                 dist.barrier()
-                t0 = time.perf_counter()
-                comm.gather(out5, n5 * world, out=full)
-                torch.cuda.synchronize()
-                tgs.append(time.perf_counter() - t0)
-            if rank == 0:
-                own_ok = bool(torch.equal(full[:, :n5], out5))
-            comm.close()
-            del full
-        else:
-            gpath = "torch.distributed.gather of padded shards + torch.cat (gloo rehearsal)"
-            send = out5.to(coll_dev)
-            bufs = gather_shards(send, n5 * world)           # untimed: connection setup
-            for _ in range(3):                                 # the collective alone, preallocated
-                torch.cuda.synchronize()
-                dist.barrier()
-                t0 = time.perf_counter()
-                gather_shards(send, n5 * world, bufs=bufs)
-                torch.cuda.synchronize()
-                tgs.append(time.perf_counter() - t0)
-            if rank == 0:
-                t0 = time.perf_counter()
-                full = torch.cat([b[:, :s] for b, s in zip(bufs, shard_sizes(n5 * world, world))], dim=1)
-                torch.cuda.synchronize()
-                tcat = time.perf_counter() - t0
-                own_ok = bool(torch.equal(full[:, :n5].to(dev), out5))
-                del full
-            del bufs, send
-        tg = sorted(tgs)[1]
+            t0 = time.perf_counter()
+            comm.gather(out5, n5 * world, out=full)
+            torch.cuda.synchronize()
+            tgs.append(time.perf_counter() - t0)
+        comm.close()
+    else:
+        from sunsky_amd.sharding import gather_shards, shard_sizes
+        gpath = "torch.distributed.gather of padded shards + torch.cat (gloo rehearsal)"
+        send = out5.to(coll_dev)
+        bufs = gather_shards(send, n5 * world)           # untimed: connection setup
+        for _ in range(3):                                 # the collective alone, preallocated
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            gather_shards(send, n5 * world, bufs=bufs)
+            torch.cuda.synchronize()
+            tgs.append(time.perf_counter() - t0)
+        if rank == 0:
+            t0 = time.perf_counter()
+            full = torch.cat([b[:, :s] for b, s in zip(bufs, shard_sizes(n5 * world, world))], dim=1)
+            torch.cuda.synchronize()
+            tcat = time.perf_counter() - t0
+        del bufs, send
+    tg = sorted(tgs)[1]
+    report = None
     if rank == 0:
-        nbytes = 11 * n5 * 4 * (world - 1)
-        return {
-            "dirs_per_gpu": n5, "lambdas": 11, "eval_s": te,
+        own_ok = bool(torch.equal(full[:, :n5].to(dev), out5))
+        del out5
+        nbytes = 11 * n5 * 4 * max(world - 1, 1)
+        parity = parity_c5(full, n5, world, dev)
+        report = {
+            "dirs_per_gpu": n5, "lambdas": 11, "eval_s": te, "eval_kernel_ms": kernel_ms,
             "evals_per_s_whole_job": 11 * n5 * world / te,
+            "eval_achieved_GBps": BYTES_SPEC_PER_DIR * n5 / (kernel_ms * 1e-3) / 1e9,
             "gather_s": tg, "gather_bytes_to_root": nbytes, "gather_GBps": nbytes / tg / 1e9 if tg else None,
+            "gather_bytes_note": ("bytes received by rank 0 from the other ranks" if world > 1 else
+                                  "one rank: the device-to-device copy of the own shard into the planes"),
             "gather_path": gpath,
             "gather_timing": "median of 3 gathers into preallocated buffers after one untimed call",
             "reassemble_planes_s": tcat, "end_to_end_s": te + tg + tcat, "bitwise_own_shard": own_ok,
+            "parity": parity,
             "note": "configs[4]: per-GPU spectral eval (weak scaling) then gather of the radiance to rank 0"}
-    return None
+    del full
+    return report
+
+
+class C5Watchdog:
+    """A rank whose communicator setup fails leaves the others waiting in a collective
+    (RCCL init, a barrier).  Past `limit_s` rank 0 prints the bench line with the C5 error
+    (the measured `value` is kept) and EVERY rank exits with EXIT_CODE: a process that has
+    touched the GPU and hung is never reported as a success."""
+    EXIT_CODE = 3
+    KEY = "c5_spectral_shard_gather"
+
+    def __init__(self, limit_s, rank, result):
+        import threading
+        self.limit_s, self.rank, self.result, self.printed = limit_s, rank, result, False
+        self.timer = threading.Timer(limit_s, self._fire)
+        self.timer.daemon = True
+
+    def start(self):
+        self.timer.start()
+        return self
+
+    def cancel(self):
+        self.timer.cancel()
+
+    def _fire(self):
+        if self.rank == 0 and not self.printed and self.result is not None:
+            self.result[self.KEY] = {"error": f"timed out after {self.limit_s:.0f} s (a rank stuck in a collective); "
+                                              f"value is unaffected; every rank exits {self.EXIT_CODE}"}
+            print(json.dumps(self.result), flush=True)
+        sys.stderr.write(f"bench.py rank {self.rank}: configs[4] timed out after {self.limit_s:.0f} s\n")
+        sys.stderr.flush()
+        os._exit(self.EXIT_CODE)
 
 
 def main():
@@ -548,13 +632,12 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather of the radiance to rank 0")
     ap.add_argument("--no-pmc", action="store_true", help="do not read the committed PMC traffic summary")
-    ap.add_argument("--c5", action="store_true",
-                    help="also run configs[4]: spectral 11-lambda eval of --c5-dirs per GPU + gather to rank 0 "
-                         "(default on when more than one rank runs; --no-c5 turns it off)")
-    ap.add_argument("--no-c5", action="store_true")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip configs[4] (spectral 11-lambda eval of --c5-dirs per GPU + gather to rank 0, "
+                         "with its parity block; on by default at every N)")
     ap.add_argument("--headline-only", action="store_true",
                     help="run the settle, warmup and timed headline steps only (for a rocprof trace of the burst)")
-    ap.add_argument("--c5-dirs", type=int, default=1 << 26, help="directions per GPU for --c5 (default 64M)")
+    ap.add_argument("--c5-dirs", type=int, default=1 << 26, help="configs[4] directions per GPU (default 64M)")
     args = ap.parse_args()
     SUN_SLACK[0] = 4.0 if args.precision == "reference" else 1.25
 
@@ -1019,24 +1102,10 @@ def main():
         del full
 
     # ------------------------------------------- configs[4]: spectral shard + gather
-    watchdog, printed = None, False
-    if (args.c5 or world > 1) and not args.no_c5:
+    watchdog = None
+    if not args.no_c5:
         del outs
-        # A rank whose communicator setup fails leaves the others waiting in a collective
-        # (RCCL init, a barrier).  The watchdog keeps that from costing the bench line: past
-        # the limit rank 0 prints the line with the C5 error and every rank exits 0.
-        import threading
-
-        def c5_timeout():
-            if rank == 0 and not printed:
-                result["c5_spectral_shard_gather"] = {"error": f"timed out after {c5_limit:.0f} s (a rank stuck in "
-                                                               "a collective); value is unaffected"}
-                print(json.dumps(result), flush=True)
-            os._exit(0)
-        c5_limit = float(os.environ.get("SUNSKY_BENCH_C5_TIMEOUT", "150"))
-        watchdog = threading.Timer(c5_limit, c5_timeout)
-        watchdog.daemon = True
-        watchdog.start()
+        watchdog = C5Watchdog(float(os.environ.get("SUNSKY_BENCH_C5_TIMEOUT", "150")), rank, result).start()
         try:
             c5 = run_c5(args, world, rank, dev, coll_dev, rehearsal)
         except Exception as exc:   # reported beside `value`; never fail the bench line
@@ -1049,12 +1118,11 @@ def main():
         if not args.no_cpu and world == 1:   # the CPU baseline: rank 0 at N=1 only
             result["cpu_baseline"] = cpu_baseline(wi.T.cpu().numpy())
         print(json.dumps(result), flush=True)
-        printed = True
     if world > 1:
+        from sunsky_amd.sharding import clear_radiance_comms
+        clear_radiance_comms()
         dist.barrier()
         dist.destroy_process_group()
-    if watchdog is not None:
-        watchdog.cancel()
 
 
 if __name__ == "__main__":

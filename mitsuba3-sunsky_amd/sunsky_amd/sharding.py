@@ -63,16 +63,34 @@ def gather_shards(local, n_total, dst=0, group=None, bufs=None):
 _COMMS = {}
 
 
+def _group_key(group, dev):
+    """Cache key of a communicator: the group object, the device and the group's current
+    rank / size, so a re-initialised world (destroy_process_group + init) never reuses a
+    communicator built for the old one."""
+    if not dist.is_available() or not dist.is_initialized():
+        return (None, dev.index, 0, 1)
+    return (id(group) if group is not None else None, dev.index, dist.get_rank(group), dist.get_world_size(group))
+
+
 def radiance_comm(group=None, device=None):
     """The process's RadianceComm for (group, device), created on first use and kept: a
     communicator costs an RCCL init plus connection setup, far more than one gather.
     Collective on first use (every rank of the group calls it)."""
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-    key = (id(group) if group is not None else None, dev.index)
+    key = _group_key(group, dev)
     comm = _COMMS.get(key)
     if comm is None or comm._h is None:
         comm = _COMMS[key] = RadianceComm(group, dev)
     return comm
+
+
+def clear_radiance_comms():
+    """Close every cached communicator (call before dist.destroy_process_group(): RCCL
+    communicators must not outlive the world they were built for, nor run their
+    destructors after RCCL itself is gone at interpreter teardown)."""
+    while _COMMS:
+        _, comm = _COMMS.popitem()
+        comm.close()
 
 
 def gather_radiance(local, n_total, dst=0, group=None, comm=None, out=None):
@@ -97,14 +115,21 @@ class RadianceComm:
 
     def __init__(self, group=None, device=None):
         self.group = group
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
+        single = not dist.is_available() or not dist.is_initialized()
+        if single and group is not None:
+            raise ValueError("a process group was given but torch.distributed is not initialised")
+        # without torch.distributed the communicator is the process alone (world 1, rank 0):
+        # a one-GPU job gathers its own shard into the output planes through the same call
+        self.rank = 0 if single else dist.get_rank(group)
+        self.world = 1 if single else dist.get_world_size(group)
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         uid = C.create_string_buffer(128)
         if self.rank == 0:
             check(lib().sunsky_comm_get_unique_id(uid))
         box = [bytes(uid.raw)]
-        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        if not single:
+            dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                       group=group)
         h = C.c_void_p()
         with torch.cuda.device(self.device):
             check(lib().sunsky_comm_create(box[0], self.world, self.rank, C.byref(h)))

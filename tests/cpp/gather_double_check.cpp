@@ -7,12 +7,18 @@
 // (shard_range's 4-aligned split), RGB eval (3 planes) and the C3 node kernel (11
 // planes), root first or last, ranks calling in either order.  Exit 0 when every
 // gathered buffer equals the whole batch evaluated alone, bit for bit.
+//
+// `gather_double_check c5 [world] [rays_per_rank]` runs the same check at configs[4]'s
+// sizes instead: `world` ranks (default 4) of 64M rays x the 11 node wavelengths each,
+// so the root's planes hold more than 2^31 floats (plane offsets past 2^33 bytes), every
+// shard evaluated on its own and gathered, then compared with the whole batch bitwise.
 #include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <vector>
@@ -54,7 +60,93 @@ static int eval(sunsky_emitter* em, bool spec, const float* wi, size_t stride, s
 
 extern "C" int ncclGetUniqueId(void*);   // the double this program links
 
-int main() {
+// configs[4] sizes: world x n rays x 11 planes; the inputs tile a host pattern whose length
+// (2^20 + 7) divides neither a shard nor a plane, so a shard landing at a wrong column range
+// or plane would not compare equal by accident
+static int run_c5(sunsky_emitter* spec, int world, size_t per) {
+    const int np = 11;
+    const size_t n = per * world, tile = (1u << 20) + 7;
+    std::printf("c5: %d ranks x %zu rays x %d planes: root planes %zu floats (%.2f GB)\n", world, per, np,
+                (size_t)np * n, np * n * 4.0 / 1e9);
+    std::fflush(stdout);
+    std::vector<float> h(3 * tile);
+    std::mt19937 rng(4321);
+    std::uniform_real_distribution<float> U(0.f, 1.f);
+    for (size_t i = 0; i < tile; ++i) {
+        float ct = U(rng), ph = 6.2831853f * U(rng), st = std::sqrt(std::max(0.f, 1 - ct * ct));
+        h[i] = -st * std::cos(ph); h[tile + i] = -st * std::sin(ph); h[2 * tile + i] = -ct;
+    }
+    float *wi, *whole, *out;
+    HK(hipMalloc(&wi, 3 * n * 4));
+    for (int c = 0; c < 3; ++c)
+        for (size_t i = 0; i < n; i += tile)
+            HK(hipMemcpy(wi + c * n + i, h.data() + c * tile, std::min(tile, n - i) * 4, hipMemcpyHostToDevice));
+    HK(hipMalloc(&whole, (size_t)np * n * 4));
+    if (eval(spec, true, wi, n, n, whole)) return 2;
+    unsigned char uid[SUNSKY_COMM_ID_BYTES];
+    CK(sunsky_comm_get_unique_id(uid));
+    std::vector<sunsky_comm*> comms(world);
+    for (int r = 0; r < world; ++r) CK(sunsky_comm_create(uid, world, r, &comms[r]));
+    std::vector<hipStream_t> streams(world);
+    for (auto& st : streams) HK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    std::vector<float*> shard(world, nullptr);
+    std::vector<size_t> counts(world);
+    for (int r = 0; r < world; ++r) {
+        size_t a, b;
+        shard_range(n, r, world, &a, &b);
+        counts[r] = b - a;
+        float* wr;
+        HK(hipMalloc(&wr, 3 * counts[r] * 4));
+        for (int c = 0; c < 3; ++c)
+            HK(hipMemcpy(wr + c * counts[r], wi + c * n + a, counts[r] * 4, hipMemcpyDeviceToDevice));
+        HK(hipMalloc(&shard[r], (size_t)np * counts[r] * 4));
+        if (eval(spec, true, wr, counts[r], counts[r], shard[r])) return 2;
+        HK(hipDeviceSynchronize());
+        (void)hipFree(wr);
+    }
+    (void)hipFree(wi);
+    HK(hipMalloc(&out, (size_t)np * n * 4));
+    const size_t chunk = (size_t)1 << 26;   // compared through pinned 256 MB host buffers
+    float *ha, *hb;
+    HK(hipHostMalloc(&ha, chunk * 4, 0));
+    HK(hipHostMalloc(&hb, chunk * 4, 0));
+    int cases = 0;
+    for (int root : {0, world - 1}) {
+        const bool rev = root != 0;
+        HK(hipMemset(out, 0xff, (size_t)np * n * 4));   // NaN
+        HK(hipDeviceSynchronize());
+        for (int k = 0; k < world; ++k) {
+            const int r = rev ? world - 1 - k : k;
+            CK(sunsky_gather_radiance(comms[r], root, shard[r], counts[r], np, counts.data(), r == root ? out : nullptr,
+                                      r == root ? n : 0, streams[r]));
+        }
+        HK(hipDeviceSynchronize());
+        for (size_t off = 0; off < (size_t)np * n; off += chunk) {
+            const size_t m = std::min(chunk, (size_t)np * n - off);
+            HK(hipMemcpy(ha, out + off, m * 4, hipMemcpyDeviceToHost));
+            HK(hipMemcpy(hb, whole + off, m * 4, hipMemcpyDeviceToHost));
+            if (std::memcmp(ha, hb, m * 4) != 0) {
+                std::printf("c5 root %d: gathered planes differ in floats [%zu, %zu) (plane %zu)\n", root, off,
+                            off + m, off / n);
+                return 1;
+            }
+        }
+        ++cases;
+        std::printf("c5 case %d: world %d root %d order %d: %zu floats bitwise equal\n", cases, world, root, (int)rev,
+                    (size_t)np * n);
+        std::fflush(stdout);
+    }
+    (void)hipHostFree(ha); (void)hipHostFree(hb);
+    for (float* x : shard) (void)hipFree(x);
+    (void)hipFree(out); (void)hipFree(whole);
+    for (auto* c : comms) sunsky_comm_destroy(c);
+    for (auto st : streams) (void)hipStreamDestroy(st);
+    std::printf("c5 gather through the RCCL double: %d cases bitwise equal\n", cases);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    const bool c5 = argc > 1 && std::strcmp(argv[1], "c5") == 0;
     // the product resolves RCCL with dlopen("librccl.so.1"): it must get the double, or the
     // communicators below would be real ones waiting for ranks that never come
     void* so = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
@@ -76,6 +168,19 @@ int main() {
     CK(sunsky_emitter_create(p, 1, 0, nullptr, &spec));
     std::printf("emitters staged\n");
     std::fflush(stdout);
+    if (c5) {
+        const int world = argc > 2 ? std::atoi(argv[2]) : 4;
+        const size_t per = argc > 3 ? (size_t)std::atoll(argv[3]) : ((size_t)1 << 26);
+        if (world < 2 || world > 16 || per < 4 || per % 4) {
+            std::fprintf(stderr, "c5: world in [2, 16], rays per rank a positive multiple of 4\n");
+            return 5;
+        }
+        const int rc = run_c5(spec, world, per);
+        sunsky_emitter_destroy(rgb);
+        sunsky_emitter_destroy(spec);
+        sunsky_props_destroy(p);
+        return rc;
+    }
     int cases = 0;
     for (int world = 2; world <= 4; ++world) {
         unsigned char uid[SUNSKY_COMM_ID_BYTES];

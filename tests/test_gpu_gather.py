@@ -109,3 +109,22 @@ def test_multi_rank_gather_through_rccl_double():
     print(p.stdout)
     assert p.returncode == 0, p.stdout
     assert "48 cases bitwise equal" in p.stdout
+
+
+def test_c5_sized_gather_through_rccl_double():
+    """configs[4] at its own sizes: 4 ranks x 64M rays x the 11 node planes,
+    each shard evaluated by the C3 node kernel on its own and gathered through the grouped
+    send / recv branch into the root's (11, 256M) planes -- 2.95e9 floats, plane offsets past
+    2^33 bytes -- then every gathered float compared with the whole batch evaluated alone,
+    bitwise, for root 0 and root 3 (ranks calling in reverse order).  ~45 GB of HBM."""
+    if torch.cuda.get_device_properties(0).total_memory < (64 << 30):
+        pytest.skip("needs > 64 GiB of device memory")
+    exe = os.path.join(ROOT, "tests", "cpp", "build", "gather_double_check")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "cpp"), "build/gather_double_check"], check=True,
+                       capture_output=True)
+    p = subprocess.run([exe, "c5", "4", str(1 << 26)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=240)
+    print(p.stdout)
+    assert p.returncode == 0, p.stdout
+    assert "c5 gather through the RCCL double: 2 cases bitwise equal" in p.stdout

@@ -636,6 +636,48 @@ def test_full_size_c4_sampling_64M():
     assert_parity(gw[up], w32[up], w64[up], disc_lanes(gd, info)[up], rtol=2e-5)
 
 
+def test_full_size_c5_per_rank_leg_64M_x11_and_one_rank_gather():
+    """BASELINE configs[4]'s per-rank leg at full size on one GPU: 67,108,864
+    directions x the 11 node wavelengths through the C3 node kernel on the C5 emitter (T = 3,
+    albedo 0.3, sun at 45 deg), then the one-rank C-ABI gather (sunsky_gather_radiance) of the
+    (11, 64M) shard into the output planes.  Every lane finite, the gathered planes bitwise
+    the shard, and every 64th direction plus every sun-disc direction of the batch against
+    the oracle at the DESIGN.md §6 bars."""
+    from sunsky_amd.sharding import RadianceComm
+    n = 1 << 26
+    d = angles_dict(3.0, 0.0, np.deg2rad(45), 0.3, 1.0, 1.0)
+    g = torch.Generator(device="cuda").manual_seed(4321)
+    u = torch.rand((2, n), generator=g, device="cuda")
+    st = torch.sqrt(torch.clamp(1 - u[0] * u[0], min=0))
+    wo = torch.stack([st * torch.cos(2 * np.pi * u[1]), st * torch.sin(2 * np.pi * u[1]), u[0]]).contiguous()
+    del u, st
+    em = ss.SunskyEmitter(d, "spectral")
+    nodes = [float(x) for x in range(320, 721, 40)]
+    out = em.eval_spectral_broadcast(-wo, nodes)                      # (11, n)
+    assert bool(torch.isfinite(out).all())
+    comm = RadianceComm()
+    try:
+        full = comm.gather(out, n)
+    finally:
+        comm.close()
+    torch.cuda.synchronize()
+    assert full.shape == (11, n) and torch.equal(full, out)
+    del full
+    o32, o64 = O.Oracle(d, "spectral", "jit", "f32"), O.Oracle(d, "spectral", "jit", "f64")
+    inf = o32.info()
+    s = torch.tensor(inf["sun_dir_local"], dtype=torch.float32, device="cuda")
+    disc = ((s[:, None] * wo).sum(0) >= inf["cos_cutoff"]) & (wo[2] >= 0)
+    idx = torch.unique(torch.cat([torch.arange(0, n, 64, device="cuda"), disc.nonzero().flatten()]))
+    wh, got = host(wo[:, idx]).T, host(out[:, idx]).T
+    del out, wo
+    lam = np.repeat(np.asarray(nodes, np.float32)[:, None], wh.shape[0], 1)
+    sm = sun_mask(o32, wh)
+    assert sm.sum() > 300          # ~1e-5 of 64M directions hit the disc
+    st = assert_parity(got, o32.eval(-wh, lam).T, o64.eval(-wh, lam).T, sm)
+    print(f"C5 per-rank leg: {wh.shape[0]} directions x 11 checked, {int(sm.sum())} sun-disc; "
+          f"sky max rel vs o32 {st['sky_max_rel_vs_o32']:.2e}, sun max rel vs o64 {st['sun_max_rel_vs_o64']:.2e}")
+
+
 @pytest.mark.parametrize("precision", PRECISIONS)
 def test_full_size_c4_spectral_sampling_64M_x4(precision):
     """BASELINE config 4 in the spectral variants Mitsuba renders with (sunsky.cpp:430-439,

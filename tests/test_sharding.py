@@ -66,3 +66,31 @@ def test_gloo_world2_gather_matches_single_process(tmp_path, n):
     got = np.load(out)
     assert got.shape == ref.shape
     assert np.array_equal(got, ref)
+
+
+def _key_worker(rank, world, port, out_path):
+    from sunsky_amd.sharding import _group_key
+    dev = torch.device("cuda", 0)               # a device object only: no GPU is touched
+    keys = [_group_key(None, dev)]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    keys.append(_group_key(None, dev))
+    dist.destroy_process_group()
+    keys.append(_group_key(None, dev))
+    if rank == 1:
+        np.save(out_path, np.array(keys, dtype=object), allow_pickle=True)
+
+
+def test_comm_cache_key_tracks_the_world(tmp_path):
+    """the cached RCCL communicator is keyed by the group's rank and size, so a
+    re-initialised world (destroy_process_group + init) never reuses one built for another
+    world, and a process without torch.distributed gets its own world-1 key."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "keys.npy")
+    mp.start_processes(_key_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    keys = [tuple(k) for k in np.load(out, allow_pickle=True)]
+    assert keys[0] == (None, 0, 0, 1) and keys[2] == keys[0]
+    assert keys[1] == (None, 0, 1, 2)

@@ -57,10 +57,13 @@ HW_DIR = os.path.join(REF, "include/mitsuba/render/sunsky")
 @pytest.mark.skipif(not os.path.isdir(HW_DIR), reason="Hosek-Wilkie data headers not present (GPU box)")
 def test_datasets_regenerated_from_hosek_wilkie_headers_are_bit_exact(tmp_path):
     """tools/mk_hw_datasets.py restates sunsky.h:600-932; its output must be the shipped files
-    byte for byte, and the pack's entries must hold the same numbers."""
+    byte for byte, and the pack's entries must hold the same numbers.  All 7 Hosek-Wilkie
+    tables, including the derived RGB sun table behind every RGB sun-disc lane
+    (write_sun_data_rgb, sunsky.h:716-770: linear_rgb_rec over the CIE table of
+    src/core/spectrum.cpp:158); with the TGMM test above, all 8 shipped files."""
     from mk_hw_datasets import generate
     names = generate(HW_DIR, str(tmp_path))
-    assert len(names) == 6
+    assert len(names) == 7 and "sun_rgb_rad.bin" in names
     for name in names:
         assert (tmp_path / name).read_bytes() == open(os.path.join(REF, "resources/sunsky/datasets", name), "rb").read()
         np.testing.assert_array_equal(ss.array_from_file(tmp_path / name), read_pack_entry(name[:-4]))

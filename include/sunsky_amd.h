@@ -161,8 +161,14 @@ int sunsky_emitter_get_param(const sunsky_emitter *e, const char *name, float *o
  * An update the device staging rejects (a negative wavelength-distribution node, as
  * ContinuousDistribution's constructor checks) is reported by the next call that reads
  * the state back (get_info / get_table / the blocking form), which restores and restages
- * the previous parameters. */
+ * the parameters of the last staging known to be accepted (every update queued since that
+ * read-back is rolled back: the rejection status is sticky across stagings, so one
+ * rejected update among several queued ones is never lost). */
 int sunsky_emitter_parameters_changed_async(sunsky_emitter *e, void *stream);
+/* TESTING ONLY (tests/test_graph_capture.py): the next `count` device stagings of `e`
+ * report a rejected wavelength distribution, so the rollback path above can be exercised
+ * without a parameter set that produces one.  0 turns it off. */
+int sunsky_emitter_inject_staging_fault(sunsky_emitter *e, int count);
 /* Blocking form: _async on the default (null) stream, then waits for the staging. */
 int sunsky_emitter_parameters_changed(sunsky_emitter *e);
 /* set_scene(), sunsky.cpp:287-301: bounding sphere of the scene bbox */

@@ -303,7 +303,8 @@ struct sunsky_emitter {
     hipEvent_t ring_ev[kRing] = {};
     bool ring_used[kRing] = {};
     int ring_i = 0;
-    bool restoring = false;                    // restaging the previous state after a rejection
+    bool restoring = false;                    // restaging the accepted state after a rejection
+    int inject_faults = 0;                     // testing: stagings left that report a rejection
     mutable hipEvent_t stage_done = nullptr;   // recorded after the last device staging
     mutable float* d_jvp = nullptr;   // eval_jvp tangent tables (layout: sunsky_kernels.hip)
     mutable float* d_vjp = nullptr;   // eval_vjp basis-tangent tables
@@ -419,8 +420,10 @@ struct sunsky_emitter {
             hip_check(hipModuleLaunchKernel(mod->quad_finish, 1, 1, 1, 256, 1, 1, 0, s, qargs, nullptr),
                       "hipModuleLaunchKernel(sunsky_stage_quad_finish)");
         }
-        if (const char* f = std::getenv("SUNSKY_AMD_FAULT_STAGE_STATUS"))   // test fault injection
-            if (*f == '1' && model->semantics() == kJit && !restoring) hip_check(hipMemsetAsync(d_status, 1, 1, s), "hipMemsetAsync");
+        if (inject_faults > 0 && model->semantics() == kJit && !restoring) {   // sunsky_emitter_inject_staging_fault
+            --inject_faults;
+            hip_check(hipMemsetAsync(d_status, 1, 1, s), "hipMemsetAsync");
+        }
         hip_check(hipEventRecord(stage_done, s), "hipEventRecord");
         ++rev;
     }
@@ -439,16 +442,20 @@ struct sunsky_emitter {
         hip_check(hipMemcpy(&status, d_status, sizeof(int), hipMemcpyDeviceToHost), "hipMemcpy");
         auto* self = const_cast<sunsky_emitter*>(this);
         if (status) {
-            // The device staging rejected the update (a negative wavelength-distribution
-            // node, the check of ContinuousDistribution's constructor).  As the reference
-            // throws from parameters_changed and keeps its old state: restore the previous
-            // committed parameters, restage them, and report the error once, here.
+            // A device staging since the last read-back rejected its update (a negative
+            // wavelength-distribution node, the check of ContinuousDistribution's
+            // constructor); the status is sticky, so which one is unknown.  As the reference
+            // throws from parameters_changed and keeps its old state: restore the parameters
+            // of the last staging known to be accepted, restage them, report the error once.
             hip_check(hipMemset(d_status, 0, sizeof(int)), "hipMemset");
-            if (restoring)   // the restored state itself is rejected (e.g. at creation)
+            if (restoring || !model->has_accepted())   // the accepted state itself is rejected (e.g. at creation)
                 throw std::runtime_error("ContinuousDistribution: entries must be non-negative!");
-            model->revert_last_commit();
+            model->revert_to_accepted();
             self->restoring = true;
             try {
+                // batch kernels queued on any stream may still read d_state: let them drain
+                // before it is rewritten (a rare error path; no stream of the caller is known)
+                hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
                 self->stage_async(nullptr);
                 hip_check(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
                 sync_host();
@@ -458,8 +465,9 @@ struct sunsky_emitter {
             }
             self->restoring = false;
             throw std::runtime_error("ContinuousDistribution: entries must be non-negative! (update rejected by the "
-                                     "device staging; the previous parameters were restored)");
+                                     "device staging; the parameters of the last accepted update were restored)");
         }
+        model->mark_accepted();
         model->adopt_device_stage(dk, st.data());
         const SunskyKArgs& hk = model->kargs();
         std::memcpy(self->kargs.sky, hk.sky, sizeof(hk.sky));
@@ -650,6 +658,13 @@ int sunsky_emitter_parameters_changed_async(sunsky_emitter* e, void* stream) {
             e->kargs = e->model->kargs();
         }
     });
+}
+
+int sunsky_emitter_inject_staging_fault(sunsky_emitter* e, int count) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (count < 0) return fail(SUNSKY_ERROR_INVALID_VALUE, "count must be >= 0");
+    e->inject_faults = count;
+    return SUNSKY_OK;
 }
 
 int sunsky_emitter_parameters_changed(sunsky_emitter* e) {

@@ -3732,7 +3732,7 @@ struct QuadArgs {                  // mirrors the host-side struct (sunsky_capi.
     int nq, nch;
     float cie_y[kNbWavelengths];
     float sky_scale, sun_scale;
-    int* status;                   // 0 ok, 1 negative wavelength-distribution entry
+    int* status;                   // set to 1 by a rejected staging (negative wavelength-distribution entry)
 };
 
 // Workgroup j = quadrature row j, thread i = point (i, j): its direction terms once,
@@ -3791,6 +3791,6 @@ extern "C" __global__ __launch_bounds__(256) void sunsky_stage_quad_finish(QuadA
     __syncthreads();
     if (c == 0) {
         const bool ok = quad_finish(A.state, sky, sun, A.cie_y, A.sky_scale, A.sun_scale);
-        *A.status = ok ? 0 : 1;
+        if (!ok) *A.status = 1;   // sticky until the host reads it back (sync_host)
     }
 }

@@ -232,7 +232,6 @@ SunskyModel::SunskyModel(const Properties& props, int variant, int semantics, co
     k_.bs_center[0] = k_.bs_center[1] = k_.bs_center[2] = 0.f;   // unit bounding sphere until set_scene
     k_.bs_radius = 1.f;
     commit();
-    previous_ = committed_;   // nothing before the construction to go back to
 
     std::vector<std::string> unq = props.unqueried();
     if (!unq.empty()) {
@@ -751,7 +750,6 @@ void SunskyModel::parameters_changed(bool radiance_on_host) {
 }
 
 void SunskyModel::commit() {
-    previous_ = committed_;
     Snapshot& c = committed_;
     c.turbidity = turbidity_; c.sky_scale = sky_scale_; c.sun_scale = sun_scale_;
     c.albedo = albedo_; c.time = time_; c.location = location_;
@@ -781,8 +779,8 @@ void SunskyModel::rollback() {
     radiance_stale_ = c.radiance_stale;
 }
 
-void SunskyModel::revert_last_commit() {
-    committed_ = previous_;
+void SunskyModel::revert_to_accepted() {
+    committed_ = accepted_;
     rollback();
 }
 

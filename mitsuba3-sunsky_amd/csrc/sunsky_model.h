@@ -79,7 +79,11 @@ public:
     void adopt_device_stage(const SunskyKArgs& device_kargs, const float* sun_table);
     // The device staging rejected the last committed update: make the commit before it the
     // committed state again and restore it (the caller restages the device).
-    void revert_last_commit();
+    // The device staging's verdict, known only at a read-back: mark_accepted records the
+    // committed state as accepted; revert_to_accepted restores the last such state.
+    void mark_accepted() { accepted_ = committed_; has_accepted_ = true; }
+    bool has_accepted() const { return has_accepted_; }
+    void revert_to_accepted();
     // Drop parameter values set since the last commit (an update refused before staging).
     void discard_pending() { rollback(); }
     static void quadrature_nodes(std::vector<float>* x, std::vector<float>* w);
@@ -133,7 +137,8 @@ private:
         SunskyKArgs k;
         bool radiance_stale;
     };
-    Snapshot committed_, previous_;
+    Snapshot committed_, accepted_;
+    bool has_accepted_ = false;
     void commit();
     void rollback();
 };

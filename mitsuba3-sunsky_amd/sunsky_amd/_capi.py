@@ -67,6 +67,7 @@ _SIGS = {
     "sunsky_emitter_set_param": (C.c_int, [vp, C.c_char_p, c_float_p, C.c_int]),
     "sunsky_emitter_parameters_changed": (C.c_int, [vp]),
     "sunsky_emitter_parameters_changed_async": (C.c_int, [vp, vp]),
+    "sunsky_emitter_inject_staging_fault": (C.c_int, [vp, C.c_int]),
     "sunsky_emitter_get_param": (C.c_int, [vp, C.c_char_p, c_float_p, C.c_int, C.POINTER(C.c_int)]),
     "sunsky_emitter_set_scene": (C.c_int, [vp, C.c_int, c_float_p, C.c_float]),
     "sunsky_emitter_set_precision": (C.c_int, [vp, C.c_int]),

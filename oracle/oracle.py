@@ -318,6 +318,12 @@ def set_threads(n):
     lib().oracle_set_threads(int(n))
 
 
+def set_quadrature_sum(sequential):
+    """estimate_sky_sun_ratio's 40,000-term sums (sunsky.cpp:815, 849): False (default) adds
+    the fp32 terms exactly, True one by one in fp32 (affects Oracles created afterwards)."""
+    lib().oracle_set_quadrature_sum(int(bool(sequential)))
+
+
 def get_threads():
     return lib().oracle_get_threads()
 

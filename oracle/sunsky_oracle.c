@@ -226,6 +226,16 @@ void oracle_sun_coordinates(int year, int month, int day, float hour, float minu
     out[2] = cosf(theta);
 }
 
+/* estimate_sky_sun_ratio's two 40,000-term sums (dr::sum_inner, sunsky.cpp:815, 849).
+   Dr.Jit leaves the reduction order to its backend (LLVM: blocked SIMD partial sums,
+   CUDA: a tree), so the oracle's default adds the fp32 terms exactly (an fp64
+   accumulator, rounded once): the order-independent value every reasonable reduction
+   approximates.  1 = the terms added one by one in R, the worst-case order (the
+   round-1..3 restatement), kept for reporting. */
+static int g_quad_sum_sequential = 0;
+void oracle_set_quadrature_sum(int sequential) { g_quad_sum_sequential = sequential != 0; }
+int oracle_get_quadrature_sum(void) { return g_quad_sum_sequential; }
+
 /* -------------------------------------------------- precision instantiation */
 #define R float
 #define SFX f32

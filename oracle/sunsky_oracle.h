@@ -66,6 +66,9 @@ typedef struct oracle_info {
 
 const char *oracle_last_error(void);
 void oracle_set_threads(int n);
+/* estimate_sky_sun_ratio's sums: 0 (default) the fp32 terms added exactly, 1 sequentially in R */
+void oracle_set_quadrature_sum(int sequential);
+int oracle_get_quadrature_sum(void);
 int  oracle_get_threads(void);
 
 /* Restated helper exposed for tests: Gauss-Legendre nodes (quad.h:27-86). */

@@ -285,3 +285,55 @@ def test_device_tangent_staging_is_the_host_tangent_bitwise(variant, rotated):
         p["turbidity"] = 7.25
         p["albedo"] = 0.55
         p.update()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+def test_sun_disc_tangent_along_sun_direction(variant):
+    """the sun-disc part of the sun_direction tangent -- d cos(psi) / d s in the
+    limb darkening (sunsky.cpp:631-650) and, for RGB, in the cos(psi) powers of render_sun
+    (:572-614), through gamma = unit_angle(s, wo) (:311) -- on lanes well inside the disc,
+    alpha/32 <= gamma <= alpha/4 (alpha/2 = the half aperture), which the sun_direction check
+    above masks out.  The step h = 1e-4 along tangents orthogonal to s cannot flip the disc
+    test there (alpha/4 = 2.3e-3), and the disc radiance is a smooth function of cos(gamma)
+    on the scale of the aperture, so the central differences of the fp64 oracle are accurate
+    to (h / (alpha/2))^2 ~ 5e-4.  JVP per lane and the VJP's sun-axis gradient projected on
+    the tangent (sum over the disc lanes with a random cotangent) against them."""
+    d = scene()
+    em = ss.load_dict(d, variant=variant)
+    o32 = O.Oracle(d, variant, "jit", "f32")
+    inf = o32.info()
+    half = math.acos(inf["cos_cutoff"])
+    wo = sun_cone_wo(16384, inf["sun_dir_local"], half, seed=21, scale=0.5)
+    gam = np.arccos(np.clip(wo.astype(np.float64) @ inf["sun_dir_local"], -1.0, 1.0))
+    wo = wo[gam >= half / 16]
+    n = wo.shape[0]
+    wi = -wo
+    rng = np.random.default_rng(22)
+    lam = rng.uniform(330, 710, (4, n)).astype(np.float32)
+    lam_o = lam if variant == "spectral" else None
+    si = ss.SurfaceInteraction3f(wi=_gpu(wi), wavelengths=torch.from_numpy(lam).cuda() if variant == "spectral" else None)
+    s = np.array(d["sun_direction"], np.float64)
+    t1 = np.cross(s, [0.0, 0.0, 1.0])
+    t1 /= np.linalg.norm(t1)
+    t2 = np.cross(s, t1)
+    k = 4 if variant == "spectral" else 3
+    cot = rng.standard_normal((k, n))
+    grad, view = em.eval_vjp(si, torch.from_numpy(cot.astype(np.float32)).cuda())
+    g_sun = view["sun_direction"].cpu().numpy().astype(np.float64)
+    h = 1e-4
+    ev = lambda dd: O.Oracle(dd, variant, "jit", "f64").eval(wi, lam_o)   # noqa: E731
+    for t in (t1, t2, 0.6 * t1 + 0.8 * t2):
+        plus = scene(sun=(s + h * t) / np.linalg.norm(s + h * t))
+        minus = scene(sun=(s - h * t) / np.linalg.norm(s - h * t))
+        fd = (ev(plus) - ev(minus)) / (2 * h)
+        fd = fd.T if variant == "spectral" else fd
+        _, dval = em.eval_jvp(si, "sun_direction", list(t))
+        dval = dval.cpu().numpy().T.astype(np.float64)
+        assert np.abs(fd).max() > 0
+        worst = np.max(np.abs(dval - fd) / (2e-3 * np.abs(fd) + 1e-4 * np.abs(fd).max()))
+        print(f"{variant} t={np.round(t, 3)}: {n} disc lanes, JVP vs FD worst {worst:.2f}x of the bound")
+        check(dval, fd, np.ones_like(dval, bool))
+        proj, ref = float(g_sun @ t), float((cot.T * fd).sum())
+        mag = float(np.abs(cot.T * fd).sum())
+        assert abs(proj - ref) <= 1e-3 * mag, (proj, ref, mag)

@@ -194,4 +194,4 @@ def test_c4_sampling_at_30deg_elevation(variant, precision):
     if variant == "spectral":
         e32, e64 = e32.T, e64.T
     assert_parity(gw, (e32 / gp[:, None]).astype(np.float32), e64 / gp[:, None].astype(np.float64), disc_lanes(gd, o32.info()),
-                  rtol=2e-5, precision=precision)
+                  rtol=1e-5, precision=precision)

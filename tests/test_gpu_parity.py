@@ -216,7 +216,7 @@ def test_sample_direction_and_pdf_parity(variant, semantics, precision):
     e32, e64 = (e32.T, e64.T) if variant == "spectral" else (e32, e64)
     wref32 = (e32 / gp[:, None]).astype(np.float32)
     wref64 = e64 / gp[:, None].astype(np.float64)
-    assert_parity(gw, wref32, wref64, disc_lanes(gd, info), rtol=2e-5, precision=precision)
+    assert_parity(gw, wref32, wref64, disc_lanes(gd, info), rtol=1e-5, precision=precision)
 
 
 @pytest.mark.parametrize("variant", ["rgb", "spectral"])
@@ -376,7 +376,7 @@ def test_sun_disc_weights_across_elevations(elev_deg, precision):
     # The sun's blue channel at a low sun is a near-cancelling sum of 24 polynomial terms
     # of the size of the lane's largest channel: its rounding floor is relative to that.
     scale = np.maximum(np.abs(b), 1e-2 * np.abs(b).max(axis=1, keepdims=True))
-    bound = 2e-5 * scale + SUN_SLACK[precision] * np.abs(a - b) + 1e-30
+    bound = 1e-5 * scale + SUN_SLACK[precision] * np.abs(a - b) + 1e-30
     worst = (np.abs(g - b) / bound).max()
     assert worst <= 1.0, f"sun-disc weights {worst:.2f}x over bound"
 
@@ -633,7 +633,7 @@ def test_full_size_c4_sampling_64M():
     up = gd[:, 2] >= 0
     w32 = (o32.eval(-gd) / gp[:, None]).astype(np.float32)
     w64 = o64.eval(-gd) / gp[:, None].astype(np.float64)
-    assert_parity(gw[up], w32[up], w64[up], disc_lanes(gd, info)[up], rtol=2e-5)
+    assert_parity(gw[up], w32[up], w64[up], disc_lanes(gd, info)[up], rtol=1e-5)
 
 
 def test_full_size_c5_per_rank_leg_64M_x11_and_one_rank_gather():
@@ -676,6 +676,65 @@ def test_full_size_c5_per_rank_leg_64M_x11_and_one_rank_gather():
     st = assert_parity(got, o32.eval(-wh, lam).T, o64.eval(-wh, lam).T, sm)
     print(f"C5 per-rank leg: {wh.shape[0]} directions x 11 checked, {int(sm.sum())} sun-disc; "
           f"sky max rel vs o32 {st['sky_max_rel_vs_o32']:.2e}, sun max rel vs o64 {st['sun_max_rel_vs_o64']:.2e}")
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+def test_c4_sampling_with_independently_staged_oracle(variant, precision):
+    """End-to-end sampling parity WITHOUT adopted state: the C4 emitter (T = 3,
+    albedo 0.3, sun elevation 30 deg) staged on the device, against an oracle that stages its
+    own w_sky and wavelength distribution (the 200 x 200 quadrature of sunsky.cpp:772-886 with
+    the fp32 terms added exactly) -- no override_w_sky / adopt_sampling_state.
+    * staged state: w_sky within 1e-6, the wavelength nodes within 1e-6 (DESIGN.md §6);
+    * pdf and pdf_direction at the GPU's directions within 1e-5 of the oracle's pdf, and the
+      weights (RGB; spectral x 4 per-sample wavelengths) at the 1e-5 bars of assert_parity;
+    * directions: inverse-CDF sampling is discontinuous in w_sky (u.x / w_sky feeds the
+      discrete pick and its reused sample), so a w_sky a few ulps apart moves most samples by
+      < 1e-5 and a few across a CDF edge; bounded statistically (measured on the oracle with
+      the product's w_sky: p99 2.4e-5 for 2.5e-7 relative);
+    * spectral: sample_wavelengths at 1e-5 of the oracle's own wavelengths."""
+    d = angles_dict(3.0, 0.0, np.deg2rad(60), 0.3, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, variant, precision=precision)
+    o32, o64 = O.Oracle(d, variant, "jit", "f32"), O.Oracle(d, variant, "jit", "f64")
+    w_p, w_o = em.sky_sampling_w, o32.info()["w_sky"]
+    assert abs(w_p - w_o) <= 1e-6 * w_o, (w_p, w_o)
+    if variant == "spectral":
+        np.testing.assert_allclose(em.table("spectral_pdf"), o32.info()["spec_pdf"], rtol=1e-6)
+    rng = np.random.default_rng(30)
+    n = 1 << 18
+    u = rng.random((n, 2), dtype=np.float32)
+    lam = rng.uniform(360, 720, (4, n)).astype(np.float32) if variant == "spectral" else None
+    it = ss.Interaction3f(wavelengths=torch.from_numpy(lam).cuda() if lam is not None else None)
+    ds, w = em.sample_direction(it, soa(u))
+    gd, gp, gw = host(ds.d).T, host(ds.pdf), host(w).T
+    ref = o32.sample_direction(u, wavelengths=lam)
+    between = (u[:, 0] >= min(w_p, w_o)) & (u[:, 0] < max(w_p, w_o))     # sky / sun pick differs
+    derr = np.abs(gd - ref["d"]).max(axis=1)[~between]
+    q = np.quantile(derr, [0.5, 0.99, 0.999])
+    print(f"{variant}/{precision}: w_sky {w_p!r} vs {w_o!r}, picks differing {int(between.sum())}, "
+          f"|dd| p50 {q[0]:.2e} p99 {q[1]:.2e} p99.9 {q[2]:.2e} max {derr.max():.2e}")
+    assert between.sum() <= max(2, 1e-5 * n)
+    assert q[0] < 1e-6 and q[1] < 1e-4 and np.mean(derr > 1e-3) < 2e-3
+    info = o32.info()
+    inside = (gd @ info["sun_dir_local"]) >= info["cos_cutoff"]
+    same = (u[:, 0] < w_p) | inside            # sun picks skip the cone test (sunsky.cpp:720)
+    pref = o32.pdf_direction(gd)
+    assert max_rel(gp[same], pref[same]) < 1e-5
+    assert max_rel(host(em.pdf_direction(ss.Interaction3f(), ds)), pref) < 1e-5
+    e32, e64 = o32.eval(-gd, lam), o64.eval(-gd, lam)
+    e32, e64 = (e32.T, e64.T) if variant == "spectral" else (e32, e64)
+    up = gd[:, 2] >= 0
+    assert_parity(gw[up], (e32 / gp[:, None]).astype(np.float32)[up], (e64 / gp[:, None].astype(np.float64))[up],
+                  disc_lanes(gd, info)[up], rtol=1e-5, precision=precision)
+    if variant == "spectral":
+        # sample_wavelengths (sunsky.cpp:463-480) from each side's own wavelength distribution
+        ws = rng.random(n, dtype=np.float32)
+        wi_h = -hemisphere_wo(n, seed=31)
+        lam_g, _ = em.sample_wavelengths(ss.SurfaceInteraction3f(wi=soa(wi_h)), torch.from_numpy(ws).cuda())
+        lam_o, _ = o32.sample_wavelengths(wi_h, ws)
+        rel = np.abs(host(lam_g).T.astype(np.float64) - lam_o) / lam_o
+        print(f"sample_wavelengths: max rel {rel.max():.2e}")
+        assert rel.max() <= 1e-5
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)
@@ -724,7 +783,7 @@ def test_full_size_c4_spectral_sampling_64M_x4(precision):
     up = gd[:, 2] >= 0
     w32 = (o32.eval(-gd, lh).T / gp[:, None]).astype(np.float32)
     w64 = o64.eval(-gd, lh).T / gp[:, None].astype(np.float64)
-    st = assert_parity(gw[up], w32[up], w64[up], disc_lanes(gd, info)[up], rtol=2e-5, precision=precision)
+    st = assert_parity(gw[up], w32[up], w64[up], disc_lanes(gd, info)[up], rtol=1e-5, precision=precision)
     print(f"C4 spectral 64M x 4 ({precision}): {int(up.sum())} checked samples, sun lanes {st.get('sun_lanes')}")
 
 

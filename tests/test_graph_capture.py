@@ -153,12 +153,16 @@ def test_update_is_refused_inside_a_capture():
     assert torch.equal(em.eval(ss.SurfaceInteraction3f(wi=wi)), fresh.eval(ss.SurfaceInteraction3f(wi=wi)))
 
 
-def test_update_rejected_by_the_device_staging_restores_the_previous_state(monkeypatch):
+def _inject(em, count):
+    ss._capi.check(ss.lib().sunsky_emitter_inject_staging_fault(em._h, count))
+
+
+def test_update_rejected_by_the_device_staging_restores_the_previous_state():
     """A negative wavelength-distribution node found by the device staging (the check of
     ContinuousDistribution's constructor, distr_1d.h) rejects the update as the reference's
     parameters_changed does: the next read-back raises once, the previous parameters are
     restored and restaged on the device, and later calls see the old state.  The status is
-    forced with the SUNSKY_AMD_FAULT_STAGE_STATUS fault injection."""
+    forced with the test-only sunsky_emitter_inject_staging_fault."""
     d = angles_dict(3.0, 0.3, np.deg2rad(50), 0.3, 1.0, 1.0)
     em = ss.SunskyEmitter(d, "spectral")
     n = 1 << 12
@@ -167,9 +171,8 @@ def test_update_rejected_by_the_device_staging_restores_the_previous_state(monke
     before = em.eval(ss.SurfaceInteraction3f(wi=wi, wavelengths=lam)).clone()
     params = em.traverse()
     params["turbidity"] = 6.5
-    monkeypatch.setenv("SUNSKY_AMD_FAULT_STAGE_STATUS", "1")
+    _inject(em, 1)
     params.update()                        # async: nothing waits for the device
-    monkeypatch.delenv("SUNSKY_AMD_FAULT_STAGE_STATUS")
     with pytest.raises(ValueError, match="non-negative"):
         em.info()
     assert em.info()["turbidity"] == 3.0 and em.get_param("turbidity") == 3.0
@@ -181,3 +184,43 @@ def test_update_rejected_by_the_device_staging_restores_the_previous_state(monke
     fresh = ss.SunskyEmitter(dict(d, turbidity=6.5), "spectral")
     assert torch.equal(em.eval(ss.SurfaceInteraction3f(wi=wi, wavelengths=lam)),
                        fresh.eval(ss.SurfaceInteraction3f(wi=wi, wavelengths=lam)))
+
+
+@pytest.mark.parametrize("second", ["accepted", "rejected"])
+def test_two_queued_updates_with_a_rejection(second):
+    """two async updates queued before a read-back.  The rejection status is
+    sticky across stagings, so a rejected update followed by an accepted one still reports
+    the error, and two rejected ones revert to the last ACCEPTED state (not to the first
+    rejected snapshot); the emitter then evaluates exactly as a fresh one at that state,
+    and later updates work."""
+    d = angles_dict(3.0, 0.3, np.deg2rad(50), 0.3, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, "spectral")
+    n = 1 << 12
+    wi, _ = _inputs(n, 7)
+    lam = torch.full((4, n), 610.0, device="cuda")
+    si = ss.SurfaceInteraction3f(wi=wi, wavelengths=lam)
+    params = em.traverse()
+    params["turbidity"] = 5.0
+    params.update()
+    assert em.info()["turbidity"] == 5.0           # read back: this state is accepted
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):                    # batch work queued on a caller stream
+        em.eval(si)
+    _inject(em, 1 if second == "accepted" else 2)
+    params = em.traverse()
+    params["turbidity"] = 6.0
+    params.update()                                # rejected
+    params = em.traverse()
+    params["albedo"] = 0.45
+    params.update()                                # accepted or rejected
+    with pytest.raises(ValueError, match="non-negative"):
+        em.info()
+    assert em.get_param("turbidity") == 5.0 and np.allclose(em.get_param("albedo"), 0.3, rtol=0, atol=1e-7)
+    fresh = ss.SunskyEmitter(dict(d, turbidity=5.0), "spectral")
+    assert torch.equal(em.eval(si), fresh.eval(si))
+    np.testing.assert_array_equal(em.table("spectral_pdf"), fresh.table("spectral_pdf"))
+    assert em.info()["turbidity"] == 5.0           # reported once
+    params = em.traverse()
+    params["turbidity"] = 7.0
+    params.update()
+    assert torch.equal(em.eval(si), ss.SunskyEmitter(dict(d, turbidity=7.0), "spectral").eval(si))

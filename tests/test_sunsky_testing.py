@@ -116,4 +116,4 @@ def test_sky_sun_sampling_weight_map():
             ref = O.Oracle(d, "rgb", "jit", "f32").info()["w_sky"]
             assert 0.0 <= w <= 1.0
             worst = max(worst, abs(w - ref))
-    assert worst < 2e-5, worst
+    assert worst < 1e-6, worst

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 measurement: full bench, then a rocprofv3 kernel trace of the timed headline burst
+# Headline measurement: full bench, then a rocprofv3 kernel trace of the timed headline burst
 # alone (bench.py --headline-only) with its per-launch statistics, then the PMC traffic of
 # the same burst (separate FETCH_SIZE / WRITE_SIZE passes, no tracing domains with --pmc).
 set -o pipefail

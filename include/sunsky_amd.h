@@ -81,7 +81,9 @@ typedef enum sunsky_table_id {      /* staged tables, for inspection / parity te
     SUNSKY_TABLE_GAUSSIAN_CDF = 5,  /* 20       (DiscreteDistribution cdf) */
     SUNSKY_TABLE_SPECTRAL_PDF = 6,  /* m_spectral_distr pdf                */
     SUNSKY_TABLE_SPECTRAL_CDF = 7,  /* m_spectral_distr cdf                */
-    SUNSKY_TABLE_ALBEDO = 8         /* extract_albedo() result             */
+    SUNSKY_TABLE_ALBEDO = 8,        /* extract_albedo() result             */
+    SUNSKY_TABLE_SUN_SKY_FIT = 9    /* 10: the FAST samplers' sun-pick sky pdf fit: c0..c5, bound,
+                                       smallest value, usable (0/1), in use for this w_sky (0/1) */
 } sunsky_table_id;
 
 #define SUNSKY_FLAG_INFINITE 0x04u          /* EmitterFlags::Infinite (emitter.h:29-30) */

@@ -473,6 +473,7 @@ struct sunsky_emitter {
         std::memcpy(self->kargs.sky, hk.sky, sizeof(hk.sky));
         std::memcpy(self->kargs.fsky, hk.fsky, sizeof(hk.fsky));
         self->kargs.w_sky = hk.w_sky;
+        self->kargs.sun_sky_fit_on = hk.sun_sky_fit_on;
         self->kargs.spec_size = hk.spec_size;
         std::memcpy(self->kargs.spec_pdf, hk.spec_pdf, sizeof(hk.spec_pdf));
         std::memcpy(self->kargs.spec_cdf, hk.spec_cdf, sizeof(hk.spec_cdf));
@@ -525,7 +526,7 @@ struct sunsky_emitter {
         A.sky_rad_ds = d_sky_rad_ds;
         A.sun_rad_ds = d_sun_rad_ds;
         A.out = out;
-        A.nbasis = nbasis;
+        A.nbasis = A.nsky = nbasis;
         A.sun_local_off = sun_local_off;
         A.sun_local_first = sun_local_first;
         A.sun_off = sun_off;
@@ -757,6 +758,10 @@ int sunsky_emitter_get_table(const sunsky_emitter* e, int id, float* out, size_t
         case SUNSKY_TABLE_SPECTRAL_PDF: v.assign(k.spec_pdf, k.spec_pdf + k.spec_size); break;
         case SUNSKY_TABLE_SPECTRAL_CDF: v.assign(k.spec_cdf, k.spec_cdf + std::max(0, k.spec_size - 1)); break;
         case SUNSKY_TABLE_ALBEDO: v = e->model->albedo(); break;
+        case SUNSKY_TABLE_SUN_SKY_FIT:
+            v.assign(k.sun_sky_fit, k.sun_sky_fit + 6);
+            v.insert(v.end(), {k.sun_sky_fit_dev, k.sun_sky_fit_fmin, (float)k.sun_sky_fit_ok, (float)k.sun_sky_fit_on});
+            break;
         default: return fail(SUNSKY_ERROR_INVALID_VALUE, "unknown table id");
     }
     *count = v.size();
@@ -1145,6 +1150,7 @@ int sunsky_eval_vjp(const sunsky_emitter* e, sunsky_vec3_in wi, const float* lam
                 // (kVjpSunEta), one sky tangent per channel for the 3 axes instead of 3
                 A.eta_off = kVjpSunEta;
                 A.st[2].dx = A.st[2].dx_per_eta;
+                A.nsky = 3;   // the sky blocks of bases 3 and 4 are never read: written 0, not staged
             }
             e->stage_tangent(A, st);
             e->vjp_rev = e->rev;

@@ -1152,7 +1152,8 @@ __device__ __forceinline__ float3_ sample_sun(const SunskyKArgs& K, float ux, fl
 // the same directions.
 template <bool FAST>
 __device__ __forceinline__ float3_ sample_sky_or_sun(const SunskyKArgs& K, const TgmmLds<FAST>& T, bool pick_sky,
-                                                     float ux, float uy, float inv_w, float inv_w_sun) {
+                                                     float ux, float uy, float inv_w, float inv_w_sun,
+                                                     float* sun_a, float* sun_b) {
     const float a = div_exact<FAST>(pick_sky ? ux : ux - K.w_sky, pick_sky ? K.w_sky : 1.f - K.w_sky,
                                     pick_sky ? inv_w : inv_w_sun);
     float arg, phi = 0.f, r = 0.f;
@@ -1193,8 +1194,10 @@ __device__ __forceinline__ float3_ sample_sky_or_sun(const SunskyKArgs& K, const
     const float pn = fmaf(px, px, py * py);
     const float z = K.cos_cutoff + omc * (1.f - pn);
     const float sc = safe_sqrt_sel<FAST>(omc * (2.f - omc * pn));
+    *sun_a = px * sc;
+    *sun_b = py * sc;
     return frame_to_world(mk3(K.sun_s[0], K.sun_s[1], K.sun_s[2]), mk3(K.sun_t[0], K.sun_t[1], K.sun_t[2]),
-                          mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), mk3(px * sc, py * sc, z));
+                          mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), mk3(*sun_a, *sun_b, z));
 }
 
 // The FAST mixture sum of tgmm_pdf at a wrapped (phi, theta), one pair of
@@ -1258,6 +1261,25 @@ __device__ __forceinline__ void compute_pdfs(const SunskyKArgs& K, const TgmmLds
     *sky_pdf = fdiv<FAST>(tgmm_pdf<FAST>(K, T, phi, theta, active), sin_theta);
     float cosg = dot3(mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]), d);
     *sun_pdf = (!check_sun || cosg >= K.cos_cutoff) ? K.sun_pdf : 0.f;
+}
+
+// compute_pdfs of a sampled direction (check_sun = pick_sky, sunsky.cpp:415).  FAST sun
+// picks take the sky pdf from the host's quadratic fit over the disc at their disc
+// coordinates (a, b) when the staging turned it on (SunskyKArgs::sun_sky_fit_on): a sun
+// pick's pdf is dominated by (1 - w) sun_pdf, and the fit moves it by < kSunSkyFitTol =
+// 1e-7 relative (the host's bound), while the exact path costs the TGMM sum (one exp2 per
+// gaussian), atan2, the polar angle and a division per sample.
+template <bool FAST>
+__device__ __forceinline__ void sample_pdfs(const SunskyKArgs& K, const TgmmLds<FAST>& T, float3_ sd, bool pick_sky,
+                                            float sun_a, float sun_b, bool active, float* sky_pdf, float* sun_pdf) {
+    if (FAST && !pick_sky && K.sun_sky_fit_on) {
+        const float* c = K.sun_sky_fit;
+        const float f = fmaf(sun_a, fmaf(c[3], sun_a, fmaf(c[4], sun_b, c[1])), fmaf(sun_b, fmaf(c[5], sun_b, c[2]), c[0]));
+        *sky_pdf = active ? f : 0.f;
+        *sun_pdf = K.sun_pdf;
+        return;
+    }
+    compute_pdfs<FAST>(K, T, sd, pick_sky, active, sky_pdf, sun_pdf);
 }
 
 // ContinuousDistribution::sample_pdf (distr_1d.h:468-499) over [360, 720]
@@ -1385,8 +1407,9 @@ __device__ __forceinline__ void sample_direction_body(
         // sx / w and the reused sample stay correctly rounded even in FAST: the
         // discrete-distribution reuse divides by the picked gaussian's pmf, so one
         // ulp here moves sky directions by up to ~1e-5 (measured).
+        float sun_a = 0.f, sun_b = 0.f;
 #ifndef SS_PROBE_NO_SKY_SAMPLE   // probe builds (tools/Makefile) only: cost ablations
-        const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
+        const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun, &sun_a, &sun_b);
 #else
         const float3_ sd = sample_sun<FAST>(K, div_exact<FAST>(sx - K.w_sky, w_sun, inv_w_sun), sy);
 #endif
@@ -1394,7 +1417,7 @@ __device__ __forceinline__ void sample_direction_body(
         float3_ d = to_world(K, sd);
         float skyp, sunp;
 #ifndef SS_PROBE_NO_PDF
-        compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+        sample_pdfs<FAST>(K, S.tgmm, sd, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
 #else
         skyp = sd.z; sunp = K.sun_pdf;
 #endif
@@ -1521,8 +1544,9 @@ __device__ __forceinline__ void sample_direction_spec4_body(
         for (int k = 0; k < 4; ++k) l[k] = nl[k];
         if (i + stride < n) load(i + stride);
         const bool pick_sky = sx < K.w_sky;
+        float sun_a = 0.f, sun_b = 0.f;
 #ifndef SS_PROBE_NO_SKY_SAMPLE
-        const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
+        const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun, &sun_a, &sun_b);
 #else
         const float3_ sd = sample_sun<FAST>(K, div_exact<FAST>(sx - K.w_sky, w_sun, inv_w_sun), sy);
 #endif
@@ -1530,7 +1554,7 @@ __device__ __forceinline__ void sample_direction_spec4_body(
         const float3_ d = to_world(K, sd);
         float skyp, sunp;
 #ifndef SS_PROBE_NO_PDF
-        compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+        sample_pdfs<FAST>(K, S.tgmm, sd, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
 #else
         skyp = sd.z; sunp = K.sun_pdf;
 #endif
@@ -1570,11 +1594,12 @@ template <bool FAST>
 __device__ __forceinline__ void sample_one_spec4(const SunskyKArgs& K, const SamplerLds<FAST, true>& S, float sx,
                                                  float sy, const float l[4], float inv_w, float inv_w_sun, float o[8]) {
     const bool pick_sky = sx < K.w_sky;
-    const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
+    float sun_a = 0.f, sun_b = 0.f;
+    const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun, &sun_a, &sun_b);
     const bool act = sd.z >= 0.f;
     const float3_ d = to_world(K, sd);
     float skyp, sunp;
-    compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+    sample_pdfs<FAST>(K, S.tgmm, sd, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
     const float pd = lerpf_(sunp, skyp, K.w_sky);
     o[0] = d.x; o[1] = d.y; o[2] = d.z; o[3] = pd;
     // scheduler held between the pdf and the eval: 127 -> 124 VGPRs, no spills, 1.7 % faster
@@ -1691,8 +1716,9 @@ template <bool FAST>
 __device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const SamplerLds<FAST, false>& S, float sx,
                                                float sy, bool act, float inv_w, float inv_w_sun, float o[7]) {
     const bool pick_sky = sx < K.w_sky;
+    float sun_a = 0.f, sun_b = 0.f;
 #ifndef SS_PROBE_NO_SKY_SAMPLE   // probe builds (tools/Makefile) only: cost ablations
-    const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
+    const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun, &sun_a, &sun_b);
 #else
     const float3_ sd = sample_sun<FAST>(K, div_exact<FAST>(sx - K.w_sky, 1.f - K.w_sky, inv_w_sun), sy);
 #endif
@@ -1700,7 +1726,7 @@ __device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const Sampl
     const float3_ d = to_world(K, sd);
     float skyp, sunp;
 #ifndef SS_PROBE_NO_PDF
-    compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+    sample_pdfs<FAST>(K, S.tgmm, sd, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
 #else
     skyp = sd.z; sunp = K.sun_pdf;
 #endif
@@ -1992,11 +2018,12 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
         disk_concentric_dev<FAST>(s2x[i], s2y[i], &offx, &offy);
         const float sx = s3x[i], sy = s3y[i];
         const bool pick_sky = sx < K.w_sky;
-        const float3_ d = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
+        float sun_a = 0.f, sun_b = 0.f;
+        const float3_ d = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun, &sun_a, &sun_b);
         float3_ dw = to_world(K, mk3(-d.x, -d.y, -d.z));
         act = act && (d.z >= 0.f);
         float skyp, sunp;
-        compute_pdfs<FAST>(K, S.tgmm, d, pick_sky, act, &skyp, &sunp);
+        sample_pdfs<FAST>(K, S.tgmm, d, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
         float pd = lerpf_(sunp, skyp, K.w_sky);
         pd *= kInvPi * (1.f / (K.bs_radius * K.bs_radius));
         act = act && pd > 0.f;
@@ -2106,11 +2133,12 @@ __device__ __forceinline__ void sample_ray_rgb_sorted_body(
             const int q = p * 64 + lane;
             const float sx = Y[0][q], sy = Y[1][q];
             const bool pick_sky = sx < K.w_sky;
-            const float3_ d = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun);
+            float sun_a = 0.f, sun_b = 0.f;
+            const float3_ d = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun, &sun_a, &sun_b);
             const float3_ dw = to_world(K, mk3(-d.x, -d.y, -d.z));
             bool act = d.z >= 0.f;
             float skyp, sunp;
-            compute_pdfs<FAST>(K, S.tgmm, d, pick_sky, act, &skyp, &sunp);
+            sample_pdfs<FAST>(K, S.tgmm, d, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
             float pd = lerpf_(sunp, skyp, K.w_sky);
             pd *= kInvPi * (1.f / (K.bs_radius * K.bs_radius));
             act = act && pd > 0.f;
@@ -2180,11 +2208,12 @@ __device__ __forceinline__ void dd_emitter_rgb(const SunskyKArgs& K, const Sampl
                                                float u0, float u1, unsigned v, float inv_w, float inv_w_sun,
                                                float* scale, float w[3]) {
     const bool pick_sky = u0 < K.w_sky;
-    const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, u0, u1, inv_w, inv_w_sun);
+    float sun_a = 0.f, sun_b = 0.f;
+    const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, u0, u1, inv_w, inv_w_sun, &sun_a, &sun_b);
     const bool act = sd.z >= 0.f;
     const float3_ d = to_world(K, sd);
     float skyp, sunp;
-    compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+    sample_pdfs<FAST>(K, S.tgmm, sd, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
     const float pd = lerpf_(sunp, skyp, K.w_sky);
     const float cos_em = dot3(nrm, d);
     *scale = 0.f;
@@ -2301,11 +2330,12 @@ __device__ __forceinline__ void direct_diffuse_body(
             }
             // ---- emitter sampling: sample_direction (sunsky.cpp:399-441)
             const bool pick_sky = u0 < K.w_sky;
-            float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, u0, u1, inv_w, inv_w_sun);
+            float sun_a = 0.f, sun_b = 0.f;
+            float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, u0, u1, inv_w, inv_w_sun, &sun_a, &sun_b);
             bool act = sd.z >= 0.f;
             const float3_ d = to_world(K, sd);
             float skyp, sunp;
-            compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+            sample_pdfs<FAST>(K, S.tgmm, sd, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
             const float pd = lerpf_(sunp, skyp, K.w_sky);
             const float cos_em = dot3(nrm, d);
             if ((v & 1u) && pd != 0.f && cos_em > 0.f) {
@@ -2585,11 +2615,12 @@ __device__ __forceinline__ void direct_conductor_body(
             // ---- emitter sampling
             {
                 const bool pick_sky = u0 < K.w_sky;
-                const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, u0, u1, inv_w, inv_w_sun);
+                float sun_a = 0.f, sun_b = 0.f;
+                const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, u0, u1, inv_w, inv_w_sun, &sun_a, &sun_b);
                 const bool act = sd.z >= 0.f;
                 const float3_ d = to_world(K, sd);
                 float skyp, sunp;
-                compute_pdfs<FAST>(K, S.tgmm, sd, pick_sky, act, &skyp, &sunp);
+                sample_pdfs<FAST>(K, S.tgmm, sd, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
                 const float pd = lerpf_(sunp, skyp, K.w_sky);
                 const float3_ wo = mk3(dot3(d, fs), dot3(d, ft), dot3(d, nrm));
                 float bpdf, cih;
@@ -2691,11 +2722,12 @@ __device__ __forceinline__ void direct_conductor_rays_body(
             (void)rng.next_float();
             const float u2 = rng.next_float(), u3 = rng.next_float();
             const bool pick_sky = u0 < K.w_sky;
-            const float3_ sd = sample_sky_or_sun<FAST>(K, T, pick_sky, u0, u1, inv_w, inv_w_sun);
+            float sun_a = 0.f, sun_b = 0.f;
+            const float3_ sd = sample_sky_or_sun<FAST>(K, T, pick_sky, u0, u1, inv_w, inv_w_sun, &sun_a, &sun_b);
             const bool act = sd.z >= 0.f;
             const float3_ d = to_world(K, sd);
             float skyp, sunp;
-            compute_pdfs<FAST>(K, T, sd, pick_sky, act, &skyp, &sunp);
+            sample_pdfs<FAST>(K, T, sd, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
             const float pd = lerpf_(sunp, skyp, K.w_sky);
             const float3_ wo = mk3(dot3(d, fs), dot3(d, ft), dot3(d, nrm));
             float bpdf, cih;
@@ -2762,11 +2794,12 @@ __device__ __forceinline__ void direct_diffuse_rays_body(
             (void)rng.next_float();   // sample_1 (path.cpp:233), unused by the diffuse BSDF
             const float u2 = rng.next_float(), u3 = rng.next_float();
             const bool pick_sky = u0 < K.w_sky;
-            const float3_ sd = sample_sky_or_sun<FAST>(K, T, pick_sky, u0, u1, inv_w, inv_w_sun);
+            float sun_a = 0.f, sun_b = 0.f;
+            const float3_ sd = sample_sky_or_sun<FAST>(K, T, pick_sky, u0, u1, inv_w, inv_w_sun, &sun_a, &sun_b);
             const bool act = sd.z >= 0.f;
             const float3_ d = to_world(K, sd);
             float skyp, sunp;
-            compute_pdfs<FAST>(K, T, sd, pick_sky, act, &skyp, &sunp);
+            sample_pdfs<FAST>(K, T, sd, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
             const float pd = lerpf_(sunp, skyp, K.w_sky);
             const bool em_ok = pd != 0.f && dot3(nrm, d) > 0.f;
             float px, py;

@@ -380,6 +380,7 @@ void SunskyModel::adopt_device_stage(const SunskyKArgs& dk, const float* sun_tab
         sky_rad_[c] = ch.rad;
     }
     k_.w_sky = dk.w_sky;
+    k_.sun_sky_fit_on = dk.sun_sky_fit_on;
     k_.spec_size = dk.spec_size;
     std::memcpy(k_.spec_pdf, dk.spec_pdf, sizeof(k_.spec_pdf));
     std::memcpy(k_.spec_cdf, dk.spec_cdf, sizeof(k_.spec_cdf));
@@ -510,6 +511,7 @@ void SunskyModel::stage_geometry() {
         k_.gauss_norm = 1.f / k_.gauss_sum;
         build_gauss_guide();
     }
+    stage_sun_sky_fit();
 
     k_.sun_table = nullptr;   // device pointers are patched in by the C-ABI layer
     k_.sun_ld = nullptr;
@@ -550,12 +552,97 @@ void SunskyModel::build_gauss_guide() {
     k_.gauss_guide_span = span;
 }
 
+// The sky pdf over the sun disc, for the FAST samplers' sun picks (SunskyKArgs::sun_sky_fit).
+// f(a, b) = tgmm_pdf(phi, theta) / sin(theta) (sunsky.cpp:711-763) of the local direction
+// a s + b t + sqrt(1 - a^2 - b^2) n, (a, b) in the disc of radius rho = sin(half aperture),
+// in fp64 from the staged fp32 gaussians.  Least-squares quadratic on 12 x 24 polar points,
+// then the deviation and the smallest value over a 41 x 96 polar grid (rim included); the
+// bound kept is twice the grid deviation plus 4e-7 of the largest value (the kernels
+// evaluate the fp32 coefficients in fp32).  Not used (sun_sky_fit_ok = 0) when the disc
+// comes within 16 rho of the zenith (1 / sin(theta) varies fast there), within 2 rho of the
+// horizon (the pdf's mask), or near the wrap of phi.
+void SunskyModel::stage_sun_sky_fit() {
+    k_.sun_sky_fit_ok = 0;
+    k_.sun_sky_fit_on = 0;
+    for (float& c : k_.sun_sky_fit) c = 0.f;
+    k_.sun_sky_fit_dev = k_.sun_sky_fit_fmin = 0.f;
+    const double cc = (double)k_.cos_cutoff, rho = std::sqrt(std::max(0.0, 1.0 - cc * cc));
+    const double n[3] = {k_.sun_n[0], k_.sun_n[1], k_.sun_n[2]}, s[3] = {k_.sun_s[0], k_.sun_s[1], k_.sun_s[2]},
+                 t[3] = {k_.sun_t[0], k_.sun_t[1], k_.sun_t[2]};
+    const double pi = 3.14159265358979323846, phi0 = (double)k_.sun_phi - 0.5 * (double)kPi;
+    if (!(rho > 0.0) || !(n[2] > 2.0 * rho) || std::sqrt(n[0] * n[0] + n[1] * n[1]) < 16.0 * rho) return;
+    bool ok = true;
+    auto f = [&](double x, double y) {   // x, y: disc coordinates / rho
+        const double a = x * rho, b = y * rho, z = std::sqrt(std::max(0.0, 1.0 - a * a - b * b));
+        const double d[3] = {a * s[0] + b * t[0] + z * n[0], a * s[1] + b * t[1] + z * n[1],
+                             a * s[2] + b * t[2] + z * n[2]};
+        const double st = std::sqrt(d[0] * d[0] + d[1] * d[1]), th = std::atan2(st, d[2]);
+        double ph = std::atan2(d[1], d[0]) - phi0;
+        if (ph < 0.0) ph += 2.0 * pi;
+        if (ph > 2.0 * pi) ph -= 2.0 * pi;
+        if (!(d[2] > rho) || ph < 0.25 || ph > 2.0 * pi - 0.25 || th > 0.5 * pi) ok = false;
+        double pdf = 0.0;
+        for (int i = 0; i < k_.tgmm_count; ++i) {
+            const Gaussian& g = k_.gauss[k_.tgmm_idx[i]];
+            const double sx = (ph - g.mu_phi) / g.sigma_phi, sy = (th - g.mu_theta) / g.sigma_theta;
+            pdf += (double)g.coef * std::exp(-0.5 * (sx * sx + sy * sy)) / (2.0 * pi);
+        }
+        return pdf / st;
+    };
+    auto basis = [](double x, double y, double* v) { v[0] = 1; v[1] = x; v[2] = y; v[3] = x * x; v[4] = x * y; v[5] = y * y; };
+    double A[6][7] = {};
+    for (int i = 0; i < 12; ++i)
+        for (int j = 0; j < 24; ++j) {
+            const double r = std::sqrt((i + 0.5) / 12.0), ang = 2.0 * pi * (j + 0.5 * (i & 1)) / 24.0;
+            const double x = r * std::cos(ang), y = r * std::sin(ang), v0 = f(x, y);
+            double v[6];
+            basis(x, y, v);
+            for (int p = 0; p < 6; ++p) {
+                for (int q = 0; q < 6; ++q) A[p][q] += v[p] * v[q];
+                A[p][6] += v[p] * v0;
+            }
+        }
+    for (int c = 0; c < 6; ++c) {   // Gaussian elimination, partial pivoting
+        int piv = c;
+        for (int r = c + 1; r < 6; ++r)
+            if (std::fabs(A[r][c]) > std::fabs(A[piv][c])) piv = r;
+        for (int q = 0; q < 7; ++q) std::swap(A[c][q], A[piv][q]);
+        for (int r = 0; r < 6; ++r) {
+            if (r == c) continue;
+            const double m = A[r][c] / A[c][c];
+            for (int q = c; q < 7; ++q) A[r][q] -= m * A[c][q];
+        }
+    }
+    double cn[6];
+    for (int c = 0; c < 6; ++c) cn[c] = A[c][6] / A[c][c];
+    double dev = 0.0, fmin = 1e300, fmax = 0.0;
+    for (int i = 0; i <= 40; ++i)
+        for (int j = 0; j < 96; ++j) {
+            const double r = i / 40.0, ang = 2.0 * pi * j / 96.0, x = r * std::cos(ang), y = r * std::sin(ang);
+            const double v0 = f(x, y);
+            double v[6], p = 0.0;
+            basis(x, y, v);
+            for (int q = 0; q < 6; ++q) p += cn[q] * v[q];
+            dev = std::max(dev, std::fabs(p - v0));
+            fmin = std::min(fmin, v0);
+            fmax = std::max(fmax, v0);
+        }
+    if (!ok || !(fmin > 0.0) || !std::isfinite(dev)) return;
+    // unnormalised coefficients: x = a / rho, y = b / rho
+    const double sc[6] = {1.0, 1.0 / rho, 1.0 / rho, 1.0 / (rho * rho), 1.0 / (rho * rho), 1.0 / (rho * rho)};
+    for (int c = 0; c < 6; ++c) k_.sun_sky_fit[c] = (float)(cn[c] * sc[c]);
+    k_.sun_sky_fit_dev = (float)(2.0 * dev + 4e-7 * fmax);
+    k_.sun_sky_fit_fmin = (float)(0.99 * fmin);
+    k_.sun_sky_fit_ok = 1;
+}
+
 // estimate_sky_sun_ratio, sunsky.cpp:772-886
 void SunskyModel::estimate_sky_sun_ratio() {
     const bool spec = variant_ == kSpectral;
     if (semantics_ == kScalar) {
         // Mean ratio + uniform spectral sampling (:778-783)
         k_.w_sky = 0.5f;
+        decide_sun_sky_fit(&k_);
         if (spec) {
             k_.spec_size = 2;
             k_.spec_pdf[0] = k_.spec_pdf[1] = 1.f;

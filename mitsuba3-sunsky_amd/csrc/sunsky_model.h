@@ -103,6 +103,7 @@ private:
     void stage_radiance();               // sky channels + sun table (host-only emitters)
     int gauss_search(float s) const;
     void build_gauss_guide();
+    void stage_sun_sky_fit();            // SunskyKArgs::sun_sky_fit (the FAST samplers' sun-pick sky pdf)
     void estimate_sky_sun_ratio();
     void validate() const;
 

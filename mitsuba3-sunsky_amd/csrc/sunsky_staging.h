@@ -128,9 +128,11 @@ SS_HD inline float sun_param_tangent(const float* ds, int block, int i, const Ta
 }
 
 // Layouts of the tangent tables the AD kernels read (sunsky_kernels.hip): per basis a
-// block of kTanBlock floats, d{A..I, rad} of channel c at c * 10 (+ q); the local sun
-// direction's tangent at kTanSunLocal (JVP) or kVjpSunLocal + 3 k (VJP, sun axis k);
-// the sun table's at kJvpSunOffset (JVP) / kVjpSunOffset (VJP, turbidity basis).
+// block of kTanBlock floats, d{A..I, rad} of channel c at c * 10 (+ q) -- the VJP reads
+// blocks 0-2 only (turbidity, albedo, the unit-elevation tangent its sun axes share);
+// blocks 3-4 stay reserved and zero -- the local sun direction's tangent at kTanSunLocal
+// (JVP) or kVjpSunLocal + 3 k (VJP, sun axis k); the sun table's at kJvpSunOffset (JVP) /
+// kVjpSunOffset (VJP, turbidity basis).
 constexpr int kTanBlock = kNbWavelengths * 10;   // 110
 constexpr int kTanSunLocal = kTanBlock;          // JVP: 110..112
 constexpr int kJvpSunOffset = 128;
@@ -150,23 +152,24 @@ SS_HD inline float tangent_value(const float* sky_params_ds, const float* sky_ra
                                     : radiance_param_tangent(sky_rad_ds, 1, c, s));
 }
 
-// Arguments of the device tangent staging (sunsky_stage_tangent): `nbasis` tangents,
-// basis b's sky block at out + b x kTanBlock, the local sun tangents of bases
-// [sun_local_first, nbasis) at out + sun_local_off (3 each), basis 0's sun-table tangent
-// at out + sun_off; every other float of [0, total) is written 0.
+// Arguments of the device tangent staging (sunsky_stage_tangent): `nbasis` tangents, the
+// sky blocks of the first `nsky` of them at out + b x kTanBlock (the VJP's sun axes
+// share basis 2's unit-elevation block, so it stages 3 of its 5), the local sun tangents
+// of bases [sun_local_first, nbasis) at out + sun_local_off (3 each), basis 0's sun-table
+// tangent at out + sun_off; every other float of [0, total) is written 0.
 struct TangentArgs {
     const float* sky_params_ds;
     const float* sky_rad_ds;
     const float* sun_rad_ds;
     float* out;
-    int nbasis, sun_local_off, sun_local_first, sun_off, sun_block, total;
+    int nbasis, nsky, sun_local_off, sun_local_first, sun_off, sun_block, total;
     TangentStage st[kVjpBases];
     int eta_off;   // > 0: d eta of bases [sun_local_first, nbasis) at out + eta_off (VJP)
 };
 
 // Float idx of the tangent buffer described by A (the device kernel's per-thread work).
 SS_HD inline float tangent_buffer_value(const TangentArgs& A, int idx) {
-    if (idx < A.nbasis * kTanBlock) {
+    if (idx < A.nsky * kTanBlock) {
         const int b = idx / kTanBlock, j = idx % kTanBlock;
         return j < A.st[b].nch * 10 ? tangent_value(A.sky_params_ds, A.sky_rad_ds, A.st[b], j) : 0.f;
     }
@@ -254,6 +257,20 @@ SS_HD inline void quad_channel(const SunskyKArgs& K, const float* sun_table, con
     }
 }
 
+// Relative bound on a sun pick's total pdf from the quadratic sky-pdf fit (SunskyKArgs::
+// sun_sky_fit): 1e-7, a hundredth of the 1e-5 parity bar.
+constexpr float kSunSkyFitTol = 1e-7f;
+
+// Turn the fit on when w dev <= tol ((1 - w) sun_pdf + w fmin) for the staged w_sky: the
+// error of the sky term, relative to the smallest pdf a sun pick can have.
+SS_HD inline void decide_sun_sky_fit(SunskyKArgs* k) {
+    SS_NO_CONTRACT
+    const float w = k->w_sky;
+    k->sun_sky_fit_on = (k->sun_sky_fit_ok &&
+                         w * k->sun_sky_fit_dev <= kSunSkyFitTol * ((1.f - w) * k->sun_pdf + w * k->sun_sky_fit_fmin))
+                            ? 1 : 0;
+}
+
 // The end of estimate_sky_sun_ratio: the per-channel sums of the quadrature rows (added
 // in row order by the caller), luminance, the sky sampling weight and (spectral) the
 // wavelength distribution (ContinuousDistribution over [360, 720] of avg_spec[1..10],
@@ -282,6 +299,7 @@ SS_HD inline bool quad_finish(SunskyKArgs* k, const float* sky_sum, const float*
     float res = sky_lum / (sky_lum + sun_lum);
     if (res != res) res = 0.f;
     k->w_sky = res;
+    decide_sun_sky_fit(k);
     if (!spec) {
         k->spec_size = 0;
         return true;

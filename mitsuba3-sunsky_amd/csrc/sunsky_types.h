@@ -131,6 +131,18 @@ struct SunskyKArgs {
     // corner weight is 0 (integer turbidity / table-node elevation) adds exactly +0
     int   tgmm_count;
     uint8_t tgmm_idx[kNbMixture];
+    // The sky pdf at a SUN pick (the FAST sampling kernels).  A sun pick's pdf is
+    // (1 - w) sun_pdf + w sky_pdf(d) (sunsky.cpp:711-723 with check_sun = false), d inside the
+    // disc, and sky_pdf = tgmm_pdf / sin(theta) is smooth over the 0.27-degree disc.  The host
+    // fits it with a quadratic in the disc coordinates (a, b) of the sun frame
+    // (square_to_uniform_cone's x, y; sun_sky_fit[6]: c0 + a (c1 + c3 a + c4 b) + b (c2 + c5 b)),
+    // bounds the fit's deviation over the disc (sun_sky_fit_dev, with the smallest value
+    // sun_sky_fit_fmin), and the staging turns it on only where w dev stays below
+    // kSunSkyFitTol of the smallest total pdf (decide_sun_sky_fit, once w_sky is known).
+    float sun_sky_fit[6];
+    float sun_sky_fit_dev, sun_sky_fit_fmin;
+    int   sun_sky_fit_ok;          // host: the disc lies away from the zenith, the horizon and the phi wrap
+    int   sun_sky_fit_on;          // staging: sun_sky_fit_ok and the bound holds for this w_sky
     // -------- wavelength sampling (ContinuousDistribution over [360, 720])
     int   spec_size;               // 10 (JIT) / 2 (scalar) / 0 (RGB)
     float spec_pdf[10], spec_cdf[9];

@@ -21,7 +21,7 @@ VARIANT_RGB, VARIANT_SPECTRAL = 0, 1
 SEMANTICS_JIT, SEMANTICS_SCALAR = 0, 1
 PRECISION_FAST, PRECISION_REFERENCE = 0, 1
 TABLES = {"sky_params": 0, "sky_radiance": 1, "sun_radiance": 2, "sun_ld": 3, "gaussians": 4,
-          "gaussian_cdf": 5, "spectral_pdf": 6, "spectral_cdf": 7, "albedo": 8}
+          "gaussian_cdf": 5, "spectral_pdf": 6, "spectral_cdf": 7, "albedo": 8, "sun_sky_fit": 9}
 FLAG_INFINITE, FLAG_SPATIALLY_VARYING = 0x04, 0x10
 PARAMS = {"turbidity": 0, "albedo": 1, "sun_direction": 2}   # sunsky_param (differentiable, sunsky.cpp:220-240)
 MAX_LAMBDA_PER_RAY = 16   # kMaxLambdaPerRay (csrc/sunsky_types.h)

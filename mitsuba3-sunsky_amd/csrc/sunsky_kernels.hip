@@ -892,18 +892,25 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
     }
 }
 
+template <bool FAST>
+__device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
+                                           const float* sun_tab, const float* ldp, const DirTerms& t,
+                                           const float lam[4], float e[4]);
+
 // ======================================================================
 // eval(): spectral with per-ray wavelengths (Mitsuba Spectrum<Float, k>):
 // lambda plane k at lam + k * lstride, out plane k at out + k * ostride.
 // ======================================================================
-template <int VEC, bool FAST, bool NEG>
+template <int VEC, bool FAST, bool NEG, bool E4 = false>
 __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                                     const float* __restrict__ wy, const float* __restrict__ wz,
                                                     const float* __restrict__ lam, size_t lstride, int nlam,
                                                     const uint8_t* __restrict__ active, size_t n,
                                                     float* __restrict__ out, size_t ostride) {
     __shared__ ChanLds<FAST> S;
+    __shared__ alignas(16) float ldp[E4 ? kNbWavelengths * 2 * kNbSunLdParams : 4];   // eval_spec4's LdPairs layout
     const auto* chans = stage_chans<FAST>(K, &S);
+    if (E4 && nlam == 4) stage_ld_pairs(K.sun_ld, ldp);
     __syncthreads();
     const size_t nvec = n / VEC;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -918,6 +925,26 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (k < nlam) load_vec<VEC>(lam + (size_t)k * lstride, i, l4[k]);
+        if (E4 && nlam == 4) {
+            // E4 (probe builds): ray-outer through the branchless eval_spec4 (bitwise
+            // eval_spec_one per wavelength), one ray's terms live at a time; the 4 x VEC
+            // outputs wait in registers for the 16-byte stores
+            float o[4][VEC];
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) {
+                DirTerms t = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);
+                add_sun_terms<FAST>(K, t);
+                const float lj[4] = {l4[0][j], l4[1][j], l4[2][j], l4[3][j]};
+                float e[4];
+                eval_spec4<FAST>(K, chans, K.sun_table, ldp, t, lj, e);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) o[k][j] = e[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) store_vec<VEC>(out + (size_t)k * ostride, i, o[k]);
+            continue;
+        }
+        {
         DirTerms t[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
@@ -938,6 +965,7 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
                 for (int j = 0; j < VEC; ++j) o[j] = eval_spec_one<FAST>(K, chans, K.sun_table, K.sun_ld, t[j], l4[k][j]);
                 store_vec<VEC>(out + (size_t)(k0 + k) * ostride, i, o);
             }
+        }
         }
     }
 }
@@ -3451,6 +3479,19 @@ SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_dir_fast, 4, true, false)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_dir_fast, 1, true, false)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_dir_ref, 4, false, false)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_dir_ref, 1, false, false)
+#ifdef SS_PROBE_RAYS_VARIANTS   // probe builds (tools/Makefile build/probe_rays.hsaco) only: loop-shape A/B
+#define SS_EVAL_SPEC_RAYS_PROBE(NAME, VEC, E4)                                                                  \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
+        const SunskyKArgs* __restrict__ Kp, const float* wx, const float* wy, const float* wz, const float* lam, size_t lstride,    \
+        int nlam, const uint8_t* active, size_t n, float* out, size_t ostride, float sign) {                   \
+        (void)sign;                                                                                            \
+        eval_spec_rays_body<VEC, true, true, E4>(*Kp, wx, wy, wz, lam, lstride, nlam, active, n, out, ostride); \
+    }
+SS_EVAL_SPEC_RAYS_PROBE(probe_rays_v2_fast, 2, false)
+SS_EVAL_SPEC_RAYS_PROBE(probe_rays_e4_v4_fast, 4, true)
+SS_EVAL_SPEC_RAYS_PROBE(probe_rays_e4_v2_fast, 2, true)
+SS_EVAL_SPEC_RAYS_PROBE(probe_rays_e4_v1_fast, 1, true)
+#endif
 
 #define SS_SAMPLE_DIRECTION(NAME, FAST, SPEC, LEAN)                                                           \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \

@@ -293,12 +293,15 @@ def test_sun_disc_tangent_along_sun_direction(variant):
     """the sun-disc part of the sun_direction tangent -- d cos(psi) / d s in the
     limb darkening (sunsky.cpp:631-650) and, for RGB, in the cos(psi) powers of render_sun
     (:572-614), through gamma = unit_angle(s, wo) (:311) -- on lanes well inside the disc,
-    alpha/32 <= gamma <= alpha/4 (alpha/2 = the half aperture), which the sun_direction check
-    above masks out.  The step h = 1e-4 along tangents orthogonal to s cannot flip the disc
-    test there (alpha/4 = 2.3e-3), and the disc radiance is a smooth function of cos(gamma)
-    on the scale of the aperture, so the central differences of the fp64 oracle are accurate
-    to (h / (alpha/2))^2 ~ 5e-4.  JVP per lane and the VJP's sun-axis gradient projected on
-    the tangent (sum over the disc lanes with a random cotangent) against them."""
+    alpha/8 <= gamma <= alpha/4 (alpha/2 = the half aperture), which the sun_direction check
+    above masks out.  Steps of up to 2h = 4e-4 along tangents orthogonal to s cannot flip
+    the disc test there (alpha/4 = 2.3e-3), and the disc radiance is a smooth function of
+    cos(gamma) on the scale of the aperture, so the 4-point central differences of the fp64
+    oracle are accurate to ~(h / (alpha/4))^4 / 30 ~ 2e-6; their noise is the fp32 rounding
+    of the perturbed sun direction the oracle takes (~3e-8 / h).  Below alpha/8 the fp32
+    chord wo . ds of the kernel's d gamma cancels (6e-8 / gamma relative), as in the
+    reference's own fp32 AD.  JVP per lane and the VJP's sun-axis gradient projected on the
+    tangent (sum over the disc lanes with a random cotangent) against them."""
     d = scene()
     em = ss.load_dict(d, variant=variant)
     o32 = O.Oracle(d, variant, "jit", "f32")
@@ -306,7 +309,7 @@ def test_sun_disc_tangent_along_sun_direction(variant):
     half = math.acos(inf["cos_cutoff"])
     wo = sun_cone_wo(16384, inf["sun_dir_local"], half, seed=21, scale=0.5)
     gam = np.arccos(np.clip(wo.astype(np.float64) @ inf["sun_dir_local"], -1.0, 1.0))
-    wo = wo[gam >= half / 16]
+    wo = wo[gam >= half / 4]
     n = wo.shape[0]
     wi = -wo
     rng = np.random.default_rng(22)
@@ -321,12 +324,11 @@ def test_sun_disc_tangent_along_sun_direction(variant):
     cot = rng.standard_normal((k, n))
     grad, view = em.eval_vjp(si, torch.from_numpy(cot.astype(np.float32)).cuda())
     g_sun = view["sun_direction"].cpu().numpy().astype(np.float64)
-    h = 1e-4
-    ev = lambda dd: O.Oracle(dd, variant, "jit", "f64").eval(wi, lam_o)   # noqa: E731
+    h = 2e-4
+    ev = lambda k, t: O.Oracle(scene(sun=(s + k * h * t) / np.linalg.norm(s + k * h * t)), variant, "jit",  # noqa: E731
+                               "f64").eval(wi, lam_o)
     for t in (t1, t2, 0.6 * t1 + 0.8 * t2):
-        plus = scene(sun=(s + h * t) / np.linalg.norm(s + h * t))
-        minus = scene(sun=(s - h * t) / np.linalg.norm(s - h * t))
-        fd = (ev(plus) - ev(minus)) / (2 * h)
+        fd = (8 * (ev(1, t) - ev(-1, t)) - (ev(2, t) - ev(-2, t))) / (12 * h)
         fd = fd.T if variant == "spectral" else fd
         _, dval = em.eval_jvp(si, "sun_direction", list(t))
         dval = dval.cpu().numpy().T.astype(np.float64)

@@ -210,8 +210,7 @@ def test_two_queued_updates_with_a_rejection(second):
     params = em.traverse()
     params["turbidity"] = 6.0
     params.update()                                # rejected
-    params = em.traverse()
-    params["albedo"] = 0.45
+    params["albedo"] = 0.45                        # (traverse() would read the state back)
     params.update()                                # accepted or rejected
     with pytest.raises(ValueError, match="non-negative"):
         em.info()

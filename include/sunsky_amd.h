@@ -42,9 +42,11 @@
 extern "C" {
 #endif
 
-#define SUNSKY_AMD_ABI_VERSION 5   /* 3: direct_diffuse visibility, direct_diffuse_rays; 4: direct_conductor(_rays),
+#define SUNSKY_AMD_ABI_VERSION 6   /* 3: direct_diffuse visibility, direct_diffuse_rays; 4: direct_conductor(_rays),
                                      emitter_tangent_tables, direct_diffuse draws sample_1 (path.cpp:233);
-                                     5: direct_conductor(_rays)_aniso (alpha_u, alpha_v) */
+                                     5: direct_conductor(_rays)_aniso (alpha_u, alpha_v);
+                                     6: SUNSKY_TABLE_SUN_SKY_FIT, emitter_inject_staging_fault (testing),
+                                        a rejected update reverts to the last accepted one */
 
 typedef enum sunsky_status {
     SUNSKY_OK = 0,

@@ -20,7 +20,7 @@ def test_library_exports_every_declared_symbol():
     assert len(declared) >= 30
     missing = [f for f in declared if not hasattr(L, f)]
     assert not missing, missing
-    assert ss.lib().sunsky_abi_version() == 5
+    assert ss.lib().sunsky_abi_version() == 6
     assert os.path.exists(ss.CODE_OBJECT), "gfx950 code object not built"
 
 

@@ -644,6 +644,25 @@ __device__ __forceinline__ float eval_spec_one(const SunskyKArgs& K, const typen
     return res;
 }
 
+// eval_spec_one without per-wavelength branches on the sky side (the per-ray kernels, where
+// random wavelengths almost never sit on a node): the channel pair clamped to (lo, lo + 1)
+// with lo <= 9 and f in [0, 1], both sky evaluations always, as eval_spec4 does -- lerpf_
+// returns its operands exactly at f = 0 and f = 1, so a node and 720 nm give eval_spec_one's
+// bits -- and the sun term in the one rare branch with eval_spec_one's own (lo, f).
+template <bool FAST>
+__device__ __forceinline__ float eval_spec_one_flat(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
+                                                    const float* sun_tab, const float* ld_tab, const DirTerms& t,
+                                                    float lambda) {
+    const float nw = wavelength_node(lambda);
+    const bool ok = t.active && (0.f <= nw) && (nw <= (float)(kNbWavelengths - 1));
+    const int c = ok ? (int)floorf(nw) : 0;
+    const int lo = c < kNbWavelengths - 2 ? c : kNbWavelengths - 2;
+    const float f = ok ? nw - (float)lo : 0.f;
+    float res = lerpf_(sky_eval<FAST>(chans[lo], t, K.sky_scale), sky_eval<FAST>(chans[lo + 1], t, K.sky_scale), f);
+    if (t.hit_sun && ok) res += sun_spec_term<FAST>(K, sun_tab, ld_tab, t, c, nw - (float)c);
+    return ok ? res : 0.f;
+}
+
 // ------------------------------------------------------------ memory helpers
 template <int VEC>
 __device__ __forceinline__ void load_vec(const float* p, size_t i, float v[VEC]) {
@@ -892,25 +911,67 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
     }
 }
 
-template <bool FAST>
-__device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
-                                           const float* sun_tab, const float* ldp, const DirTerms& t,
-                                           const float lam[4], float e[4]);
-
 // ======================================================================
 // eval(): spectral with per-ray wavelengths (Mitsuba Spectrum<Float, k>):
 // lambda plane k at lam + k * lstride, out plane k at out + k * ostride.
 // ======================================================================
-template <int VEC, bool FAST, bool NEG, bool E4 = false>
+// PF (nlam == 4 only): software-pipelined grid-stride loop -- the next group's directions and
+// wavelengths are loaded before this group's evaluation, so their HBM latency overlaps it.
+template <int VEC, bool FAST, bool NEG>
+__device__ __forceinline__ void eval_spec_rays_pf_body(const SunskyKArgs& K, const float* __restrict__ wx,
+                                                       const float* __restrict__ wy, const float* __restrict__ wz,
+                                                       const float* __restrict__ lam, size_t lstride,
+                                                       const uint8_t* __restrict__ active, size_t n,
+                                                       float* __restrict__ out, size_t ostride) {
+    __shared__ ChanLds<FAST> S;
+    const auto* chans = stage_chans<FAST>(K, &S);
+    __syncthreads();
+    const size_t nvec = n / VEC;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    float nx[VEC], ny[VEC], nz[VEC], nl[4][VEC];
+    bool nm[VEC];
+    auto load = [&](size_t vv) {
+        load_dirs<VEC>(wx, wy, wz, active, vv * VEC, nx, ny, nz, nm);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) load_vec<VEC>(lam + (size_t)k * lstride, vv * VEC, nl[k]);
+    };
+    if (v < nvec) load(v);
+    for (; v < nvec; v += stride) {
+        const size_t i = v * VEC;
+        float x[VEC], y[VEC], z[VEC], l4[4][VEC];
+        bool m[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            x[j] = nx[j]; y[j] = ny[j]; z[j] = nz[j]; m[j] = nm[j];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) l4[k][j] = nl[k][j];
+        }
+        if (v + stride < nvec) load(v + stride);
+        DirTerms t[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+            t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);
+            add_sun_terms<FAST>(K, t[j]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float o[VEC];
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) o[j] = eval_spec_one_flat<FAST>(K, chans, K.sun_table, K.sun_ld, t[j], l4[k][j]);
+            store_vec<VEC>(out + (size_t)k * ostride, i, o);
+        }
+    }
+}
+
+template <int VEC, bool FAST, bool NEG>
 __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                                     const float* __restrict__ wy, const float* __restrict__ wz,
                                                     const float* __restrict__ lam, size_t lstride, int nlam,
                                                     const uint8_t* __restrict__ active, size_t n,
                                                     float* __restrict__ out, size_t ostride) {
     __shared__ ChanLds<FAST> S;
-    __shared__ alignas(16) float ldp[E4 ? kNbWavelengths * 2 * kNbSunLdParams : 4];   // eval_spec4's LdPairs layout
     const auto* chans = stage_chans<FAST>(K, &S);
-    if (E4 && nlam == 4) stage_ld_pairs(K.sun_ld, ldp);
     __syncthreads();
     const size_t nvec = n / VEC;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
@@ -925,26 +986,6 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (k < nlam) load_vec<VEC>(lam + (size_t)k * lstride, i, l4[k]);
-        if (E4 && nlam == 4) {
-            // E4 (probe builds): ray-outer through the branchless eval_spec4 (bitwise
-            // eval_spec_one per wavelength), one ray's terms live at a time; the 4 x VEC
-            // outputs wait in registers for the 16-byte stores
-            float o[4][VEC];
-#pragma unroll
-            for (int j = 0; j < VEC; ++j) {
-                DirTerms t = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);
-                add_sun_terms<FAST>(K, t);
-                const float lj[4] = {l4[0][j], l4[1][j], l4[2][j], l4[3][j]};
-                float e[4];
-                eval_spec4<FAST>(K, chans, K.sun_table, ldp, t, lj, e);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) o[k][j] = e[k];
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) store_vec<VEC>(out + (size_t)k * ostride, i, o[k]);
-            continue;
-        }
-        {
         DirTerms t[VEC];
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
@@ -962,10 +1003,14 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
                 if (k0 + k >= nlam) break;
                 float o[VEC];
 #pragma unroll
-                for (int j = 0; j < VEC; ++j) o[j] = eval_spec_one<FAST>(K, chans, K.sun_table, K.sun_ld, t[j], l4[k][j]);
+                for (int j = 0; j < VEC; ++j)
+#ifndef SS_PROBE_RAYS_BRANCHY   // probe build (A/B of the branching per-wavelength eval): never in the product
+                    o[j] = eval_spec_one_flat<FAST>(K, chans, K.sun_table, K.sun_ld, t[j], l4[k][j]);
+#else
+                    o[j] = eval_spec_one<FAST>(K, chans, K.sun_table, K.sun_ld, t[j], l4[k][j]);
+#endif
                 store_vec<VEC>(out + (size_t)(k0 + k) * ostride, i, o);
             }
-        }
         }
     }
 }
@@ -1618,10 +1663,10 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
 
 // One spectral sample at 4 wavelengths (u, lambda -> d, pdf, 4 weights): the per-sample
 // work of sample_direction_spec4_body in the same operation order (bitwise its outputs).
-template <bool FAST>
+template <bool FAST, int KIND = 0>
 __device__ __forceinline__ void sample_one_spec4(const SunskyKArgs& K, const SamplerLds<FAST, true>& S, float sx,
                                                  float sy, const float l[4], float inv_w, float inv_w_sun, float o[8]) {
-    const bool pick_sky = sx < K.w_sky;
+    const bool pick_sky = KIND == 1 ? true : KIND == 2 ? false : sx < K.w_sky;   // KIND: sample_one_rgb
     float sun_a = 0.f, sun_b = 0.f;
     const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun, &sun_a, &sun_b);
     const bool act = sd.z >= 0.f;
@@ -1682,7 +1727,8 @@ __device__ __forceinline__ void sample_direction_spec4_sorted_body(
     if (w < nwin) load_window(w);
     for (; w < nwin; w += wstep) {
         const size_t base = w * W;
-        int slot[R];
+        int slot[R], nsky = 0;
+        (void)nsky;
         {
             float a[R], b[R], l[4][R];
             uint64_t m[R];
@@ -1712,6 +1758,7 @@ __device__ __forceinline__ void sample_direction_spec4_sorted_body(
                 psky += c;
                 psun += 64 - c;
             }
+            nsky = psky;
         }
         wave_lds_order();
 #pragma unroll 1
@@ -1719,6 +1766,11 @@ __device__ __forceinline__ void sample_direction_spec4_sorted_body(
             const int q = p * 64 + lane;
             const float l4[4] = {Y[2][q], Y[3][q], Y[4][q], Y[5][q]};
             float o[8];
+#ifdef SS_PROBE_SPEC_UNIFORM_PASSES   // probe build: specialised sky / sun passes, measured 0.7 % slower here
+            if (p * 64 + 64 <= nsky) sample_one_spec4<FAST, 1>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);
+            else if (p * 64 >= nsky) sample_one_spec4<FAST, 2>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);
+            else
+#endif
             sample_one_spec4<FAST>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);
 #pragma unroll
             for (int k = 0; k < 8; ++k) Y[k][q] = o[k];
@@ -1740,10 +1792,12 @@ __device__ __forceinline__ void sample_direction_spec4_sorted_body(
 // One RGB sample (u -> d, pdf, weight), the per-sample work of
 // sample_direction_body<FAST, false, LEAN> in the same operation order; `act` is the
 // caller's mask (true in the LEAN form).
-template <bool FAST>
+// KIND: 0 = each lane's own pick (u.x < w_sky); 1 / 2 = a sorted pass known to hold sky /
+// sun picks only (the same pick on every lane, so the other branch is compiled out).
+template <bool FAST, int KIND = 0>
 __device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const SamplerLds<FAST, false>& S, float sx,
                                                float sy, bool act, float inv_w, float inv_w_sun, float o[7]) {
-    const bool pick_sky = sx < K.w_sky;
+    const bool pick_sky = KIND == 1 ? true : KIND == 2 ? false : sx < K.w_sky;
     float sun_a = 0.f, sun_b = 0.f;
 #ifndef SS_PROBE_NO_SKY_SAMPLE   // probe builds (tools/Makefile) only: cost ablations
     const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun, &sun_a, &sun_b);
@@ -1824,7 +1878,7 @@ __device__ __forceinline__ void sample_direction_sorted_body(
     if (w < nwin) load_window(w);
     for (; w < nwin; w += wstep) {
         const size_t base = w * W;
-        int slot[R];
+        int slot[R], nsky = 0;
         {
             float a[R], b[R];
             uint64_t m[R];
@@ -1851,6 +1905,7 @@ __device__ __forceinline__ void sample_direction_sorted_body(
                 psky += c;
                 psun += 64 - c;
             }
+            nsky = psky;
         }
         // FULL: this window's it.p, loaded before the passes and consumed after them
         float ipx[FULL ? R : 1], ipy[FULL ? R : 1], ipz[FULL ? R : 1];
@@ -1870,6 +1925,13 @@ __device__ __forceinline__ void sample_direction_sorted_body(
             const int q = p * 64 + lane;
             const bool act = FULL && active ? Y[2][q] != 0.f : true;
             float o[7];
+#ifndef SS_PROBE_MIXED_PASSES   // probe build (A/B of the per-lane pick in every pass): never in the product
+            // ranks [0, nsky) are the window's sky picks: a pass wholly on one side takes the
+            // specialised body (wave-uniform branch)
+            if (p * 64 + 64 <= nsky) sample_one_rgb<FAST, 1>(K, S, Y[0][q], Y[1][q], act, inv_w, inv_w_sun, o);
+            else if (p * 64 >= nsky) sample_one_rgb<FAST, 2>(K, S, Y[0][q], Y[1][q], act, inv_w, inv_w_sun, o);
+            else
+#endif
             sample_one_rgb<FAST>(K, S, Y[0][q], Y[1][q], act, inv_w, inv_w_sun, o);
 #pragma unroll
             for (int k = 0; k < 7; ++k) Y[k][q] = o[k];
@@ -3479,19 +3541,19 @@ SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_dir_fast, 4, true, false)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_dir_fast, 1, true, false)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_dir_ref, 4, false, false)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_dir_ref, 1, false, false)
-#ifdef SS_PROBE_RAYS_VARIANTS   // probe builds (tools/Makefile build/probe_rays.hsaco) only: loop-shape A/B
-#define SS_EVAL_SPEC_RAYS_PROBE(NAME, VEC, E4)                                                                  \
+#ifdef SS_PROBE_RAYS_PF   // probe builds only: the software-pipelined per-ray eval at 4 wavelengths
+#define SS_EVAL_SPEC_RAYS_PF(NAME, VEC)                                                                        \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
         const SunskyKArgs* __restrict__ Kp, const float* wx, const float* wy, const float* wz, const float* lam, size_t lstride,    \
         int nlam, const uint8_t* active, size_t n, float* out, size_t ostride, float sign) {                   \
-        (void)sign;                                                                                            \
-        eval_spec_rays_body<VEC, true, true, E4>(*Kp, wx, wy, wz, lam, lstride, nlam, active, n, out, ostride); \
+        (void)sign; (void)nlam;                                                                                \
+        eval_spec_rays_pf_body<VEC, true, true>(*Kp, wx, wy, wz, lam, lstride, active, n, out, ostride);       \
     }
-SS_EVAL_SPEC_RAYS_PROBE(probe_rays_v2_fast, 2, false)
-SS_EVAL_SPEC_RAYS_PROBE(probe_rays_e4_v4_fast, 4, true)
-SS_EVAL_SPEC_RAYS_PROBE(probe_rays_e4_v2_fast, 2, true)
-SS_EVAL_SPEC_RAYS_PROBE(probe_rays_e4_v1_fast, 1, true)
+SS_EVAL_SPEC_RAYS_PF(probe_rays_pf_v4_fast, 4)
+SS_EVAL_SPEC_RAYS_PF(probe_rays_pf_v2_fast, 2)
+SS_EVAL_SPEC_RAYS_PF(probe_rays_pf_v1_fast, 1)
 #endif
+
 
 #define SS_SAMPLE_DIRECTION(NAME, FAST, SPEC, LEAN)                                                           \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \

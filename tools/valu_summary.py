@@ -41,6 +41,19 @@ def main(root):
                 disp[k].add(r["Dispatch_Id"])
         for k, c in acc.items():
             nd = len(disp[k])
+            if "SQ_WAIT_ANY" in c:   # the stall pass (gpu_valu.sh C2): where the wave cycles go
+                wc = c["SQ_WAVE_CYCLES"]
+                out.setdefault(k, {}).update({
+                    "stall": {"wait_any_frac": c["SQ_WAIT_ANY"] / wc, "wait_inst_any_frac": c["SQ_WAIT_INST_ANY"] / wc,
+                              "active_inst_any_frac": c["SQ_ACTIVE_INST_ANY"] / wc,
+                              "wait_inst_lds_frac": c["SQ_WAIT_INST_LDS"] / wc,
+                              "active_inst_valu_frac": c["SQ_ACTIVE_INST_VALU"] / wc,
+                              "active_inst_lds_frac": c["SQ_ACTIVE_INST_LDS"] / wc,
+                              "lds_bank_conflict_per_dispatch": c["SQ_LDS_BANK_CONFLICT"] / nd,
+                              "note": "fractions of SQ_WAVE_CYCLES: WAIT_ANY = parked on s_waitcnt / barrier, "
+                                      "WAIT_INST_ANY = issue stalls, ACTIVE_INST_ANY = issuing (disjoint, "
+                                      "MI355X_MICROARCH.md PMC table)"}})
+                continue
             N, T = c["SQ_INSTS_VALU"] / nd, c["SQ_INSTS_VALU_TRANS_F32"] / nd
             waves = c["SQ_WAVES"] / nd
             t_valu = ((N - T) * PLAIN + T * TRANS) / (SIMDS * CLK)
@@ -60,7 +73,7 @@ def main(root):
                         rec["kernel_ms"] = us * 1e-3
                         rec["valu_frac"] = t_valu * 1e3 / rec["kernel_ms"]
                         break
-            out[k] = rec
+            out.setdefault(k, {}).update(rec)
     print(json.dumps(out, indent=1))
 
 

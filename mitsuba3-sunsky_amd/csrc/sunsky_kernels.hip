@@ -460,11 +460,15 @@ __device__ __forceinline__ void stage_sun_rows(const SunskyKArgs& K, SunRowsRgb*
     }
 }
 
+// HOIST: the 4 control-point rows unrolled with no scheduling barrier, so their LDS reads
+// can be issued ahead of the Horner steps (callers with VGPRs to spare: the sorted RGB
+// sampler runs at 4 waves/SIMD, held there by its LDS, with ~35 VGPRs below the 4-wave cap).
+template <bool HOIST = false>
 __device__ __forceinline__ void render_sun_rgb_rows(const SunRowsRgb& R, int row, float x, float cpsi,
                                                     float out[3]) {
     static_assert(kNbSunLdParams == 6 && kSunRowFloats == 20, "row slots: 12 pair values, 6 channel-2 values, 2 pad");
     float r0 = 0.f, r1 = 0.f, r2 = 0.f;
-#pragma unroll 1
+#pragma unroll (HOIST ? 2 : 1)
     for (int k = kNbSunCtrlPts - 1; k >= 0; --k) {
         const float4* q = R.r[row][k];
         float v[kSunRowFloats];
@@ -480,7 +484,7 @@ __device__ __forceinline__ void render_sun_rgb_rows(const SunRowsRgb& R, int row
         // Channel 2 first, then the pairs, with the scheduler held between them: without the
         // barrier it hoists all five reads (and more around them) and the callers' register
         // peaks rise (direct_conductor 0 -> 19 spilled VGPRs, the sorted sampler 96 -> 111).
-        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!HOIST) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const float4 b = q[i];
@@ -504,7 +508,7 @@ __device__ __forceinline__ void render_sun_rgb_rows(const SunRowsRgb& R, int row
 // Full RGB eval for one local direction (sunsky.cpp:317-323).
 // chans: the 3 channels (K.fsky / K.sky, or an LDS copy in the sampling kernels,
 // whose other constants already fill the SGPR file).
-template <bool FAST>
+template <bool FAST, bool HOIST = false>
 __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
                                                const float* sun_tab, float3_ wo, bool mask, float out[3],
                                                const SunRowsRgb* rows = nullptr) {
@@ -520,7 +524,7 @@ __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const typen
             const int row = t.sun_pos - K.sun_row_lo;
             if (rows && row >= 0 && row < kSunRowsLds) {
                 float sr[3];
-                render_sun_rgb_rows(*rows, row, t.sun_x, t.sun_cpsi, sr);
+                render_sun_rgb_rows<HOIST>(*rows, row, t.sun_x, t.sun_cpsi, sr);
 #pragma unroll
                 for (int c = 0; c < 3; ++c) out[c] += K.sun_mul * sr[c];
             } else {
@@ -1794,7 +1798,7 @@ __device__ __forceinline__ void sample_direction_spec4_sorted_body(
 // caller's mask (true in the LEAN form).
 // KIND: 0 = each lane's own pick (u.x < w_sky); 1 / 2 = a sorted pass known to hold sky /
 // sun picks only (the same pick on every lane, so the other branch is compiled out).
-template <bool FAST, int KIND = 0>
+template <bool FAST, int KIND = 0, bool HOIST = false>
 __device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const SamplerLds<FAST, false>& S, float sx,
                                                float sy, bool act, float inv_w, float inv_w_sun, float o[7]) {
     const bool pick_sky = KIND == 1 ? true : KIND == 2 ? false : sx < K.w_sky;
@@ -1816,7 +1820,7 @@ __device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const Sampl
     o[0] = d.x; o[1] = d.y; o[2] = d.z; o[3] = pd;
     float e[3];
 #ifndef SS_PROBE_NO_WEIGHT
-    eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, to_local(K, d), act, e, S.rows);
+    eval_rgb_local<FAST, HOIST>(K, S.chans.c, K.sun_table, to_local(K, d), act, e, S.rows);
 #else
     e[0] = d.x; e[1] = d.y; e[2] = d.z;
 #endif
@@ -1854,6 +1858,12 @@ __device__ __forceinline__ void sample_direction_sorted_body(
         dist = opx = opy = opz = nullptr;
     }
     constexpr int W = 64 * R;
+#ifndef SS_PROBE_SUN_ROWS_BARRIER   // probe build (A/B of the hoisted sun rows): never in the product
+    // the LEAN form has VGPRs to spare below the 4-wave cap its LDS sets: hoist the sun-row reads
+    constexpr bool kHoist = !FULL;
+#else
+    constexpr bool kHoist = false;
+#endif
     __shared__ SamplerLds<FAST, false> S;
     __shared__ float X[SS_BLOCK / 64][7][W];
     stage_sampler_lds<FAST, false>(K, &S);
@@ -1928,11 +1938,11 @@ __device__ __forceinline__ void sample_direction_sorted_body(
 #ifndef SS_PROBE_MIXED_PASSES   // probe build (A/B of the per-lane pick in every pass): never in the product
             // ranks [0, nsky) are the window's sky picks: a pass wholly on one side takes the
             // specialised body (wave-uniform branch)
-            if (p * 64 + 64 <= nsky) sample_one_rgb<FAST, 1>(K, S, Y[0][q], Y[1][q], act, inv_w, inv_w_sun, o);
-            else if (p * 64 >= nsky) sample_one_rgb<FAST, 2>(K, S, Y[0][q], Y[1][q], act, inv_w, inv_w_sun, o);
+            if (p * 64 + 64 <= nsky) sample_one_rgb<FAST, 1, kHoist>(K, S, Y[0][q], Y[1][q], act, inv_w, inv_w_sun, o);
+            else if (p * 64 >= nsky) sample_one_rgb<FAST, 2, kHoist>(K, S, Y[0][q], Y[1][q], act, inv_w, inv_w_sun, o);
             else
 #endif
-            sample_one_rgb<FAST>(K, S, Y[0][q], Y[1][q], act, inv_w, inv_w_sun, o);
+            sample_one_rgb<FAST, 0, kHoist>(K, S, Y[0][q], Y[1][q], act, inv_w, inv_w_sun, o);
 #pragma unroll
             for (int k = 0; k < 7; ++k) Y[k][q] = o[k];
         }

@@ -508,14 +508,14 @@ __device__ __forceinline__ void render_sun_rgb_rows(const SunRowsRgb& R, int row
 // Full RGB eval for one local direction (sunsky.cpp:317-323).
 // chans: the 3 channels (K.fsky / K.sky, or an LDS copy in the sampling kernels,
 // whose other constants already fill the SGPR file).
-template <bool FAST, bool HOIST = false>
+template <bool FAST, bool HOIST = false, bool PROBE_NO_SKY = false>
 __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
                                                const float* sun_tab, float3_ wo, bool mask, float out[3],
                                                const SunRowsRgb* rows = nullptr) {
     DirTerms t = dir_terms<FAST>(K, wo, mask);
     if constexpr (FAST) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) out[c] = sky_fast(chans[c], t);   // sky_scale and CIE folded
+        for (int c = 0; c < 3; ++c) out[c] = PROBE_NO_SKY ? t.gamma : sky_fast(chans[c], t);   // sky_scale and CIE folded
 #ifdef SS_PROBE_NO_SUN_DISC   // probe builds (tools/Makefile) only: cost ablations
         t.hit_sun = false;
 #endif
@@ -1820,7 +1820,11 @@ __device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const Sampl
     o[0] = d.x; o[1] = d.y; o[2] = d.z; o[3] = pd;
     float e[3];
 #ifndef SS_PROBE_NO_WEIGHT
+#ifdef SS_PROBE_SUNPICK_NO_SKY   // probe build (cost bound of the sun picks' sky radiance): wrong results
+    eval_rgb_local<FAST, HOIST, KIND == 2>(K, S.chans.c, K.sun_table, to_local(K, d), act, e, S.rows);
+#else
     eval_rgb_local<FAST, HOIST>(K, S.chans.c, K.sun_table, to_local(K, d), act, e, S.rows);
+#endif
 #else
     e[0] = d.x; e[1] = d.y; e[2] = d.z;
 #endif

@@ -145,6 +145,14 @@ int main(int argc, char** argv) {
         // bound of sample_direction; outputs differ from the unsorted run by construction)
         // KB_SORT_U=2: only partitioned, sky picks (u.x < w_sky) first, each class in its
         // random order (the bound of removing the sky/sun divergence alone)
+        // KB_UX_CLASS=sky / sun: every sample a sky (u.x in [0, w_sky)) or a sun pick (the
+        // per-class cost of sample_direction)
+        if (const char* uc = std::getenv("KB_UX_CLASS")) {
+            const float ws = model.kargs().w_sky;
+            const bool sky = std::string(uc) == "sky";
+            for (size_t i = 0; i < n; ++i) u[i] = sky ? u[i] * ws * 0.999999f : ws + (1.f - ws) * u[i];
+            for (size_t i = 0; i < n; ++i) u[i] = sky ? std::min(u[i], std::nextafter(ws, 0.f)) : std::max(u[i], ws);
+        }
         if (const char* su = std::getenv("KB_SORT_U")) {
             if (std::atoi(su) == 2) {
                 const float ws = model.kargs().w_sky;

@@ -670,29 +670,6 @@ __device__ __forceinline__ float eval_spec_one_flat(const SunskyKArgs& K, const 
     return ok ? res : 0.f;
 }
 
-// Two wavelengths of one ray through eval_spec_one_flat's operations, with the four channel
-// records read before any of the four sky evaluations (12 LDS reads in flight instead of 6).
-template <bool FAST>
-__device__ __forceinline__ void eval_spec_two_flat(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
-                                                   const float* sun_tab, const float* ld_tab, const DirTerms& t,
-                                                   float la, float lb, float* oa, float* ob) {
-    const float nwa = wavelength_node(la), nwb = wavelength_node(lb);
-    const bool oka = t.active && (0.f <= nwa) && (nwa <= (float)(kNbWavelengths - 1));
-    const bool okb = t.active && (0.f <= nwb) && (nwb <= (float)(kNbWavelengths - 1));
-    const int ca = oka ? (int)floorf(nwa) : 0, cb = okb ? (int)floorf(nwb) : 0;
-    const int loa = ca < kNbWavelengths - 2 ? ca : kNbWavelengths - 2, lob = cb < kNbWavelengths - 2 ? cb : kNbWavelengths - 2;
-    const float fa = oka ? nwa - (float)loa : 0.f, fb = okb ? nwb - (float)lob : 0.f;
-    const auto a0 = chans[loa], a1 = chans[loa + 1], b0 = chans[lob], b1 = chans[lob + 1];
-    float ra = lerpf_(sky_eval<FAST>(a0, t, K.sky_scale), sky_eval<FAST>(a1, t, K.sky_scale), fa);
-    float rb = lerpf_(sky_eval<FAST>(b0, t, K.sky_scale), sky_eval<FAST>(b1, t, K.sky_scale), fb);
-    if (t.hit_sun) {
-        if (oka) ra += sun_spec_term<FAST>(K, sun_tab, ld_tab, t, ca, nwa - (float)ca);
-        if (okb) rb += sun_spec_term<FAST>(K, sun_tab, ld_tab, t, cb, nwb - (float)cb);
-    }
-    *oa = oka ? ra : 0.f;
-    *ob = okb ? rb : 0.f;
-}
-
 // ------------------------------------------------------------ memory helpers
 template <int VEC>
 __device__ __forceinline__ void load_vec(const float* p, size_t i, float v[VEC]) {
@@ -1028,20 +1005,6 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
                 for (int k = 0; k < 4; ++k)
                     if (k0 + k < nlam) load_vec<VEC>(lam + (size_t)(k0 + k) * lstride, i, l4[k]);
             }
-#ifdef SS_PROBE_RAYS_PAIR   // probe build: two wavelengths' channel records in flight together
-            if (k0 + 4 <= nlam) {
-#pragma unroll
-                for (int k = 0; k < 4; k += 2) {
-                    float o[VEC], o2[VEC];
-#pragma unroll
-                    for (int j = 0; j < VEC; ++j)
-                        eval_spec_two_flat<FAST>(K, chans, K.sun_table, K.sun_ld, t[j], l4[k][j], l4[k + 1][j], &o[j], &o2[j]);
-                    store_vec<VEC>(out + (size_t)(k0 + k) * ostride, i, o);
-                    store_vec<VEC>(out + (size_t)(k0 + k + 1) * ostride, i, o2);
-                }
-                continue;
-            }
-#endif
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (k0 + k >= nlam) break;

@@ -152,16 +152,22 @@ def valu_floor(kernel):
         rec = json.load(fh).get(kernel)
     if not rec:
         return None
-    return {"valu_wave_insts": rec["valu_wave_insts"], "trans_wave_insts": rec["trans_wave_insts"],
-            "issue_floor_ms": rec["valu_issue_floor_ms"], "source": os.path.relpath(files[-1], ROOT)}
+    out = {"valu_wave_insts": rec["valu_wave_insts"], "trans_wave_insts": rec["trans_wave_insts"],
+           "issue_floor_ms": rec["valu_issue_floor_ms"], "source": os.path.relpath(files[-1], ROOT)}
+    if "stall" in rec:   # where the wave cycles go (SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_*)
+        out["wave_cycles"] = {k: v for k, v in rec["stall"].items() if k.endswith("_frac")}
+    return out
 
 
-def valu_frac(floor, ms, clk_mhz=None):
-    """`floor` (valu_floor) against a measured launch time: frac at the nominal 2.4 GHz, and
-    frac_at_gfxclk with the floor rescaled to the clock sampled during the launches."""
+def valu_frac(floor, ms, clk_mhz=None, eff_mhz=None):
+    """`floor` (valu_floor) against a measured launch time: frac at the nominal 2.4 GHz,
+    frac_at_gfxclk with the floor rescaled to amd-smi's sampled clock, and
+    frac_at_effective_clock rescaled to the clock the CUs ran at during the burst (ClockDuring)."""
     out = dict(floor, achieved_ms=ms, frac=floor["issue_floor_ms"] / ms)
     if clk_mhz:
         out["frac_at_gfxclk"] = floor["issue_floor_ms"] * (2400.0 / clk_mhz) / ms
+    if eff_mhz:
+        out["frac_at_effective_clock"] = floor["issue_floor_ms"] * (2400.0 / eff_mhz) / ms
     return out
 
 
@@ -207,9 +213,14 @@ def sclk_under_valu_load(dev):
             time.sleep(0.005)
         torch.cuda.synchronize(dev)
         load_ms = e0.elapsed_time(e1)
+        # every workgroup is resident for the whole launch (8 per CU): its shader-clock cycles
+        # (clock64 at its start and end) over the launch time is the clock it actually ran at
+        cycles = out.view(-1, 2)[:, 0].double().cpu().numpy()
+        eff = float(np.median(cycles)) / (load_ms * 1e-3) / 1e6
         if not samples:
-            return {"error": "no clock sample during the load", "load_ms": load_ms}
-        return {"gfxclk_mhz_median": float(np.median(samples)), "gfxclk_mhz_min": float(min(samples)),
+            return {"error": "no clock sample during the load", "load_ms": load_ms, "effective_mhz_from_cycles": eff}
+        return {"effective_mhz_from_cycles": eff,
+                "gfxclk_mhz_median": float(np.median(samples)), "gfxclk_mhz_min": float(min(samples)),
                 "gfxclk_mhz_max": float(max(samples)), "samples": len(samples), "gfxclk_mhz_idle": float(idle),
                 "load_ms": load_ms,
                 "note": "GFX clock reported by amd-smi (torch.cuda.clock_rate) while every SIMD runs independent FMA "
@@ -217,6 +228,46 @@ def sclk_under_valu_load(dev):
                         "HBM-bound headline does not"}
     finally:
         hip.hipModuleUnload(mod)
+
+
+class ClockDuring:
+    """The shader clock a VALU-bound burst actually runs at: one wave of
+    tools/clock_probe.hip `sunsky_tools_clock_during` on a side stream, launched right after
+    the burst's first kernel, counts shader-clock cycles (s_memtime) over `ms` of the constant
+    100 MHz counter (s_memrealtime).  amd-smi's sampled GFX clock (mean_ms_with_clock) is the
+    power manager's reported figure; this is the one the CUs ran at.  None when the probe's
+    code object is absent."""
+
+    def __init__(self, dev):
+        self.fn = None
+        path = os.path.join(ROOT, "tools", "build", "clock_probe.hsaco")
+        if not os.path.exists(path):
+            return
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        self.mod, fn = ctypes.c_void_p(), ctypes.c_void_p()
+        if self.hip.hipModuleLoad(ctypes.byref(self.mod), path.encode()) != 0:
+            return
+        if self.hip.hipModuleGetFunction(ctypes.byref(fn), self.mod, b"sunsky_tools_clock_during") != 0:
+            return
+        self.fn = fn
+        self.out = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.side = torch.cuda.Stream(dev)
+
+    def launch(self, ms):
+        if self.fn is None:
+            return
+        p_out, ticks = ctypes.c_void_p(self.out.data_ptr()), ctypes.c_uint64(int(ms * 1e5))
+        args = (ctypes.c_void_p * 2)(*[ctypes.cast(ctypes.pointer(x), ctypes.c_void_p) for x in (p_out, ticks)])
+        if self.hip.hipModuleLaunchKernel(self.fn, 1, 1, 1, 64, 1, 1, 0, ctypes.c_void_p(self.side.cuda_stream), args,
+                                          None) != 0:
+            self.fn = None
+
+    def mhz(self):
+        if self.fn is None:
+            return None
+        self.side.synchronize()
+        cyc, ticks = (int(v) for v in self.out.cpu())
+        return cyc / (ticks * 1e-8) / 1e6 if ticks else None
 
 
 def host_cpu_topology():
@@ -918,9 +969,12 @@ def main():
                 pdf_step()
             reps = max(10, args.steps // 4)
             t_s, t_p = KernelTimer(), KernelTimer()
+            cd = ClockDuring(dev)
             t_s.begin()
-            for _ in range(reps):
+            for r_ in range(reps):
                 sample_step()
+                if r_ == 0:
+                    cd.launch(0.4 * reps * 0.8)   # ~40 % of the burst, from its first launch on
             t_s.end(reps)
             t_p.begin()
             for _ in range(reps):
@@ -932,6 +986,7 @@ def main():
             sec[key] = {"samples_per_s": ns / (ms * 1e-3), "ms": ms, "samples": ns,
                         "sample_direction_ms": ms_s, "pdf_direction_ms": ms_p, "w_sky": smp_s.sky_sampling_w,
                         "gfxclk_mhz_during_sample_direction": clk_s,
+                        "effective_mhz_during_sample_direction": cd.mhz(),
                         "achieved_GBps": BYTES_SAMPLE * ns / (ms * 1e-3) / 1e9,
                         "note": "sample_direction (reads u; writes d, pdf, RGB weight) + pdf_direction "
                                 "(reads d; writes pdf); " + ("JIT semantics, w_sky from the quadrature" if sem == "jit"
@@ -940,7 +995,7 @@ def main():
             if sem == "jit" and vs and vp:
                 sec[key]["valu_roofline"] = {
                     "bound": "valu", "unit": "ms",
-                    "sample_direction": valu_frac(vs, ms_s, clk_s),
+                    "sample_direction": valu_frac(vs, ms_s, clk_s, sec[key]["effective_mhz_during_sample_direction"]),
                     "pdf_direction": valu_frac(vp, ms_p),
                     "note": "frac = VALU-issue floor (PMC instruction counts x issue cycles / (1024 SIMDs x 2.4 GHz)) "
                             "/ measured launch time (frac_at_gfxclk: the floor at the sampled clock); HBM frac of the same launches is achieved_GBps / 8000"}
@@ -1010,9 +1065,12 @@ def main():
             spec_sample_step()
             spec_pdf_step()
         t_ss, t_sq = KernelTimer(), KernelTimer()
+        cd = ClockDuring(dev)
         t_ss.begin()
-        for _ in range(reps):
+        for r_ in range(reps):
             spec_sample_step()
+            if r_ == 0:
+                cd.launch(0.4 * reps * 1.2)
         t_ss.end(reps)
         t_sq.begin()
         for _ in range(reps):
@@ -1023,13 +1081,16 @@ def main():
         sec["sampling_C4_spectral_4lambda"] = {
             "samples_per_s": ns / ((ms_ss + ms_sq) * 1e-3), "sample_direction_ms": ms_ss, "pdf_direction_ms": ms_sq,
             "gfxclk_mhz_during_sample_direction": clk_ss,
+            "effective_mhz_during_sample_direction": cd.mhz(),
             "samples": ns, "achieved_GBps": (8 + 16 + 12 + 4 + 16 + 12 + 4) * ns / ((ms_ss + ms_sq) * 1e-3) / 1e9,
             "note": "spectral emitter, C4 sun: sample_direction with 4 per-sample wavelengths (reads u + 4 lambda, "
                     "writes d, pdf, 4 weights; the wave-sorted LEAN kernel) + pdf_direction"}
         vss = valu_floor("sunsky_sample_direction_spec_lean4_sorted_" + kfx)
         if vss:
             sec["sampling_C4_spectral_4lambda"]["valu_roofline"] = {
-                "bound": "valu", "unit": "ms", "sample_direction": valu_frac(vss, ms_ss, clk_ss),
+                "bound": "valu", "unit": "ms",
+                "sample_direction": valu_frac(vss, ms_ss, clk_ss, sec["sampling_C4_spectral_4lambda"][
+                    "effective_mhz_during_sample_direction"]),
                 "note": "frac = VALU-issue floor (PMC instruction counts x issue cycles / (1024 SIMDs x 2.4 GHz)) / "
                         "measured launch time (frac_at_gfxclk: the floor at the sampled clock)"}
         if rank == 0:

@@ -28,3 +28,22 @@ extern "C" __global__ __launch_bounds__(256) void sunsky_tools_clock_probe(unsig
         out[2 * blockIdx.x + 1] = s == 1.2345f ? 1ull : 0ull;
     }
 }
+
+// The shader clock DURING another kernel's burst: one wave on a side stream counts shader-clock
+// cycles (s_memtime) over `ticks` of the constant 100 MHz counter (s_memrealtime), sleeping
+// between reads, then exits (a time-based exit every launch reaches).  Reads counters only;
+// the result leaves through a vector store.  Not part of the product.
+extern "C" __global__ __launch_bounds__(64) void sunsky_tools_clock_during(unsigned long long* out,
+                                                                           unsigned long long ticks) {
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
+    unsigned long long r = r0;
+    while (r - r0 < ticks) {
+        __builtin_amdgcn_s_sleep(8);
+        r = __builtin_amdgcn_s_memrealtime();
+    }
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) {
+        out[0] = c1 - c0;
+        out[1] = r - r0;
+    }
+}

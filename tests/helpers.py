@@ -110,7 +110,7 @@ def parity_stats(gpu, o32, o64, sunlanes):
 SUN_SLACK = {"fast": 1.25, "reference": 4.0}
 
 
-def assert_parity(gpu, o32, o64, sunlanes, rtol=1e-5, precision="fast", sun_k=None):
+def assert_parity(gpu, o32, o64, sunlanes, rtol=1e-5, precision="fast", sun_k=None, sun_rtol=None):
     """gpu/o32/o64: (n, c).  sky lanes: rel to o32; sun lanes: conditioning-aware vs o64,
     |gpu - o64| <= rtol |o64| + k |o32 - o64| per lane with k = 1.25 for the fast kernels
     (their cos psi comes from fp64 chord terms: more accurate than the reference's fp32) and
@@ -118,8 +118,9 @@ def assert_parity(gpu, o32, o64, sunlanes, rtol=1e-5, precision="fast", sun_k=No
     with the GPU's libm (an ulp of sin(gamma) next to the limb moves a lane by ~1e-5); those
     must also be as accurate as the fp32 reference overall (max over the sun lanes within
     1.25 x the fp32 oracle's max).  sun_k overrides k (the aggregate check then applies when
-    k > 1.25).  Returns parity_stats()."""
+    k > 1.25).  sun_rtol overrides rtol on the sun lanes.  Returns parity_stats()."""
     k = SUN_SLACK[precision] if sun_k is None else sun_k
+    sun_rtol = rtol if sun_rtol is None else sun_rtol
     sky = ~sunlanes
     if sky.any():
         g, a, b = gpu[sky].astype(np.float64), o32[sky].astype(np.float64), o64[sky]
@@ -132,7 +133,7 @@ def assert_parity(gpu, o32, o64, sunlanes, rtol=1e-5, precision="fast", sun_k=No
         assert strict.mean() >= 0.9999, f"sky lanes: only {strict.mean():.6f} within plain {rtol:g}"
     if sunlanes.any():
         g, a, b = gpu[sunlanes].astype(np.float64), o32[sunlanes].astype(np.float64), o64[sunlanes]
-        bound = rtol * np.abs(b) + k * np.abs(a - b) + 1e-30
+        bound = sun_rtol * np.abs(b) + k * np.abs(a - b) + 1e-30
         bad = np.abs(g - b) > bound
         assert not bad.any(), f"sun lanes: {bad.sum()} over bound, worst {np.max(np.abs(g - b) / bound):.2f}x"
     st = parity_stats(gpu, o32, o64, sunlanes)
@@ -171,3 +172,15 @@ def disc_lanes(d, info, band=1e-6):
     against the fp32 cos(half aperture); a lane the fp64 test puts just outside may carry
     the sun term, at the limb where the fp32 reference's own cos psi error is largest."""
     return (np.asarray(d, np.float64) @ info["sun_dir_local"]) >= info["cos_cutoff"] - band
+
+
+def fp32_sun_input(d, o32):
+    """The emitter dict with sun_direction replaced by the fp32-normalised direction the
+    reference computes from it (dr::normalize(props.get<ScalarVector3f>("sun_direction")),
+    sunsky.cpp:923) -- the product and the fp32 oracle use those bits -- for the fp64 oracle,
+    so that it evaluates exactly what an fp32 implementation was given.  From the unrounded
+    direction the disc moves by up to ~1e-8 rad, which next to the limb (d cos psi / d gamma
+    unbounded) moves disc lanes by up to 3.6e-4 (measured at 8 deg elevation / 200 deg)."""
+    if "sun_direction" not in d:
+        return d
+    return dict(d, sun_direction=[float(x) for x in o32.info()["sun_dir_world"]])

@@ -75,6 +75,14 @@ std::string code_object_path() {
     return library_dir() + "/sunsky_kernels.hsaco";
 }
 
+// The same kernels compiled with to_world / to_local as the identity (SS_XFORM_IDENTITY),
+// launched for emitters whose to_world is the identity: the same bits without the
+// per-direction identity test.  SUNSKY_AMD_CODE_OBJECT (a probe build) replaces both.
+std::string ident_code_object_path() {
+    if (const char* env = std::getenv("SUNSKY_AMD_CODE_OBJECT")) return env;
+    return library_dir() + "/sunsky_kernels_ident.hsaco";
+}
+
 // ---------------------------------------------------------------- kernels
 // The sampling kernels are instantiated per variant (RGB / spectral) so each
 // carries only its own tables and registers.
@@ -106,9 +114,10 @@ bool has_dir_form(KernelId k) {
 }
 
 struct DeviceModule {
-    hipModule_t module = nullptr;
-    hipFunction_t fn[2][K_COUNT] = {};   // [precision][kernel]
-    hipFunction_t fn_dir[2][K_COUNT] = {};   // eval_direction forms (wo = +d) of the eval kernels
+    hipModule_t module = nullptr, module_ident = nullptr;
+    // [identity to_world][precision][kernel]: [1] from sunsky_kernels_ident.hsaco
+    hipFunction_t fn[2][2][K_COUNT] = {};
+    hipFunction_t fn_dir[2][2][K_COUNT] = {};   // eval_direction forms (wo = +d) of the eval kernels
     hipFunction_t jvp_rgb = nullptr, jvp_spec = nullptr;   // eval_jvp (reference operation order)
     hipFunction_t vjp_rgb = nullptr, vjp_spec = nullptr, grad_reduce = nullptr;   // eval_vjp
     hipFunction_t latlong_tables = nullptr;                                     // bake_latlong
@@ -125,18 +134,23 @@ DeviceModule* module_for_device(int dev) {
     auto it = g_modules.find(dev);
     if (it != g_modules.end()) return it->second;
     std::unique_ptr<DeviceModule> m(new DeviceModule());
-    std::string path = code_object_path();
-    if (!file_exists(path)) throw HipError("kernel code object not found: " + path + " (run the build)");
+    const std::string path = code_object_path(), ipath = ident_code_object_path();
+    for (const std::string& p : {path, ipath})
+        if (!file_exists(p)) throw HipError("kernel code object not found: " + p + " (run the build)");
     hip_check(hipModuleLoad(&m->module, path.c_str()), "hipModuleLoad(sunsky_kernels.hsaco)");
-    for (int p = 0; p < 2; ++p)
-        for (int k = 0; k < K_COUNT; ++k) {
-            std::string name = std::string(kKernelNames[k]) + (p == SUNSKY_PRECISION_FAST ? "_fast" : "_ref");
-            hip_check(hipModuleGetFunction(&m->fn[p][k], m->module, name.c_str()), name.c_str());
-            if (has_dir_form((KernelId)k)) {
-                std::string dn = std::string(kKernelNames[k]) + (p == SUNSKY_PRECISION_FAST ? "_dir_fast" : "_dir_ref");
-                hip_check(hipModuleGetFunction(&m->fn_dir[p][k], m->module, dn.c_str()), dn.c_str());
+    if (ipath == path) m->module_ident = m->module;
+    else hip_check(hipModuleLoad(&m->module_ident, ipath.c_str()), "hipModuleLoad(sunsky_kernels_ident.hsaco)");
+    for (int id = 0; id < 2; ++id)
+        for (int p = 0; p < 2; ++p)
+            for (int k = 0; k < K_COUNT; ++k) {
+                hipModule_t mod = id ? m->module_ident : m->module;
+                std::string name = std::string(kKernelNames[k]) + (p == SUNSKY_PRECISION_FAST ? "_fast" : "_ref");
+                hip_check(hipModuleGetFunction(&m->fn[id][p][k], mod, name.c_str()), name.c_str());
+                if (has_dir_form((KernelId)k)) {
+                    std::string dn = std::string(kKernelNames[k]) + (p == SUNSKY_PRECISION_FAST ? "_dir_fast" : "_dir_ref");
+                    hip_check(hipModuleGetFunction(&m->fn_dir[id][p][k], mod, dn.c_str()), dn.c_str());
+                }
             }
-        }
     hip_check(hipModuleGetFunction(&m->jvp_rgb, m->module, "sunsky_eval_jvp_rgb"), "sunsky_eval_jvp_rgb");
     hip_check(hipModuleGetFunction(&m->jvp_spec, m->module, "sunsky_eval_jvp_spec"), "sunsky_eval_jvp_spec");
     hip_check(hipModuleGetFunction(&m->vjp_rgb, m->module, "sunsky_eval_vjp_rgb"), "sunsky_eval_vjp_rgb");
@@ -483,14 +497,20 @@ struct sunsky_emitter {
         self->kargs.spec_inv_interval = hk.spec_inv_interval;
     }
 
+    // the identity-to_world code object for emitters whose to_world is the identity
+    // (SUNSKY_AMD_GENERAL_XFORM=1: the general one always; the bitwise test of the two)
+    int xform_form() const {
+        const char* g = std::getenv("SUNSKY_AMD_GENERAL_XFORM");
+        return kargs.identity_xform && !(g && g[0] == '1') ? 1 : 0;
+    }
     hipFunction_t fn(KernelId k) const {
         if (!mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
-        return mod->fn[precision][k];
+        return mod->fn[xform_form()][precision][k];
     }
     // eval (sign < 0: wo = -wi) or eval_direction (sign > 0: wo = d) form of an eval kernel
     hipFunction_t fn_eval(KernelId k, float sign) const {
         if (!mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
-        return sign < 0.f ? mod->fn[precision][k] : mod->fn_dir[precision][k];
+        return sign < 0.f ? mod->fn[xform_form()][precision][k] : mod->fn_dir[xform_form()][precision][k];
     }
 
     ~sunsky_emitter() {

@@ -11,6 +11,7 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BUILD_DIR = os.path.join(PKG_ROOT, "build")
 LIB_PATH = os.path.join(BUILD_DIR, "libsunsky_amd.so")
 CODE_OBJECT = os.path.join(BUILD_DIR, "sunsky_kernels.hsaco")
+CODE_OBJECT_IDENT = os.path.join(BUILD_DIR, "sunsky_kernels_ident.hsaco")   # identity to_world
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "sunsky_amd.h")
 
 OK = 0

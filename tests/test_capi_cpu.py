@@ -22,6 +22,7 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     assert ss.lib().sunsky_abi_version() == 6
     assert os.path.exists(ss.CODE_OBJECT), "gfx950 code object not built"
+    assert os.path.exists(ss.CODE_OBJECT_IDENT), "identity-to_world gfx950 code object not built"
 
 
 def test_default_dataset_path_resolves_to_bundled_pack():

@@ -10,7 +10,7 @@ R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 export SUNSKY_AMD_DATASET=$R/mitsuba3-sunsky_amd/data/sunsky_datasets.pack
 O=$R/gpurun_out/ab.log
-THIS=${THIS:-$R/mitsuba3-sunsky_amd/build/sunsky_kernels.hsaco}
+THIS=${THIS:-$R/mitsuba3-sunsky_amd/build/sunsky_kernels_ident.hsaco}   # kbench emitters have an identity to_world
 OTHER=${OTHER:-$R/tools/build/ab_base.hsaco}
 MODE=$1; N=$2; shift 2
 echo "== $THIS vs $OTHER ($MODE $N: $*)" >> $O

@@ -8,7 +8,7 @@ mkdir -p $R/gpurun_out/valu
 cd /tmp
 export TMPDIR=/tmp
 export SUNSKY_AMD_DATASET=$R/mitsuba3-sunsky_amd/data/sunsky_datasets.pack
-H=$R/mitsuba3-sunsky_amd/build/sunsky_kernels.hsaco
+H=$R/mitsuba3-sunsky_amd/build/sunsky_kernels_ident.hsaco   # what the product launches for kbench's identity to_world
 KB=$R/tools/build/kbench
 C="SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE"
 # second pass per kernel: where the wave cycles go (8 SQ counters)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # VALU-roofline counters (one rocprofv3 --pmc pass per kernel; 8 SQ + 1 GRBM counters):
 # VALU / transcendental wave-instructions, VALU-active and wave cycles, waves, GPU-active cycles.
-# Summary: tools/valu_summary.py gpurun_out/valu/*/*counter_collection.csv
+# Summary: python tools/valu_summary.py gpurun_out/valu > profiles/rNN_vM_valu_roofline.json
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/valu

@@ -456,7 +456,7 @@ def parity_rays(em, d_scene, wi, lam, out, n_check=1 << 19, n_sun=1 << 13):
     got = np.concatenate([out[:, :n_check].T.cpu().numpy(), g_cone.T.cpu().numpy()])
     sun = (-wi_all @ inf["sun_dir_local"] >= inf["cos_cutoff"]) & (wi_all[:, 2] <= 0)
     st = lane_stats(got, o32.eval(wi_all, lam_all).T, o64.eval(wi_all, lam_all).T, sun)
-    return dict(st, checked_rays=wi_all.shape[0], kernel="sunsky_eval_spec_rays_v4")
+    return dict(st, checked_rays=wi_all.shape[0], kernel="sunsky_eval_spec_rays4_v4")
 
 
 def parity_c4(em, d_scene, u, d, pdf_s, wgt, pdf_q, n_check=1 << 19, semantics="jit", lam=None):
@@ -924,7 +924,7 @@ def main():
                                                 "hbm_frac": (12 + 16 + 16) * n / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                                 "note": "16M rays x 4 random wavelengths in [360, 720] nm "
                                                         "(reads wi + lambda, writes 4 radiances)"}
-        vr = valu_floor("sunsky_eval_spec_rays_v4_" + ("ref" if args.precision == "reference" else "fast"))
+        vr = valu_floor("sunsky_eval_spec_rays4_v4_" + ("ref" if args.precision == "reference" else "fast"))
         if vr:
             sec["spectral_eval_per_ray_4lambda"]["valu_roofline"] = {
                 "bound": "valu", "unit": "ms", "eval": valu_frac(vr, ms),

@@ -93,7 +93,7 @@ enum KernelId {
     K_DIRECT_DIFFUSE_RGB, K_DIRECT_DIFFUSE_SPEC, K_SAMPLE_DIRECTION_RGB_LEAN, K_SAMPLE_DIRECTION_SPEC_LEAN,
     K_DIRECT_DIFFUSE_RAYS, K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN, K_DIRECT_CONDUCTOR_RGB, K_DIRECT_CONDUCTOR_SPEC,
     K_DIRECT_CONDUCTOR_RAYS, K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED, K_SAMPLE_RAY_RGB_SORTED,
-    K_SAMPLE_DIRECTION_RGB_FULL_SORTED, K_COUNT
+    K_SAMPLE_DIRECTION_RGB_FULL_SORTED, K_EVAL_SPEC_RAYS4_V4, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
@@ -105,12 +105,13 @@ const char* kKernelNames[K_COUNT] = {
     "sunsky_sample_direction_rgb_lean", "sunsky_sample_direction_spec_lean", "sunsky_direct_diffuse_rays",
     "sunsky_sample_direction_rgb_lean_plain", "sunsky_direct_conductor_rgb", "sunsky_direct_conductor_spec",
     "sunsky_direct_conductor_rays", "sunsky_sample_direction_spec_lean4_sorted", "sunsky_sample_ray_rgb_sorted",
-    "sunsky_sample_direction_rgb_full_sorted"};
+    "sunsky_sample_direction_rgb_full_sorted", "sunsky_eval_spec_rays4_v4"};
 
 // eval kernels instantiated twice: eval(si) negates wi at compile time,
 // eval_direction(ds) uses ds.d as is (the "_dir" kernels)
 bool has_dir_form(KernelId k) {
-    return k == K_EVAL_RGB_V4 || k == K_EVAL_RGB_V1 || k == K_EVAL_SPEC_RAYS_V4 || k == K_EVAL_SPEC_RAYS_V1;
+    return k == K_EVAL_RGB_V4 || k == K_EVAL_RGB_V1 || k == K_EVAL_SPEC_RAYS_V4 || k == K_EVAL_SPEC_RAYS_V1 ||
+           k == K_EVAL_SPEC_RAYS4_V4;
 }
 
 struct DeviceModule {
@@ -193,7 +194,7 @@ int blocks_per_cu(KernelId k) {
         case K_BAKE_RGB: case K_BAKE_SPEC: return 64;
         case K_DIRECT_DIFFUSE_RGB: case K_DIRECT_DIFFUSE_SPEC: case K_DIRECT_DIFFUSE_RAYS: return 64;
         case K_DIRECT_CONDUCTOR_RGB: case K_DIRECT_CONDUCTOR_SPEC: case K_DIRECT_CONDUCTOR_RAYS: return 64;
-        case K_EVAL_SPEC_RAYS_V4: case K_EVAL_SPEC_RAYS_V1: return 64;
+        case K_EVAL_SPEC_RAYS_V4: case K_EVAL_SPEC_RAYS_V1: case K_EVAL_SPEC_RAYS4_V4: return 64;
         // kbench sweep over 8/16/32/64 (profiles/r03_v18_kbench_grid_ray_wavelengths.log)
         case K_SAMPLE_RAY_RGB: case K_SAMPLE_RAY_SPEC: return 32;
         case K_SAMPLE_WAVELENGTHS_SPEC: return 64;
@@ -848,7 +849,9 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
             if (n4) {
                 const float *x = w.x, *y = w.y, *z = w.z;
                 void* args[] = {&K, &x, &y, &z, &lam, &lstride, &nl, &active, &n4, &out, &ostride, &sign};
-                launch(e->fn_eval(K_EVAL_SPEC_RAYS_V4, sign), grid_for(e->mod, K_EVAL_SPEC_RAYS_V4, n4 / 4), s, args);
+                // Mitsuba's Spectrum<Float, 4>: the kernel with the count compiled in
+                const KernelId kr = nlam == 4 ? K_EVAL_SPEC_RAYS4_V4 : K_EVAL_SPEC_RAYS_V4;
+                launch(e->fn_eval(kr, sign), grid_for(e->mod, kr, n4 / 4), s, args);
             }
             if (n4 < n) {
                 const float *x = w.x + n4, *y = w.y + n4, *z = w.z + n4, *l = lam + n4;

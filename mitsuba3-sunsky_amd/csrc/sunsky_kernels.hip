@@ -986,7 +986,7 @@ __device__ __forceinline__ void eval_spec_rays_pf_body(const SunskyKArgs& K, con
     }
 }
 
-template <int VEC, bool FAST, bool NEG>
+template <int VEC, bool FAST, bool NEG, int NL = 0>
 __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                                     const float* __restrict__ wy, const float* __restrict__ wz,
                                                     const float* __restrict__ lam, size_t lstride, int nlam,
@@ -995,6 +995,10 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
     __shared__ ChanLds<FAST> S;
     const auto* chans = stage_chans<FAST>(K, &S);
     __syncthreads();
+    // NL > 0: the wavelength count as a compile-time constant (the rays4 kernels, Mitsuba's
+    // Spectrum<Float, 4>): the chunk loop and its bounds fold away (4.4 % faster,
+    // profiles/r04_v15_ab_rays_nl4.log)
+    if constexpr (NL > 0) nlam = NL;
     const size_t nvec = n / VEC;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
@@ -3558,21 +3562,26 @@ SS_EVAL_SPEC_BCAST(sunsky_eval_spec_bcast_v1_ref, 1, false)
 SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v4_fast, 4, true)
 SS_EVAL_SPEC_NODES(sunsky_eval_spec_nodes_v4_ref, 4, false)
 
-#define SS_EVAL_SPEC_RAYS(NAME, VEC, FAST, NEG)                                                                    \
+#define SS_EVAL_SPEC_RAYS(NAME, VEC, FAST, NEG, NL)                                                                \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_RAYS_ATTR void NAME(                                               \
         const SunskyKArgs* __restrict__ Kp, const float* wx, const float* wy, const float* wz, const float* lam, size_t lstride,    \
         int nlam, const uint8_t* active, size_t n, float* out, size_t ostride, float sign) {                   \
         (void)sign;                                                                                            \
-        eval_spec_rays_body<VEC, FAST, NEG>(*Kp, wx, wy, wz, lam, lstride, nlam, active, n, out, ostride);       \
+        eval_spec_rays_body<VEC, FAST, NEG, NL>(*Kp, wx, wy, wz, lam, lstride, nlam, active, n, out, ostride);   \
     }
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_fast, 4, true, true)
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_fast, 1, true, true)
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_ref, 4, false, true)
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_ref, 1, false, true)
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_dir_fast, 4, true, false)
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_dir_fast, 1, true, false)
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_dir_ref, 4, false, false)
-SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_dir_ref, 1, false, false)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_fast, 4, true, true, 0)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_fast, 1, true, true, 0)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_ref, 4, false, true, 0)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_ref, 1, false, true, 0)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_dir_fast, 4, true, false, 0)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_dir_fast, 1, true, false, 0)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v4_dir_ref, 4, false, false, 0)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays_v1_dir_ref, 1, false, false, 0)
+// exactly 4 wavelengths per ray (Mitsuba's Spectrum<Float, 4>), VEC = 4 over rays
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays4_v4_fast, 4, true, true, 4)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays4_v4_ref, 4, false, true, 4)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays4_v4_dir_fast, 4, true, false, 4)
+SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays4_v4_dir_ref, 4, false, false, 4)
 #ifdef SS_PROBE_RAYS_PF   // probe builds only: the software-pipelined per-ray eval at 4 wavelengths
 #define SS_EVAL_SPEC_RAYS_PF(NAME, VEC)                                                                        \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \

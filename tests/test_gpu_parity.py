@@ -138,6 +138,32 @@ def test_eval_spectral_parity(turb, precision):
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("nlam", [1, 3, 4, 5, 8])
+def test_eval_per_ray_wavelength_counts(nlam, precision):
+    """Per-ray wavelengths at counts other than Mitsuba's 4 go through the general rays kernel
+    (chunks of 4 planes), exactly 4 through the rays4 kernel with the count compiled in: each
+    against the oracle, and the rays4 kernel bitwise the general one (the first 4 planes of an
+    8-wavelength call hold the same wavelengths)."""
+    d = angles_dict(3.0, 0.9, np.deg2rad(50), 0.3, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, "spectral", precision=precision)
+    o32, o64 = O.Oracle(d, "spectral", "jit", "f32"), O.Oracle(d, "spectral", "jit", "f64")
+    inf = o32.info()
+    wo = np.concatenate([hemisphere_wo((1 << 14) + 3, seed=17),
+                         sun_cone_wo(1024, inf["sun_dir_local"], np.arccos(inf["cos_cutoff"]), seed=18, scale=1.2)])
+    n, wi = wo.shape[0], -wo
+    rng = np.random.default_rng(19)
+    lam = rng.uniform(300, 800, (8, n)).astype(np.float32)
+    lam[:, :7] = np.array([320.0, 360.0, 720.0, 719.99, 320.01, 555.0, 300.0], np.float32)   # nodes, edges, outside
+    lt = torch.from_numpy(lam).cuda()
+    pr = host(em.eval(ss.SurfaceInteraction3f(wi=soa(wi), wavelengths=lt[:nlam].contiguous())))
+    a, b = o32.eval(wi, lam[:nlam]), o64.eval(wi, lam[:nlam])
+    assert_parity(pr.T, a.T, b.T, sun_mask(o32, wo), precision=precision)
+    if nlam == 8:
+        p4 = host(em.eval(ss.SurfaceInteraction3f(wi=soa(wi), wavelengths=lt[:4].contiguous())))
+        assert np.array_equal(p4.view(np.int32), pr[:4].view(np.int32))
+
+
+@pytest.mark.parametrize("precision", PRECISIONS)
 def test04_sun_radiance_spd(golden_dir, precision):
     sp = np.load(os.path.join(golden_dir, "sun_spectra.npz"))
     phi = np.pi / 5

@@ -22,5 +22,5 @@ run sample_plain sample 67108864 sunsky_sample_direction_rgb_lean_plain_fast && 
 run pdf pdf 67108864 sunsky_pdf_direction_v4_fast && \
 run rgb rgb 16777216 sunsky_eval_rgb_v4_fast && \
 run spec spec 16777216 sunsky_eval_spec_nodes_v4_fast && \
-run rays rays 16777216 sunsky_eval_spec_rays_v4_fast && \
+run rays rays 16777216 sunsky_eval_spec_rays4_v4_fast && \
 KB_SAMPLE_SPEC=1 run sample_spec sample 67108864 sunsky_sample_direction_spec_lean4_sorted_fast

@@ -500,18 +500,25 @@ struct sunsky_emitter {
 
     // the identity-to_world code object for emitters whose to_world is the identity
     // (SUNSKY_AMD_GENERAL_XFORM=1: the general one always; the bitwise test of the two)
-    int xform_form() const {
+    // A launch being captured into a hipGraph takes the general code object: the graph may be
+    // replayed after an update that gives the emitter a non-identity to_world (captured
+    // launches read the current state), which the identity kernels would not apply.
+    int xform_form(hipStream_t s) const {
         const char* g = std::getenv("SUNSKY_AMD_GENERAL_XFORM");
-        return kargs.identity_xform && !(g && g[0] == '1') ? 1 : 0;
+        if (!kargs.identity_xform || (g && g[0] == '1')) return 0;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        hip_check(hipStreamIsCapturing(s, &cs), "hipStreamIsCapturing");
+        return cs == hipStreamCaptureStatusNone ? 1 : 0;
     }
-    hipFunction_t fn(KernelId k) const {
+    hipFunction_t fn(KernelId k, hipStream_t s) const {
         if (!mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
-        return mod->fn[xform_form()][precision][k];
+        return mod->fn[xform_form(s)][precision][k];
     }
     // eval (sign < 0: wo = -wi) or eval_direction (sign > 0: wo = d) form of an eval kernel
-    hipFunction_t fn_eval(KernelId k, float sign) const {
+    hipFunction_t fn_eval(KernelId k, float sign, hipStream_t s) const {
         if (!mod) throw std::invalid_argument("host-only emitter (sunsky_emitter_create_host) cannot launch kernels");
-        return sign < 0.f ? mod->fn[xform_form()][precision][k] : mod->fn_dir[xform_form()][precision][k];
+        const int x = xform_form(s);
+        return sign < 0.f ? mod->fn[x][precision][k] : mod->fn_dir[x][precision][k];
     }
 
     ~sunsky_emitter() {
@@ -829,7 +836,7 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
             if (n4) {
                 const float *x = w.x, *y = w.y, *z = w.z;
                 void* args[] = {&K, &x, &y, &z, &active, &n4, &out, &ostride, &sign};
-                launch(e->fn_eval(K_EVAL_RGB_V4, sign), grid_for(e->mod, K_EVAL_RGB_V4, n4 / 4), s, args);
+                launch(e->fn_eval(K_EVAL_RGB_V4, sign, s), grid_for(e->mod, K_EVAL_RGB_V4, n4 / 4), s, args);
             }
             if (n4 < n) {
                 const float *x = w.x + n4, *y = w.y + n4, *z = w.z + n4;
@@ -837,7 +844,7 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
                 float* o = out + n4;
                 size_t rem = n - n4;
                 void* args[] = {&K, &x, &y, &z, &a, &rem, &o, &ostride, &sign};
-                launch(e->fn_eval(K_EVAL_RGB_V1, sign), grid_for(e->mod, K_EVAL_RGB_V1, rem), s, args);
+                launch(e->fn_eval(K_EVAL_RGB_V1, sign, s), grid_for(e->mod, K_EVAL_RGB_V1, rem), s, args);
             }
         } else {
             // VEC = 4 over rays when every plane is 16-byte aligned; VEC = 1 tail
@@ -851,7 +858,7 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
                 void* args[] = {&K, &x, &y, &z, &lam, &lstride, &nl, &active, &n4, &out, &ostride, &sign};
                 // Mitsuba's Spectrum<Float, 4>: the kernel with the count compiled in
                 const KernelId kr = nlam == 4 ? K_EVAL_SPEC_RAYS4_V4 : K_EVAL_SPEC_RAYS_V4;
-                launch(e->fn_eval(kr, sign), grid_for(e->mod, kr, n4 / 4), s, args);
+                launch(e->fn_eval(kr, sign, s), grid_for(e->mod, kr, n4 / 4), s, args);
             }
             if (n4 < n) {
                 const float *x = w.x + n4, *y = w.y + n4, *z = w.z + n4, *l = lam + n4;
@@ -859,7 +866,7 @@ static int eval_impl(const sunsky_emitter* e, sunsky_vec3_in w, const float* lam
                 float* o = out + n4;
                 size_t rem = n - n4;
                 void* args[] = {&K, &x, &y, &z, &l, &lstride, &nl, &a, &rem, &o, &ostride, &sign};
-                launch(e->fn_eval(K_EVAL_SPEC_RAYS_V1, sign), grid_for(e->mod, K_EVAL_SPEC_RAYS_V1, rem), s, args);
+                launch(e->fn_eval(K_EVAL_SPEC_RAYS_V1, sign, s), grid_for(e->mod, K_EVAL_SPEC_RAYS_V1, rem), s, args);
             }
         }
     });
@@ -903,7 +910,7 @@ int sunsky_eval_spectral_broadcast(const sunsky_emitter* e, sunsky_vec3_in w, co
         if (n4) {
             const float *x = w.x, *y = w.y, *z = w.z;
             void* args[] = {&K, &L, &x, &y, &z, &active, &n4, &out, &ostride, &sign};
-            launch(e->fn(nodes ? K_EVAL_SPEC_NODES_V4 : K_EVAL_SPEC_BCAST_V4), grid_for(e->mod, K_EVAL_SPEC_BCAST_V4, n4 / 4), s, args);
+            launch(e->fn(nodes ? K_EVAL_SPEC_NODES_V4 : K_EVAL_SPEC_BCAST_V4, s), grid_for(e->mod, K_EVAL_SPEC_BCAST_V4, n4 / 4), s, args);
         }
         if (n4 < n) {
             const float *x = w.x + n4, *y = w.y + n4, *z = w.z + n4;
@@ -911,7 +918,7 @@ int sunsky_eval_spectral_broadcast(const sunsky_emitter* e, sunsky_vec3_in w, co
             float* o = out + n4;
             size_t rem = n - n4;
             void* args[] = {&K, &L, &x, &y, &z, &a, &rem, &o, &ostride, &sign};
-            launch(e->fn(K_EVAL_SPEC_BCAST_V1), grid_for(e->mod, K_EVAL_SPEC_BCAST_V1, rem), s, args);
+            launch(e->fn(K_EVAL_SPEC_BCAST_V1, s), grid_for(e->mod, K_EVAL_SPEC_BCAST_V1, rem), s, args);
         }
     });
 }
@@ -960,7 +967,7 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
         // the wave-sorted kernels: one wave takes a window of 4 (RGB) or 3 (spectral) x 64 samples
         const size_t items = (k == K_SAMPLE_DIRECTION_RGB_LEAN || k == K_SAMPLE_DIRECTION_RGB_FULL_SORTED) ? (n + 3) / 4
                              : k == K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED ? (n + 2) / 3 : n;
-        launch(e->fn(k), grid_for(e->mod, k, items), (hipStream_t)stream, args);
+        launch(e->fn(k, (hipStream_t)stream), grid_for(e->mod, k, items), (hipStream_t)stream, args);
     });
 }
 
@@ -980,7 +987,7 @@ int sunsky_pdf_direction(const sunsky_emitter* e, sunsky_vec3_in d, const uint8_
         size_t n4 = vec ? (n & ~(size_t)3) : 0;
         if (n4) {
             void* args[] = {&K, (void*)&d.x, (void*)&d.y, (void*)&d.z, &active, &n4, &pdf};
-            launch(e->fn(K_PDF_DIRECTION_V4), grid_for(e->mod, K_PDF_DIRECTION_V4, n4 / 4), s, args);
+            launch(e->fn(K_PDF_DIRECTION_V4, s), grid_for(e->mod, K_PDF_DIRECTION_V4, n4 / 4), s, args);
         }
         if (n4 < n) {
             const float *x = d.x + n4, *y = d.y + n4, *z = d.z + n4;
@@ -988,7 +995,7 @@ int sunsky_pdf_direction(const sunsky_emitter* e, sunsky_vec3_in d, const uint8_
             float* p = pdf + n4;
             size_t rem = n - n4;
             void* args[] = {&K, &x, &y, &z, &a, &rem, &p};
-            launch(e->fn(K_PDF_DIRECTION_V1), grid_for(e->mod, K_PDF_DIRECTION_V1, rem), s, args);
+            launch(e->fn(K_PDF_DIRECTION_V1, s), grid_for(e->mod, K_PDF_DIRECTION_V1, rem), s, args);
         }
     });
 }
@@ -1015,7 +1022,7 @@ int sunsky_sample_ray(const sunsky_emitter* e, const float* wls, const float* s2
         const bool unsorted = uns && uns[0] == '1';
         const KernelId k = e->kargs.variant == kSpectral ? K_SAMPLE_RAY_SPEC
                            : (!active && !unsorted) ? K_SAMPLE_RAY_RGB_SORTED : K_SAMPLE_RAY_RGB;
-        launch(e->fn(k), grid_for(e->mod, k, k == K_SAMPLE_RAY_RGB_SORTED ? (n + 3) / 4 : n), (hipStream_t)stream,
+        launch(e->fn(k, (hipStream_t)stream), grid_for(e->mod, k, k == K_SAMPLE_RAY_RGB_SORTED ? (n + 3) / 4 : n), (hipStream_t)stream,
                args);
     });
 }
@@ -1034,7 +1041,7 @@ int sunsky_sample_wavelengths(const sunsky_emitter* e, sunsky_vec3_in w, const f
         const SunskyKArgs* K = e->d_state;
         void* args[] = {&K, (void*)&w.x, (void*)&w.y, (void*)&w.z, &sample, &active, &n, &lam, &lstride, &weight, &wstride};
         const KernelId k = e->kargs.variant == kSpectral ? K_SAMPLE_WAVELENGTHS_SPEC : K_SAMPLE_WAVELENGTHS_RGB;
-        launch(e->fn(k), grid_for(e->mod, k, n), (hipStream_t)stream, args);
+        launch(e->fn(k, (hipStream_t)stream), grid_for(e->mod, k, n), (hipStream_t)stream, args);
     });
 }
 
@@ -1243,11 +1250,11 @@ int sunsky_bake_latlong(const sunsky_emitter* e, int width, int height, float th
         }
         if (!spec) {
             void* args[] = {&K, &G, &out, &ostride};
-            launch(e->fn(K_BAKE_RGB), grid_for(e->mod, K_BAKE_RGB, (size_t)((width + 3) / 4) * height), s, args);
+            launch(e->fn(K_BAKE_RGB, s), grid_for(e->mod, K_BAKE_RGB, (size_t)((width + 3) / 4) * height), s, args);
         } else {
             LambdaSet L = make_lambda_set(lam_host, m);
             void* args[] = {&K, &G, &L, &out, &ostride};
-            launch(e->fn(K_BAKE_SPEC), grid_for(e->mod, K_BAKE_SPEC, n), s, args);
+            launch(e->fn(K_BAKE_SPEC, s), grid_for(e->mod, K_BAKE_SPEC, n), s, args);
         }
         hip_check(hipEventRecord(e->bake_done, s), "hipEventRecord");
     });
@@ -1276,7 +1283,7 @@ int sunsky_direct_diffuse(const sunsky_emitter* e, sunsky_vec3_in nrm, const flo
         void* args[] = {&K, (void*)&nrm.x, (void*)&nrm.y, (void*)&nrm.z, &rho, &lam, &lstride, &nl, &seed, &spp, &vis,
                         &vstride, &n, &out, &ostride};
         const KernelId k = spec ? K_DIRECT_DIFFUSE_SPEC : K_DIRECT_DIFFUSE_RGB;
-        launch(e->fn(k), grid_for(e->mod, k, n), (hipStream_t)stream, args);
+        launch(e->fn(k, (hipStream_t)stream), grid_for(e->mod, k, n), (hipStream_t)stream, args);
     });
 }
 
@@ -1296,7 +1303,7 @@ int sunsky_direct_diffuse_rays(const sunsky_emitter* e, sunsky_vec3_in nrm, uint
         const SunskyKArgs* K = e->d_state;
         void* args[] = {&K, (void*)&nrm.x, (void*)&nrm.y, (void*)&nrm.z, &seed, &spp, &n, &em.x, &em.y, &em.z,
                         &bs.x, &bs.y, &bs.z, &rstride};
-        launch(e->fn(K_DIRECT_DIFFUSE_RAYS), grid_for(e->mod, K_DIRECT_DIFFUSE_RAYS, n), (hipStream_t)stream, args);
+        launch(e->fn(K_DIRECT_DIFFUSE_RAYS, (hipStream_t)stream), grid_for(e->mod, K_DIRECT_DIFFUSE_RAYS, n), (hipStream_t)stream, args);
     });
 }
 
@@ -1355,7 +1362,7 @@ static int direct_conductor_impl(const sunsky_emitter* e, sunsky_vec3_in nrm, su
         void* args[] = {&K, &C, (void*)&nrm.x, (void*)&nrm.y, (void*)&nrm.z, (void*)&wi.x, (void*)&wi.y, (void*)&wi.z,
                         &lam, &lstride, &nl, &seed, &spp, &vis, &vstride, &n, &out, &ostride};
         const KernelId kid = spec ? K_DIRECT_CONDUCTOR_SPEC : K_DIRECT_CONDUCTOR_RGB;
-        launch(e->fn(kid), grid_for(e->mod, kid, n), (hipStream_t)stream, args);
+        launch(e->fn(kid, (hipStream_t)stream), grid_for(e->mod, kid, n), (hipStream_t)stream, args);
     });
 }
 
@@ -1385,7 +1392,7 @@ static int direct_conductor_rays_impl(const sunsky_emitter* e, sunsky_vec3_in nr
         const SunskyKArgs* K = e->d_state;
         void* args[] = {&K, &C, (void*)&nrm.x, (void*)&nrm.y, (void*)&nrm.z, (void*)&wi.x, (void*)&wi.y, (void*)&wi.z,
                         &seed, &spp, &n, &em.x, &em.y, &em.z, &bs.x, &bs.y, &bs.z, &rstride, &bw, &nw};
-        launch(e->fn(K_DIRECT_CONDUCTOR_RAYS), grid_for(e->mod, K_DIRECT_CONDUCTOR_RAYS, n), (hipStream_t)stream, args);
+        launch(e->fn(K_DIRECT_CONDUCTOR_RAYS, (hipStream_t)stream), grid_for(e->mod, K_DIRECT_CONDUCTOR_RAYS, n), (hipStream_t)stream, args);
     });
 }
 

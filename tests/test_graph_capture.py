@@ -96,6 +96,52 @@ def test_replay_reads_the_updated_emitter_state():
     assert not torch.equal(captured, before)
 
 
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+def test_replay_after_a_to_world_update(variant):
+    """An emitter with the identity to_world launches the identity code object eagerly
+    (DESIGN.md §3), but a captured launch takes the general one: a graph captured before an
+    update to a rotated to_world replays with the rotation, equal to an eager call after the
+    update (which takes the general code object), and eager calls before the update equal
+    the captured replay before it."""
+    em = ss.SunskyEmitter(angles_dict(3.0, 0.3, np.deg2rad(50), 0.3, 1.0, 1.0), variant)
+    n = 1 << 14
+    wi, u = _inputs(n, 5)
+    lam = torch.full((4, n), 500.0, device="cuda") + torch.arange(4, device="cuda").view(4, 1) * 41.0
+    spec = variant == "spectral"
+
+    def step():
+        e = em.eval(ss.SurfaceInteraction3f(wi=wi, wavelengths=lam if spec else None))
+        ds, w = em.sample_direction(ss.Interaction3f(wavelengths=lam if spec else None), u, positions=False)
+        p = em.pdf_direction(ss.Interaction3f(), ds)
+        return e, ds.d, ds.pdf, w, p
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        step()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        captured = step()
+    g.replay()
+    torch.cuda.synchronize()
+    eager = step()
+    torch.cuda.synchronize()
+    for a, b in zip(captured, eager):
+        assert torch.equal(a, b)
+    c, s_ = np.cos(0.5), np.sin(0.5)
+    params = em.traverse()
+    params["to_world"] = np.array([[c, 0, s_, 0], [0, 1, 0, 0], [-s_, 0, c, 0], [0, 0, 0, 1]], np.float32)
+    params.update()
+    g.replay()
+    torch.cuda.synchronize()
+    eager = step()
+    torch.cuda.synchronize()
+    for a, b in zip(captured, eager):
+        assert torch.equal(a, b)
+    assert not torch.equal(captured[0], eager[0].new_zeros(eager[0].shape))
+
+
 def test_direct_diffuse_with_visibility_replays_bitwise():
     """The occluded caller pair (rays, then shading with the tracer's verdicts) captures too."""
     em = ss.SunskyEmitter(angles_dict(3.0, 0.3, np.deg2rad(50), 0.3, 1.0, 1.0), "rgb")

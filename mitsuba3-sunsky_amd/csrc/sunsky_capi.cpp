@@ -77,10 +77,24 @@ std::string code_object_path() {
 
 // The same kernels compiled with to_world / to_local as the identity (SS_XFORM_IDENTITY),
 // launched for emitters whose to_world is the identity: the same bits without the
-// per-direction identity test.  SUNSKY_AMD_CODE_OBJECT (a probe build) replaces both.
+// per-direction identity test.  SUNSKY_AMD_CODE_OBJECT_IDENT (a probe build) replaces it.
 std::string ident_code_object_path() {
-    if (const char* env = std::getenv("SUNSKY_AMD_CODE_OBJECT")) return env;
+    if (const char* env = std::getenv("SUNSKY_AMD_CODE_OBJECT_IDENT")) return env;
     return library_dir() + "/sunsky_kernels_ident.hsaco";
+}
+
+// An SS_XFORM_IDENTITY build exports sunsky_xform_identity_marker.  Such an object as the
+// general module would drop every rotated to_world without an error, and a general build
+// as the identity module would only be slower: both are refused at load.
+void check_xform_form(hipModule_t mod, const std::string& path, bool want_identity) {
+    hipFunction_t f = nullptr;
+    const bool is_identity = hipModuleGetFunction(&f, mod, "sunsky_xform_identity_marker") == hipSuccess;
+    (void)hipGetLastError();
+    if (is_identity != want_identity)
+        throw HipError("code object " + path + (is_identity
+            ? " is an identity-to_world build (SS_XFORM_IDENTITY); it cannot serve emitters with a rotated to_world "
+              "(SUNSKY_AMD_CODE_OBJECT takes a general build, SUNSKY_AMD_CODE_OBJECT_IDENT an identity build)"
+            : " is not an identity-to_world build (SUNSKY_AMD_CODE_OBJECT_IDENT takes an SS_XFORM_IDENTITY build)"));
 }
 
 // ---------------------------------------------------------------- kernels
@@ -139,8 +153,9 @@ DeviceModule* module_for_device(int dev) {
     for (const std::string& p : {path, ipath})
         if (!file_exists(p)) throw HipError("kernel code object not found: " + p + " (run the build)");
     hip_check(hipModuleLoad(&m->module, path.c_str()), "hipModuleLoad(sunsky_kernels.hsaco)");
-    if (ipath == path) m->module_ident = m->module;
-    else hip_check(hipModuleLoad(&m->module_ident, ipath.c_str()), "hipModuleLoad(sunsky_kernels_ident.hsaco)");
+    check_xform_form(m->module, path, false);
+    hip_check(hipModuleLoad(&m->module_ident, ipath.c_str()), "hipModuleLoad(sunsky_kernels_ident.hsaco)");
+    check_xform_form(m->module_ident, ipath, true);
     for (int id = 0; id < 2; ++id)
         for (int p = 0; p < 2; ++p)
             for (int k = 0; k < K_COUNT; ++k) {

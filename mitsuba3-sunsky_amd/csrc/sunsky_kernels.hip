@@ -331,11 +331,7 @@ __device__ __forceinline__ void add_sun_terms(const SunskyKArgs& K, DirTerms& t)
         if constexpr (FAST) {
             float elevation = elevation_fast(t.cos_theta);
             int pos;
-#ifndef SS_PROBE_CBRT_SEGMENT   // probe build (A/B of the cbrt search): never in the product
             if (K.sun_seg_nb >= 0) {
-#else
-            if (false) {
-#endif
                 // the segment starts the disc straddles (host, SunskyKArgs::sun_seg_bound):
                 // one compare per start instead of cbrt (v_log, v_exp, v_rcp, Newton step)
                 pos = K.sun_row_lo;
@@ -354,11 +350,6 @@ __device__ __forceinline__ void add_sun_terms(const SunskyKArgs& K, DirTerms& t)
             // fp32 next to the sun, the reference's subtraction) and |v|^2 = 4 h^2,
             // sin^2(gamma) = sin^2(2 asin h) = |v|^2 (1 - |v|^2 / 4); the fp32 products widen
             // exactly.  One rounding to fp32 before the square root (relative 3e-8 on cos psi).
-#ifdef SS_PROBE_F32_CPSI   // probe build (A/B of the fp32 form it replaced): never in the product
-            const float h2 = t.h * t.h, sg2 = 4.f * h2 * (1.f - h2);
-            t.sun_cpsi = fast_sqrt(fmaxf(fmaf(-K.inv_sin2_half_ap, sg2, 1.f), 0.f));
-            if (sg2 >= 0.f) return;
-#endif
             const double vx = (double)(t.wx - K.sun_n[0]), vy = (double)(t.wy - K.sun_n[1]),
                          vz = (double)(t.cos_theta - K.sun_n[2]);
             const double v2 = fma(vz, vz, fma(vy, vy, vx * vx));
@@ -416,6 +407,12 @@ __device__ __forceinline__ const typename ChanSel<FAST>::T* chan_table(const Sun
 // the same v the runtime test returns there, without the test's branches and the SGPRs it
 // holds (interleaved A/B, profiles/r04_v13_ab_identity_xform.log: headline eval 3.9 %,
 // RGB sample_direction 2.9 %, pdf_direction 2.2 % faster).
+#ifdef SS_XFORM_IDENTITY
+// Marks the identity code object: the C ABI refuses it as the general module (and a general
+// build as the identity module), so a rotated to_world is never silently dropped.
+extern "C" __global__ void sunsky_xform_identity_marker() {}
+#endif
+
 __device__ __forceinline__ float3_ to_local(const SunskyKArgs& K, float3_ v) {
 #ifdef SS_XFORM_IDENTITY
     (void)K;
@@ -526,17 +523,14 @@ __device__ __forceinline__ void render_sun_rgb_rows(const SunRowsRgb& R, int row
 // Full RGB eval for one local direction (sunsky.cpp:317-323).
 // chans: the 3 channels (K.fsky / K.sky, or an LDS copy in the sampling kernels,
 // whose other constants already fill the SGPR file).
-template <bool FAST, bool HOIST = false, bool PROBE_NO_SKY = false>
+template <bool FAST, bool HOIST = false>
 __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
                                                const float* sun_tab, float3_ wo, bool mask, float out[3],
                                                const SunRowsRgb* rows = nullptr) {
     DirTerms t = dir_terms<FAST>(K, wo, mask);
     if constexpr (FAST) {
 #pragma unroll
-        for (int c = 0; c < 3; ++c) out[c] = PROBE_NO_SKY ? t.gamma : sky_fast(chans[c], t);   // sky_scale and CIE folded
-#ifdef SS_PROBE_NO_SUN_DISC   // probe builds (tools/Makefile) only: cost ablations
-        t.hit_sun = false;
-#endif
+        for (int c = 0; c < 3; ++c) out[c] = sky_fast(chans[c], t);   // sky_scale and CIE folded
         if (t.hit_sun) {
             add_sun_terms<true>(K, t);
             const int row = t.sun_pos - K.sun_row_lo;
@@ -702,9 +696,6 @@ __device__ __forceinline__ void load_vec(const float* p, size_t i, float v[VEC])
 // Outputs are written once and not re-read by this kernel: non-temporal.
 template <int VEC>
 __device__ __forceinline__ void store_vec(float* p, size_t i, const float v[VEC]) {
-#ifdef SS_PROBE_NOSTORE   // tools/gpu_quick.sh compute-only probe build; never in the product
-    if (v[0] != -1234.5f) return;
-#endif
     if constexpr (VEC == 4) {
         f32x4 q = {v[0], v[1], v[2], v[3]};
         __builtin_nontemporal_store(q, reinterpret_cast<f32x4*>(p + i));
@@ -718,9 +709,6 @@ __device__ __forceinline__ void store_vec(float* p, size_t i, const float v[VEC]
 
 // One non-temporal fp32 store (the per-sample kernels).
 __device__ __forceinline__ void store_nt(float v, float* p) {
-#ifdef SS_PROBE_NOSTORE
-    if (v != -1234.5f) return;
-#endif
     __builtin_nontemporal_store(v, p);
 }
 
@@ -937,55 +925,6 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
 // eval(): spectral with per-ray wavelengths (Mitsuba Spectrum<Float, k>):
 // lambda plane k at lam + k * lstride, out plane k at out + k * ostride.
 // ======================================================================
-// PF (nlam == 4 only): software-pipelined grid-stride loop -- the next group's directions and
-// wavelengths are loaded before this group's evaluation, so their HBM latency overlaps it.
-template <int VEC, bool FAST, bool NEG>
-__device__ __forceinline__ void eval_spec_rays_pf_body(const SunskyKArgs& K, const float* __restrict__ wx,
-                                                       const float* __restrict__ wy, const float* __restrict__ wz,
-                                                       const float* __restrict__ lam, size_t lstride,
-                                                       const uint8_t* __restrict__ active, size_t n,
-                                                       float* __restrict__ out, size_t ostride) {
-    __shared__ ChanLds<FAST> S;
-    const auto* chans = stage_chans<FAST>(K, &S);
-    __syncthreads();
-    const size_t nvec = n / VEC;
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    float nx[VEC], ny[VEC], nz[VEC], nl[4][VEC];
-    bool nm[VEC];
-    auto load = [&](size_t vv) {
-        load_dirs<VEC>(wx, wy, wz, active, vv * VEC, nx, ny, nz, nm);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) load_vec<VEC>(lam + (size_t)k * lstride, vv * VEC, nl[k]);
-    };
-    if (v < nvec) load(v);
-    for (; v < nvec; v += stride) {
-        const size_t i = v * VEC;
-        float x[VEC], y[VEC], z[VEC], l4[4][VEC];
-        bool m[VEC];
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) {
-            x[j] = nx[j]; y[j] = ny[j]; z[j] = nz[j]; m[j] = nm[j];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) l4[k][j] = nl[k][j];
-        }
-        if (v + stride < nvec) load(v + stride);
-        DirTerms t[VEC];
-#pragma unroll
-        for (int j = 0; j < VEC; ++j) {
-            t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);
-            add_sun_terms<FAST>(K, t[j]);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float o[VEC];
-#pragma unroll
-            for (int j = 0; j < VEC; ++j) o[j] = eval_spec_one_flat<FAST>(K, chans, K.sun_table, K.sun_ld, t[j], l4[k][j]);
-            store_vec<VEC>(out + (size_t)k * ostride, i, o);
-        }
-    }
-}
-
 template <int VEC, bool FAST, bool NEG, int NL = 0>
 __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                                     const float* __restrict__ wy, const float* __restrict__ wz,
@@ -1030,11 +969,7 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
                 float o[VEC];
 #pragma unroll
                 for (int j = 0; j < VEC; ++j)
-#ifndef SS_PROBE_RAYS_BRANCHY   // probe build (A/B of the branching per-wavelength eval): never in the product
                     o[j] = eval_spec_one_flat<FAST>(K, chans, K.sun_table, K.sun_ld, t[j], l4[k][j]);
-#else
-                    o[j] = eval_spec_one<FAST>(K, chans, K.sun_table, K.sun_ld, t[j], l4[k][j]);
-#endif
                 store_vec<VEC>(out + (size_t)(k0 + k) * ostride, i, o);
             }
         }
@@ -1507,19 +1442,11 @@ __device__ __forceinline__ void sample_direction_body(
         // discrete-distribution reuse divides by the picked gaussian's pmf, so one
         // ulp here moves sky directions by up to ~1e-5 (measured).
         float sun_a = 0.f, sun_b = 0.f;
-#ifndef SS_PROBE_NO_SKY_SAMPLE   // probe builds (tools/Makefile) only: cost ablations
         const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun, &sun_a, &sun_b);
-#else
-        const float3_ sd = sample_sun<FAST>(K, div_exact<FAST>(sx - K.w_sky, w_sun, inv_w_sun), sy);
-#endif
         act = act && (sd.z >= 0.f);
         float3_ d = to_world(K, sd);
         float skyp, sunp;
-#ifndef SS_PROBE_NO_PDF
         sample_pdfs<FAST>(K, S.tgmm, sd, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
-#else
-        skyp = sd.z; sunp = K.sun_pdf;
-#endif
         float pd = lerpf_(sunp, skyp, K.w_sky);
         store_nt(d.x, dx + i);
         store_nt(d.y, dy + i);
@@ -1535,11 +1462,7 @@ __device__ __forceinline__ void sample_direction_body(
         float3_ wo = to_local(K, d);
         if constexpr (!SPEC) {
             float e[3];
-#ifndef SS_PROBE_NO_WEIGHT
             eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, wo, act, e, S.rows);
-#else
-            e[0] = wo.x; e[1] = wo.y; e[2] = wo.z;
-#endif
             const float inv_pd = fdiv<FAST>(1.f, pd);
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
@@ -1591,20 +1514,11 @@ __device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const typename 
         lo[k] = c < kNbWavelengths - 2 ? c : kNbWavelengths - 2;
         f[k] = ok[k] ? nw - (float)lo[k] : 0.f;
     }
-#ifndef SS_PROBE_SPEC_NO_SKY   // probe builds (tools/Makefile) only: cost ablations
 #pragma unroll
     for (int k = 0; k < 4; ++k)
         e[k] = lerpf_(sky_eval<FAST>(chans[lo[k]], t, K.sky_scale), sky_eval<FAST>(chans[lo[k] + 1], t, K.sky_scale),
                       f[k]);
-#else
-#pragma unroll
-    for (int k = 0; k < 4; ++k) e[k] = f[k] * t.r;
-#endif
-#ifndef SS_PROBE_SPEC_NO_SUN
     if (t.hit_sun) {
-#else
-    if (false) {
-#endif
         const SunPowers p = sun_powers(t.sun_x, t.sun_cpsi);
 #pragma unroll
         for (int k = 0; k < 4; ++k) e[k] += sun_spec_pair<FAST>(K, sun_tab, ldp, t.sun_pos, p, lo[k], f[k]);
@@ -1644,19 +1558,11 @@ __device__ __forceinline__ void sample_direction_spec4_body(
         if (i + stride < n) load(i + stride);
         const bool pick_sky = sx < K.w_sky;
         float sun_a = 0.f, sun_b = 0.f;
-#ifndef SS_PROBE_NO_SKY_SAMPLE
         const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun, &sun_a, &sun_b);
-#else
-        const float3_ sd = sample_sun<FAST>(K, div_exact<FAST>(sx - K.w_sky, w_sun, inv_w_sun), sy);
-#endif
         const bool act = sd.z >= 0.f;
         const float3_ d = to_world(K, sd);
         float skyp, sunp;
-#ifndef SS_PROBE_NO_PDF
         sample_pdfs<FAST>(K, S.tgmm, sd, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
-#else
-        skyp = sd.z; sunp = K.sun_pdf;
-#endif
         const float pd = lerpf_(sunp, skyp, K.w_sky);
         store_nt(d.x, dx + i);
         store_nt(d.y, dy + i);
@@ -1792,11 +1698,6 @@ __device__ __forceinline__ void sample_direction_spec4_sorted_body(
             const int q = p * 64 + lane;
             const float l4[4] = {Y[2][q], Y[3][q], Y[4][q], Y[5][q]};
             float o[8];
-#ifdef SS_PROBE_SPEC_UNIFORM_PASSES   // probe build: specialised sky / sun passes, measured 0.7 % slower here
-            if (p * 64 + 64 <= nsky) sample_one_spec4<FAST, 1>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);
-            else if (p * 64 >= nsky) sample_one_spec4<FAST, 2>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);
-            else
-#endif
             sample_one_spec4<FAST>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);
 #pragma unroll
             for (int k = 0; k < 8; ++k) Y[k][q] = o[k];
@@ -1825,31 +1726,15 @@ __device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const Sampl
                                                float sy, bool act, float inv_w, float inv_w_sun, float o[7]) {
     const bool pick_sky = KIND == 1 ? true : KIND == 2 ? false : sx < K.w_sky;
     float sun_a = 0.f, sun_b = 0.f;
-#ifndef SS_PROBE_NO_SKY_SAMPLE   // probe builds (tools/Makefile) only: cost ablations
     const float3_ sd = sample_sky_or_sun<FAST>(K, S.tgmm, pick_sky, sx, sy, inv_w, inv_w_sun, &sun_a, &sun_b);
-#else
-    const float3_ sd = sample_sun<FAST>(K, div_exact<FAST>(sx - K.w_sky, 1.f - K.w_sky, inv_w_sun), sy);
-#endif
     act = act && (sd.z >= 0.f);
     const float3_ d = to_world(K, sd);
     float skyp, sunp;
-#ifndef SS_PROBE_NO_PDF
     sample_pdfs<FAST>(K, S.tgmm, sd, pick_sky, sun_a, sun_b, act, &skyp, &sunp);
-#else
-    skyp = sd.z; sunp = K.sun_pdf;
-#endif
     const float pd = lerpf_(sunp, skyp, K.w_sky);
     o[0] = d.x; o[1] = d.y; o[2] = d.z; o[3] = pd;
     float e[3];
-#ifndef SS_PROBE_NO_WEIGHT
-#ifdef SS_PROBE_SUNPICK_NO_SKY   // probe build (cost bound of the sun picks' sky radiance): wrong results
-    eval_rgb_local<FAST, HOIST, KIND == 2>(K, S.chans.c, K.sun_table, to_local(K, d), act, e, S.rows);
-#else
     eval_rgb_local<FAST, HOIST>(K, S.chans.c, K.sun_table, to_local(K, d), act, e, S.rows);
-#endif
-#else
-    e[0] = d.x; e[1] = d.y; e[2] = d.z;
-#endif
     const float inv_pd = fdiv<FAST>(1.f, pd);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
@@ -1884,12 +1769,8 @@ __device__ __forceinline__ void sample_direction_sorted_body(
         dist = opx = opy = opz = nullptr;
     }
     constexpr int W = 64 * R;
-#ifndef SS_PROBE_SUN_ROWS_BARRIER   // probe build (A/B of the hoisted sun rows): never in the product
     // the LEAN form has VGPRs to spare below the 4-wave cap its LDS sets: hoist the sun-row reads
     constexpr bool kHoist = !FULL;
-#else
-    constexpr bool kHoist = false;
-#endif
     __shared__ SamplerLds<FAST, false> S;
     __shared__ float X[SS_BLOCK / 64][7][W];
     stage_sampler_lds<FAST, false>(K, &S);
@@ -1961,13 +1842,11 @@ __device__ __forceinline__ void sample_direction_sorted_body(
             const int q = p * 64 + lane;
             const bool act = FULL && active ? Y[2][q] != 0.f : true;
             float o[7];
-#ifndef SS_PROBE_MIXED_PASSES   // probe build (A/B of the per-lane pick in every pass): never in the product
             // ranks [0, nsky) are the window's sky picks: a pass wholly on one side takes the
             // specialised body (wave-uniform branch)
             if (p * 64 + 64 <= nsky) sample_one_rgb<FAST, 1, kHoist>(K, S, Y[0][q], Y[1][q], act, inv_w, inv_w_sun, o);
             else if (p * 64 >= nsky) sample_one_rgb<FAST, 2, kHoist>(K, S, Y[0][q], Y[1][q], act, inv_w, inv_w_sun, o);
             else
-#endif
             sample_one_rgb<FAST, 0, kHoist>(K, S, Y[0][q], Y[1][q], act, inv_w, inv_w_sun, o);
 #pragma unroll
             for (int k = 0; k < 7; ++k) Y[k][q] = o[k];
@@ -3582,18 +3461,6 @@ SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays4_v4_fast, 4, true, true, 4)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays4_v4_ref, 4, false, true, 4)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays4_v4_dir_fast, 4, true, false, 4)
 SS_EVAL_SPEC_RAYS(sunsky_eval_spec_rays4_v4_dir_ref, 4, false, false, 4)
-#ifdef SS_PROBE_RAYS_PF   // probe builds only: the software-pipelined per-ray eval at 4 wavelengths
-#define SS_EVAL_SPEC_RAYS_PF(NAME, VEC)                                                                        \
-    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \
-        const SunskyKArgs* __restrict__ Kp, const float* wx, const float* wy, const float* wz, const float* lam, size_t lstride,    \
-        int nlam, const uint8_t* active, size_t n, float* out, size_t ostride, float sign) {                   \
-        (void)sign; (void)nlam;                                                                                \
-        eval_spec_rays_pf_body<VEC, true, true>(*Kp, wx, wy, wz, lam, lstride, active, n, out, ostride);       \
-    }
-SS_EVAL_SPEC_RAYS_PF(probe_rays_pf_v4_fast, 4)
-SS_EVAL_SPEC_RAYS_PF(probe_rays_pf_v2_fast, 2)
-SS_EVAL_SPEC_RAYS_PF(probe_rays_pf_v1_fast, 1)
-#endif
 
 
 #define SS_SAMPLE_DIRECTION(NAME, FAST, SPEC, LEAN)                                                           \

@@ -74,3 +74,23 @@ def test_rotated_to_world_keeps_general_code_object(monkeypatch):
     b = _run(em, "rgb", n, 9)
     for k in a:
         assert torch.equal(a[k].view(torch.int32), b[k].view(torch.int32)), k
+
+
+@pytest.mark.parametrize("var,obj,msg", [
+    ("SUNSKY_AMD_CODE_OBJECT", "sunsky_kernels_ident.hsaco", "is an identity-to_world build"),
+    ("SUNSKY_AMD_CODE_OBJECT_IDENT", "sunsky_kernels.hsaco", "is not an identity-to_world build")])
+def test_code_object_override_of_the_wrong_form_is_refused(var, obj, msg):
+    """An identity build (it exports sunsky_xform_identity_marker) named as the general code
+    object would drop every rotated to_world without an error: the C ABI refuses it at load,
+    and a general build named as the identity object too."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, **{var: os.path.join(os.path.dirname(ss.CODE_OBJECT), obj)})
+    code = ("import sys, torch; sys.path.insert(0, %r); import sunsky_amd as ss\n"
+            "em = ss.load_dict({'type': 'sunsky', 'sun_direction': [0.3, 0.4, 0.866]})\n"
+            "em.eval(ss.SurfaceInteraction3f(wi=-torch.ones((3, 64), device='cuda') / 3 ** 0.5))\n"
+            "torch.cuda.synchronize()\n" % os.path.dirname(os.path.dirname(ss.__file__)))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0, "the wrong-form code object was accepted"
+    assert msg in r.stderr, r.stderr[-2000:]

@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Probe builds of the product kernels, made OUTSIDE the product source.
+
+The shipped `mitsuba3-sunsky_amd/csrc/sunsky_kernels.hip` holds no probe code.  A probe
+(cost ablation, compute-only build, layout experiment) is a list of textual edits applied
+here to a copy of it in tools/build/, which is then compiled to tools/build/probe_<name>.hsaco
+for tools/gpu_ab.sh / kbench.  An edit whose anchor is missing fails loudly, so a probe
+never silently measures the unmodified product.
+
+usage: python tools/mk_probe.py <name> [--src FILE]   (tools/Makefile: make build/probe_<name>.hsaco)
+"""
+import argparse
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(ROOT, "mitsuba3-sunsky_amd", "csrc")
+
+# name -> [(anchor, replacement)]: each anchor must occur exactly once in the product source
+PROBES = {
+    # compute-only: every global store suppressed (kept live by an impossible compare), for
+    # the roofline splits of DESIGN.md §3
+    "nostore": [
+        ("__device__ __forceinline__ void store_vec(float* p, size_t i, const float v[VEC]) {\n",
+         "__device__ __forceinline__ void store_vec(float* p, size_t i, const float v[VEC]) {\n"
+         "    if (v[0] != -1234.5f) return;\n"),
+        ("__device__ __forceinline__ void store_nt(float v, float* p) {\n",
+         "__device__ __forceinline__ void store_nt(float v, float* p) {\n"
+         "    if (v != -1234.5f) return;\n"),
+    ],
+}
+
+
+def make_source(name, src_path):
+    text = open(src_path).read()
+    for anchor, repl in PROBES[name]:
+        if text.count(anchor) != 1:
+            sys.exit(f"mk_probe: probe '{name}': anchor found {text.count(anchor)} times (want 1):\n{anchor}")
+        text = text.replace(anchor, repl)
+    return text
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("name", choices=sorted(PROBES))
+    ap.add_argument("--src", default=os.path.join(CSRC, "sunsky_kernels.hip"))
+    ap.add_argument("--general", action="store_true", help="the general-to_world code object (default: identity)")
+    args = ap.parse_args()
+    build = os.path.join(HERE, "build")
+    os.makedirs(build, exist_ok=True)
+    hip = os.path.join(build, f"probe_{args.name}.hip")
+    with open(hip, "w") as fh:
+        fh.write(make_source(args.name, args.src))
+    cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--genco",
+           "-I" + CSRC, "-I" + os.path.join(ROOT, "include"), "-o", os.path.join(build, f"probe_{args.name}.hsaco"), hip]
+    if not args.general:
+        cmd.insert(5, "-DSS_XFORM_IDENTITY")
+    subprocess.check_call(cmd)
+
+
+if __name__ == "__main__":
+    main()

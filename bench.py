@@ -22,6 +22,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -691,6 +693,93 @@ class C5Watchdog:
         os._exit(self.EXIT_CODE)
 
 
+class LaunchError(SystemExit):
+    """--gpus and the launcher's WORLD_SIZE disagree: exits non-zero before any GPU call."""
+
+
+def launch_plan(gpus, env):
+    """How this process takes part in a `--gpus N` run, decided before anything touches the GPU:
+      "single" -- N = 1 and no launcher: one process, one GPU;
+      "spawn"  -- N > 1 and no launcher (WORLD_SIZE unset): this process starts the N rank
+                  processes itself (spawn_ranks) and only waits for them;
+      "rank"   -- started by a launcher (torchrun or spawn_ranks) with WORLD_SIZE = N.
+    WORLD_SIZE set and different from --gpus raises LaunchError: a --gpus 8 line must never be
+    measured on another number of GPUs."""
+    if gpus < 1:
+        raise LaunchError(f"bench.py: --gpus {gpus}: need at least one GPU")
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        return "spawn" if gpus > 1 else "single"
+    if int(ws) != gpus:
+        raise LaunchError(f"bench.py: --gpus {gpus} but the launcher set WORLD_SIZE={ws}; refusing to measure "
+                          f"{ws} rank(s) as {gpus} GPU(s)")
+    return "rank"
+
+
+SPAWN_GRACE_S = 60.0   # after one rank fails, how long the others may take to finish before they are killed
+
+
+def spawn_ranks(n, argv, grace_s=SPAWN_GRACE_S):
+    """`bench.py --gpus N` without torchrun: N child processes of this script, one per GPU, with
+    RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE and a free MASTER_PORT on 127.0.0.1 (what
+    torchrun --standalone sets).  The parent never touches the GPU: it starts the children before
+    any HIP call and only waits (a process that has initialised HIP must never exec another).
+    Rank 0 prints the bench line.  When a rank fails, the others get `grace_s` to finish (the
+    C5 watchdog ends a rank stuck in a collective) and are then killed.  Returns the exit code:
+    0 when every rank exited 0, else the first failing rank's code (a signal as 128 + signo)."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n))
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                              env=dict(base, RANK=str(r), LOCAL_RANK=str(r))) for r in range(n)]
+    code, failed_at = 0, None
+    while True:
+        for p in procs:
+            rc = p.poll()
+            if rc not in (None, 0) and code == 0:
+                code, failed_at = (rc if rc > 0 else 128 - rc), time.monotonic()
+        alive = [p for p in procs if p.poll() is None]
+        if not alive:
+            return code
+        if failed_at is not None and time.monotonic() - failed_at > grace_s:
+            for p in alive:
+                sys.stderr.write(f"bench.py: killing rank pid {p.pid} ({grace_s:.0f} s after a rank failed)\n")
+                p.kill()
+        time.sleep(0.2)
+
+
+def c5_phase(run, rank, result, limit_s):
+    """configs[4] (`run()`) under a C5Watchdog.  Returns (report, watchdog, failed).  The
+    watchdog stays ARMED: teardown() cancels it after the teardown collectives, so a rank
+    left waiting there (a peer whose C5 raised, or hung) still exits non-zero."""
+    watchdog = C5Watchdog(limit_s, rank, result).start()
+    try:
+        return run(), watchdog, False
+    except Exception as exc:   # reported beside `value`; never fails the bench line itself
+        return {"error": f"{type(exc).__name__}: {exc}"}, watchdog, True
+
+
+def teardown(world, rank, watchdog, c5_failed):
+    """After rank 0 has printed the line.  At world > 1 a rank whose C5 raised skips the
+    teardown collectives (its peers may still sit in C5's) and exits C5Watchdog.EXIT_CODE;
+    the others close the communicators, meet at the barrier and leave the group while the
+    watchdog is still armed."""
+    if world > 1:
+        if c5_failed:
+            sys.stdout.flush()
+            sys.stderr.write(f"bench.py rank {rank}: configs[4] failed; leaving without the teardown collectives\n")
+            sys.stderr.flush()
+            os._exit(C5Watchdog.EXIT_CODE)
+        from sunsky_amd.sharding import clear_radiance_comms
+        clear_radiance_comms()
+        dist.barrier()
+        dist.destroy_process_group()
+    if watchdog is not None:
+        watchdog.cancel()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -708,10 +797,20 @@ def main():
     ap.add_argument("--headline-only", action="store_true",
                     help="run the settle, warmup and timed headline steps only (for a rocprof trace of the burst)")
     ap.add_argument("--c5-dirs", type=int, default=1 << 26, help="configs[4] directions per GPU (default 64M)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="print this rank's launch environment as JSON and exit before any GPU call (tests)")
     args = ap.parse_args()
     SUN_SLACK[0] = 4.0 if args.precision == "reference" else 1.25
 
+    plan = launch_plan(args.gpus, os.environ)
+    if plan == "spawn":            # no launcher: start the N ranks, touch no GPU here
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.launch_check:
+        print(json.dumps({"plan": plan, "gpus": args.gpus, "world": world, "rank": int(os.environ.get("RANK", "0")),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
+        return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # One rank per GPU over RCCL ("nccl").  More ranks than GPUs (a multi-rank rehearsal
@@ -1192,27 +1291,23 @@ def main():
         del full
 
     # ------------------------------------------- configs[4]: spectral shard + gather
-    watchdog = None
+    watchdog, c5_failed = None, False
     if not args.no_c5:
         del outs
-        watchdog = C5Watchdog(float(os.environ.get("SUNSKY_BENCH_C5_TIMEOUT", "150")), rank, result).start()
-        try:
-            c5 = run_c5(args, world, rank, dev, coll_dev, rehearsal)
-        except Exception as exc:   # reported beside `value`; never fail the bench line
-            c5 = {"error": f"{type(exc).__name__}: {exc}"}
-        watchdog.cancel()          # C5 is over: a slow cpu_baseline / teardown is not a C5 timeout
+        c5, watchdog, c5_failed = c5_phase(lambda: run_c5(args, world, rank, dev, coll_dev, rehearsal), rank, result,
+                                           float(os.environ.get("SUNSKY_BENCH_C5_TIMEOUT", "150")))
         if rank == 0:
             result["c5_spectral_shard_gather"] = c5
 
     if rank == 0:
+        if world == 1 and watchdog is not None:
+            watchdog.cancel()   # no collective follows at one rank: a slow cpu_baseline is not a C5 timeout
         if not args.no_cpu and world == 1:   # the CPU baseline: rank 0 at N=1 only
             result["cpu_baseline"] = cpu_baseline(wi.T.cpu().numpy())
         print(json.dumps(result), flush=True)
-    if world > 1:
-        from sunsky_amd.sharding import clear_radiance_comms
-        clear_radiance_comms()
-        dist.barrier()
-        dist.destroy_process_group()
+        if watchdog is not None:
+            watchdog.printed = True      # a later firing (teardown) exits without a second line
+    teardown(world, rank, watchdog, c5_failed)
 
 
 if __name__ == "__main__":

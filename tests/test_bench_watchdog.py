@@ -61,3 +61,107 @@ def test_watchdog_gloo_world2_rank_stuck_in_collective():
     line = json.loads(outs[0][0].strip().splitlines()[-1])
     assert line["value"] == 2.0 and "timed out" in line["c5_spectral_shard_gather"]["error"]
     assert "c5_spectral_shard_gather" not in outs[1][0]        # only rank 0 prints the line
+
+
+# ----------------------------------------------------------- bench.py --gpus N
+def _bench():
+    sys.path.insert(0, ROOT)
+    import bench
+    return bench
+
+
+def test_launch_plan():
+    b = _bench()
+    assert b.launch_plan(1, {}) == "single"
+    assert b.launch_plan(8, {}) == "spawn"
+    assert b.launch_plan(8, {"WORLD_SIZE": "8"}) == "rank"
+    assert b.launch_plan(1, {"WORLD_SIZE": "1"}) == "rank"
+    for gpus, ws in ((4, "8"), (8, "4"), (1, "2"), (2, "1")):
+        try:
+            b.launch_plan(gpus, {"WORLD_SIZE": ws})
+        except b.LaunchError as e:
+            assert f"--gpus {gpus}" in str(e) and f"WORLD_SIZE={ws}" in str(e)
+        else:
+            raise AssertionError(f"--gpus {gpus} with WORLD_SIZE={ws} accepted")
+
+
+def test_gpus_and_world_size_mismatch_exits_nonzero_before_the_gpu():
+    env = dict(os.environ, WORLD_SIZE="8", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0 and "--gpus 4 but the launcher set WORLD_SIZE=8" in p.stderr, p.stderr[-2000:]
+    assert p.stdout.strip() == ""
+
+
+def test_gpus_n_without_a_launcher_spawns_n_ranks():
+    """`bench.py --gpus 3` with no WORLD_SIZE starts 3 rank processes itself (the parent touches
+    no GPU); --launch-check makes each print its launch environment and stop before the GPU."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--launch-check"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = sorted((json.loads(x) for x in p.stdout.strip().splitlines()), key=lambda d: d["rank"])
+    assert [d["rank"] for d in lines] == [0, 1, 2] and [d["local_rank"] for d in lines] == [0, 1, 2]
+    assert {d["world"] for d in lines} == {3} and {d["gpus"] for d in lines} == {3}
+    assert {d["plan"] for d in lines} == {"rank"}
+    assert len({d["master"] for d in lines}) == 1 and lines[0]["master"].startswith("127.0.0.1:")
+
+
+def test_spawned_rank_failure_fails_the_run():
+    """A rank that exits non-zero makes the spawning parent exit non-zero (its peers are given
+    the grace period, then killed).  Here every rank fails fast: no GPU in the CPU suite."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "-1"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0, p.stderr[-2000:]
+
+
+_TEARDOWN = """
+import os, sys, time
+sys.path.insert(0, {root!r})
+import torch.distributed as dist
+import bench
+rank = int(os.environ["RANK"])
+dist.init_process_group("gloo")
+result = {{"metric": "m", "value": 3.0}} if rank == 0 else None
+
+def run():
+    if rank == {bad}:
+        raise RuntimeError("comm setup failed")
+    dist.barrier()                 # the failing rank never joins
+    return {{"ok": True}}
+
+c5, wd, failed = bench.c5_phase(run, rank, result, 4.0)
+if rank == 0:
+    result["c5_spectral_shard_gather"] = c5
+    print(__import__("json").dumps(result), flush=True)
+    wd.printed = True
+bench.teardown(2, rank, wd, failed)
+print("teardown passed", flush=True)
+"""
+
+
+def test_c5_failure_on_one_rank_ends_every_rank_nonzero():
+    """a rank whose configs[4] raised skips the teardown collectives and exits
+    EXIT_CODE; its peer, left in C5's collective, ends non-zero too: gloo raises when the peer
+    is gone (the same path as a C5 error), RCCL would wait and the still-armed watchdog ends it
+    (test_watchdog_gloo_world2_rank_stuck_in_collective)."""
+    for bad in (1, 0):
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
+        procs = [subprocess.Popen([sys.executable, "-c", _TEARDOWN.format(root=ROOT, bad=bad)],
+                                  env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                 for r in range(2)]
+        outs = [p.communicate(timeout=120) for p in procs]
+        codes = [p.returncode for p in procs]
+        assert all(c != 0 for c in codes), (bad, codes, [e[-1500:] for _, e in outs])
+        assert codes[bad] == _exit_code(), (bad, codes)
+        assert "teardown passed" not in outs[0][0] + outs[1][0]
+        lines = [x for x in outs[0][0].splitlines() if x.startswith("{")]
+        assert len(lines) == 1, outs[0][0]            # one bench line, from rank 0 only
+        line = json.loads(lines[0])
+        assert line["value"] == 3.0 and "error" in line["c5_spectral_shard_gather"]
+        if bad == 0:
+            assert "comm setup failed" in line["c5_spectral_shard_gather"]["error"]

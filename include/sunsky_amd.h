@@ -42,11 +42,12 @@
 extern "C" {
 #endif
 
-#define SUNSKY_AMD_ABI_VERSION 6   /* 3: direct_diffuse visibility, direct_diffuse_rays; 4: direct_conductor(_rays),
+#define SUNSKY_AMD_ABI_VERSION 7   /* 3: direct_diffuse visibility, direct_diffuse_rays; 4: direct_conductor(_rays),
                                      emitter_tangent_tables, direct_diffuse draws sample_1 (path.cpp:233);
                                      5: direct_conductor(_rays)_aniso (alpha_u, alpha_v);
                                      6: SUNSKY_TABLE_SUN_SKY_FIT, emitter_inject_staging_fault (testing),
-                                        a rejected update reverts to the last accepted one */
+                                        a rejected update reverts to the last accepted one;
+                                     7: SUNSKY_TABLE_SUN_SEGMENTS, emitter_sun_segments (testing) */
 
 typedef enum sunsky_status {
     SUNSKY_OK = 0,
@@ -84,8 +85,11 @@ typedef enum sunsky_table_id {      /* staged tables, for inspection / parity te
     SUNSKY_TABLE_SPECTRAL_PDF = 6,  /* m_spectral_distr pdf                */
     SUNSKY_TABLE_SPECTRAL_CDF = 7,  /* m_spectral_distr cdf                */
     SUNSKY_TABLE_ALBEDO = 8,        /* extract_albedo() result             */
-    SUNSKY_TABLE_SUN_SKY_FIT = 9    /* 10: the FAST samplers' sun-pick sky pdf fit: c0..c5, bound,
+    SUNSKY_TABLE_SUN_SKY_FIT = 9,   /* 10: the FAST samplers' sun-pick sky pdf fit: c0..c5, bound,
                                        smallest value, usable (0/1), in use for this w_sky (0/1) */
+    SUNSKY_TABLE_SUN_SEGMENTS = 10  /* 47: render_sun's segment decision (sunsky.cpp:579-584) as cos theta
+                                       thresholds z[0..44] (z[j] = smallest fp32 cos theta whose segment
+                                       is >= j), then the disc's first and last segment */
 } sunsky_table_id;
 
 #define SUNSKY_FLAG_INFINITE 0x04u          /* EmitterFlags::Infinite (emitter.h:29-30) */
@@ -173,6 +177,11 @@ int sunsky_emitter_parameters_changed_async(sunsky_emitter *e, void *stream);
  * report a rejected wavelength distribution, so the rollback path above can be exercised
  * without a parameter set that produces one.  0 turns it off. */
 int sunsky_emitter_inject_staging_fault(sunsky_emitter *e, int count);
+/* TESTING ONLY (tests/test_gpu_parity.py): pos[i] = the elevation segment render_sun
+ * (sunsky.cpp:579-584) takes for a direction inside the sun disc whose cos theta is
+ * cos_theta[i], decided by the code the emitter's eval and sampling kernels run (its
+ * precision).  Device int32 output; defined for the cos theta of disc directions. */
+int sunsky_emitter_sun_segments(const sunsky_emitter *e, const float *cos_theta, size_t n, int *pos, void *stream);
 /* Blocking form: _async on the default (null) stream, then waits for the staging. */
 int sunsky_emitter_parameters_changed(sunsky_emitter *e);
 /* set_scene(), sunsky.cpp:287-301: bounding sphere of the scene bbox */

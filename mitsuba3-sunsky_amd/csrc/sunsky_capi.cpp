@@ -107,7 +107,7 @@ enum KernelId {
     K_DIRECT_DIFFUSE_RGB, K_DIRECT_DIFFUSE_SPEC, K_SAMPLE_DIRECTION_RGB_LEAN, K_SAMPLE_DIRECTION_SPEC_LEAN,
     K_DIRECT_DIFFUSE_RAYS, K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN, K_DIRECT_CONDUCTOR_RGB, K_DIRECT_CONDUCTOR_SPEC,
     K_DIRECT_CONDUCTOR_RAYS, K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED, K_SAMPLE_RAY_RGB_SORTED,
-    K_SAMPLE_DIRECTION_RGB_FULL_SORTED, K_EVAL_SPEC_RAYS4_V4, K_COUNT
+    K_SAMPLE_DIRECTION_RGB_FULL_SORTED, K_EVAL_SPEC_RAYS4_V4, K_DEBUG_SUN_SEGMENTS, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
@@ -119,7 +119,7 @@ const char* kKernelNames[K_COUNT] = {
     "sunsky_sample_direction_rgb_lean", "sunsky_sample_direction_spec_lean", "sunsky_direct_diffuse_rays",
     "sunsky_sample_direction_rgb_lean_plain", "sunsky_direct_conductor_rgb", "sunsky_direct_conductor_spec",
     "sunsky_direct_conductor_rays", "sunsky_sample_direction_spec_lean4_sorted", "sunsky_sample_ray_rgb_sorted",
-    "sunsky_sample_direction_rgb_full_sorted", "sunsky_eval_spec_rays4_v4"};
+    "sunsky_sample_direction_rgb_full_sorted", "sunsky_eval_spec_rays4_v4", "sunsky_debug_sun_segments"};
 
 // eval kernels instantiated twice: eval(si) negates wi at compile time,
 // eval_direction(ds) uses ds.d as is (the "_dir" kernels)
@@ -711,6 +711,20 @@ int sunsky_emitter_inject_staging_fault(sunsky_emitter* e, int count) {
     return SUNSKY_OK;
 }
 
+int sunsky_emitter_sun_segments(const sunsky_emitter* e, const float* cos_theta, size_t n, int* pos, void* stream) {
+    if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
+    if (n == 0) return SUNSKY_OK;
+    if (!cos_theta || !pos) return fail(SUNSKY_ERROR_INVALID_VALUE, "null input / output pointer");
+    return guarded([&] {
+        require_device(e);
+        DeviceScope dev_scope(e->device);
+        const SunskyKArgs* K = e->d_state;
+        hipStream_t s = (hipStream_t)stream;
+        void* args[] = {&K, &cos_theta, &n, &pos};
+        launch(e->fn(K_DEBUG_SUN_SEGMENTS, s), grid_for(e->mod, K_DEBUG_SUN_SEGMENTS, n), s, args);
+    });
+}
+
 int sunsky_emitter_parameters_changed(sunsky_emitter* e) {
     if (!e) return fail(SUNSKY_ERROR_INVALID_VALUE, "null emitter");
     int rc = sunsky_emitter_parameters_changed_async(e, nullptr);
@@ -804,6 +818,10 @@ int sunsky_emitter_get_table(const sunsky_emitter* e, int id, float* out, size_t
         case SUNSKY_TABLE_SUN_SKY_FIT:
             v.assign(k.sun_sky_fit, k.sun_sky_fit + 6);
             v.insert(v.end(), {k.sun_sky_fit_dev, k.sun_sky_fit_fmin, (float)k.sun_sky_fit_ok, (float)k.sun_sky_fit_on});
+            break;
+        case SUNSKY_TABLE_SUN_SEGMENTS:
+            v.assign(k.sun_seg_z, k.sun_seg_z + kNbSunSegments);
+            v.insert(v.end(), {(float)k.sun_row_lo, (float)k.sun_row_hi});
             break;
         default: return fail(SUNSKY_ERROR_INVALID_VALUE, "unknown table id");
     }

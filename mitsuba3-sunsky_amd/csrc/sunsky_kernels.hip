@@ -108,17 +108,6 @@ __device__ __forceinline__ float elevation_fast(float z) {
     return big ? fmaf(-2.f, p, kHalfPi) : p;
 }
 
-// FAST cbrt on [0, 1] for the sun segment index (sunsky.cpp:579-587): exp2(log2(x) / 3)
-// with v_log_f32 / v_exp_f32, then one Newton step c - (c^3 - x) / (3 c^2).  No
-// denormal rescaling, sign handling or class fix-ups: the argument is 2 elevation / pi
-// in [0, 1], and x <= 2^-126 (a sun on the horizon) gives segment 0 either way.
-__device__ __forceinline__ float cbrt_unit_fast(float x) {
-    const float c = fast_exp2(__builtin_amdgcn_logf(x) * (1.f / 3.f));
-    const float r = fmaf(c * c, c, -x);
-    const float c1 = fmaf(-r * (1.f / 3.f), fast_rcp(c * c), c);
-    return x > 0x1p-126f ? c1 : 0.f;
-}
-
 // atan on [0, 1]: t + t^3 P(t^2), degree 7 in t^2 (tools/fit_atan.py; 1.07 ulp).
 __device__ __forceinline__ float atan_unit(float t) {
     const float u = t * t;
@@ -317,6 +306,29 @@ __device__ __forceinline__ DirTerms dir_terms(const SunskyKArgs& K, float3_ wo, 
     return t;
 }
 
+// render_sun's segment of a direction inside the sun disc (sunsky.cpp:579-584): the
+// reference's fp32 floor(cbrt(2 elevation / pi) 45) decision, made exactly by counting the
+// host-staged cos theta thresholds it passes (SunskyKArgs::sun_seg_z) over the disc's
+// segments -- one compare each (wave-uniform bounds and table reads) instead of acos / cbrt,
+// and no index flip within ulps of a segment start (tests/test_gpu_parity.py
+// test_sun_segment_index_at_segment_starts).
+__device__ __forceinline__ int sun_segment_index(const SunskyKArgs& K, float cos_theta) {
+    int pos = K.sun_row_lo;
+#pragma unroll 1
+    for (int j = K.sun_row_lo + 1; j <= K.sun_row_hi; ++j) pos += cos_theta >= K.sun_seg_z[j] ? 1 : 0;
+    return pos;
+}
+
+// The reference-precision kernels: the same index, x = elevation - pi/2 (pos / 45)^3 with the
+// reference's elevation = pi/2 - acos(cos theta) (sunsky.cpp:580-587).
+__device__ __forceinline__ int sun_segment_ref(const SunskyKArgs& K, float cos_theta, float* x) {
+    const int pos = sun_segment_index(K, cos_theta);
+    const float elevation = kHalfPi - acosf(cos_theta);
+    const float frac = (float)pos / (float)kNbSunSegments;
+    *x = elevation - kHalfPi * (frac * frac * frac);
+    return pos;
+}
+
 // Sun-disc terms of a direction, once per ray and only on lanes inside the disc.
 // Computed here rather than inside the per-wavelength loops: those calls are
 // loop-invariant, and the compiler would otherwise hoist the acos / cbrt /
@@ -330,18 +342,7 @@ __device__ __forceinline__ void add_sun_terms(const SunskyKArgs& K, DirTerms& t)
     if (t.hit_sun) {
         if constexpr (FAST) {
             float elevation = elevation_fast(t.cos_theta);
-            int pos;
-            if (K.sun_seg_nb >= 0) {
-                // the segment starts the disc straddles (host, SunskyKArgs::sun_seg_bound):
-                // one compare per start instead of cbrt (v_log, v_exp, v_rcp, Newton step)
-                pos = K.sun_row_lo;
-#pragma unroll 1
-                for (int k = 0; k < K.sun_seg_nb; ++k) pos += elevation >= K.sun_seg_bound[k] ? 1 : 0;
-            } else {
-                float seg = cbrt_unit_fast(2.f * elevation * kInvPi) * (float)kNbSunSegments;
-                pos = seg > 0.f ? (int)floorf(seg) : 0;
-                pos = pos < kNbSunSegments - 1 ? pos : kNbSunSegments - 1;
-            }
+            const int pos = sun_segment_index(K, t.cos_theta);
             float frac = (float)pos * (1.f / (float)kNbSunSegments);
             t.sun_pos = pos;
             t.sun_x = elevation - kHalfPi * (frac * frac * frac);
@@ -357,7 +358,7 @@ __device__ __forceinline__ void add_sun_terms(const SunskyKArgs& K, DirTerms& t)
             const float c2 = (float)fma(-inv, v2 * fma(-0.25, v2, 1.0), 1.0);
             t.sun_cpsi = fast_sqrt(fmaxf(c2, 0.f));   // v_sqrt_f32, 1 ulp
         } else {
-            t.sun_pos = sun_segment(t.cos_theta, &t.sun_x);
+            t.sun_pos = sun_segment_ref(K, t.cos_theta, &t.sun_x);
             t.sun_cpsi = cos_psi(t.gamma, K.inv_sin2_half_ap);
         }
     }
@@ -553,7 +554,7 @@ __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const typen
         for (int c = 0; c < 3; ++c) out[c] = sky_ref(chans[c], t, K.sky_scale);
         if (t.hit_sun) {
             float xs;
-            int pos = sun_segment(t.cos_theta, &xs);
+            int pos = sun_segment_ref(K, t.cos_theta, &xs);
             float cpsi = cos_psi(t.gamma, K.inv_sin2_half_ap);
             const float conv = (float)kSpecToRgbSunConv;
 #pragma unroll 1
@@ -3061,7 +3062,7 @@ __device__ __forceinline__ void eval_jvp_rgb_body(const SunskyKArgs& K, const fl
         }
         if (t.hit_sun) {
             float xs, cp, dcp;
-            int pos = sun_segment(t.cos_theta, &xs);
+            int pos = sun_segment_ref(K, t.cos_theta, &xs);
             cos_psi_jvp(K, t, sg, dg, &cp, &dcp);
             const float sc = K.sun_scale * K.area_ratio * conv;
 #pragma unroll 1
@@ -3106,7 +3107,7 @@ __device__ __forceinline__ void eval_jvp_spec_body(const SunskyKArgs& K, const f
         float xs = 0.f, cp = 0.f, dcp = 0.f;
         int pos = 0;
         if (t.hit_sun) {
-            pos = sun_segment(t.cos_theta, &xs);
+            pos = sun_segment_ref(K, t.cos_theta, &xs);
             cos_psi_jvp(K, t, sg, dg, &cp, &dcp);
         }
         for (int q = 0; q < nlam; ++q) {
@@ -3278,7 +3279,7 @@ __device__ __forceinline__ void eval_vjp_rgb_body(const SunskyKArgs& K, const fl
         int pos = 0;
         float xs = 0.f, cp = 0.f, dcps[3] = {0.f, 0.f, 0.f};
         if (t.hit_sun) {
-            pos = sun_segment(t.cos_theta, &xs);
+            pos = sun_segment_ref(K, t.cos_theta, &xs);
 #pragma unroll
             for (int k = 0; k < 3; ++k) cos_psi_jvp(K, t, sg, dgs[k], &cp, &dcps[k]);
         }
@@ -3342,7 +3343,7 @@ __device__ __forceinline__ void eval_vjp_spec_body(const SunskyKArgs& K, const f
         int pos = 0;
         float xs = 0.f, cp = 0.f, dcps[3] = {0.f, 0.f, 0.f};
         if (t.hit_sun) {
-            pos = sun_segment(t.cos_theta, &xs);
+            pos = sun_segment_ref(K, t.cos_theta, &xs);
 #pragma unroll
             for (int k = 0; k < 3; ++k) cos_psi_jvp(K, t, sg, dgs[k], &cp, &dcps[k]);
         }
@@ -3552,6 +3553,30 @@ SS_PDF_DIRECTION(sunsky_pdf_direction_v4_fast, 4, true)
 SS_PDF_DIRECTION(sunsky_pdf_direction_v1_fast, 1, true)
 SS_PDF_DIRECTION(sunsky_pdf_direction_v4_ref, 4, false)
 SS_PDF_DIRECTION(sunsky_pdf_direction_v1_ref, 1, false)
+
+// TESTING ONLY (sunsky_emitter_sun_segments): the segment add_sun_terms picks for a disc
+// direction with this cos theta, i.e. the index every eval / sampling kernel of the
+// precision uses (sunsky.cpp:579-584).
+template <bool FAST>
+__device__ __forceinline__ void debug_sun_segments_body(const SunskyKArgs& K, const float* __restrict__ z, size_t n,
+                                                        int* __restrict__ pos) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const float3_ n_ = mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]);
+        DirTerms t = dir_terms<FAST>(K, n_, true);
+        t.cos_theta = z[i];
+        t.hit_sun = true;
+        add_sun_terms<FAST>(K, t);
+        pos[i] = t.sun_pos;
+    }
+}
+#define SS_DEBUG_SUN_SEGMENTS(NAME, FAST)                                                                     \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(const SunskyKArgs* __restrict__ Kp, const float* z,  \
+                                                                size_t n, int* pos) {                         \
+        debug_sun_segments_body<FAST>(*Kp, z, n, pos);                                                         \
+    }
+SS_DEBUG_SUN_SEGMENTS(sunsky_debug_sun_segments_fast, true)
+SS_DEBUG_SUN_SEGMENTS(sunsky_debug_sun_segments_ref, false)
 
 #define SS_SAMPLE_WAVELENGTHS(NAME, FAST, SPEC)                                                               \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) void NAME(                                               \

@@ -420,29 +420,20 @@ void SunskyModel::stage_geometry() {
                      ? sun_scale_ * k_.area_ratio * (float)kSpecToRgbSunConv * (float)kCieYNormalization
                      : sun_scale_ * k_.area_ratio;
     {
-        // Lowest segment of render_sun's search (sunsky.cpp:579-587) over the elevations of
+        // Segments of render_sun's search (sunsky.cpp:579-587) over the elevations of the
         // directions inside the disc, [eta - aperture / 2, eta + aperture / 2], with a margin
         // far above fp32 rounding: the sampling kernels stage kSunRowsStaged segments from
-        // here (a lane outside them reads the device table).
-        const double lo = std::max(0.0, (double)eta - (double)sun_half_aperture_ - 1e-3);
-        const double seg = std::cbrt(2.0 * std::min(lo, 0.5 * 3.14159265358979323846) / 3.14159265358979323846) *
-                           (double)kNbSunSegments;
-        k_.sun_row_lo = std::min((int)std::floor(seg), kNbSunSegments - 1);
-        // segment starts inside [lo, hi] (the disc's elevations with the same margin): the
-        // FAST kernels count the ones a direction's elevation has passed instead of taking
-        // cbrt(2 elevation / pi) (sunsky.cpp:579-587).  A start is pi/2 (j / 45)^3, the value
-        // the kernels subtract for x, in fp32 as the kernels form it.
-        const double hi = std::min((double)eta + (double)sun_half_aperture_ + 1e-3, 0.5 * 3.14159265358979323846);
-        int nb = 0;
-        for (int j = k_.sun_row_lo + 1; j < kNbSunSegments; ++j) {
-            const float frac = (float)j * (1.f / (float)kNbSunSegments);
-            const float start = kHalfPi * (frac * frac * frac);
-            if ((double)start > hi) break;
-            if (nb == kSunRowsStaged) { nb = -1; break; }
-            k_.sun_seg_bound[nb++] = start;
-        }
-        k_.sun_seg_nb = nb;
-        for (int k = std::max(nb, 0); k < kSunRowsStaged; ++k) k_.sun_seg_bound[k] = 0.f;
+        // sun_row_lo (a lane outside them reads the device table), and every kernel counts the
+        // cos theta thresholds in (sun_row_lo, sun_row_hi] for a disc direction's segment.
+        constexpr double kPiD = 3.14159265358979323846;
+        auto seg_of = [](double elev) {
+            const double seg = std::cbrt(2.0 * std::min(std::max(elev, 0.0), 0.5 * kPiD) / kPiD) * (double)kNbSunSegments;
+            return std::min((int)std::floor(seg), kNbSunSegments - 1);
+        };
+        k_.sun_row_lo = seg_of((double)eta - (double)sun_half_aperture_ - 1e-3);
+        k_.sun_row_hi = seg_of((double)eta + (double)sun_half_aperture_ + 1e-3);
+        const std::array<float, kNbSunSegments>& z = sun_segment_thresholds();
+        std::copy(z.begin(), z.end(), k_.sun_seg_z);
     }
 
     // ---------------- TGMM, sunsky.h:438-501
@@ -521,6 +512,34 @@ void SunskyModel::stage_geometry() {
 // JIT, the prefix count of ((cdf < s) || cdf == 0) && cdf != sum over [0, n-1)
 // (distr_1d.h:116-136); scalar, first + #{i in [first, last) : cdf[i] < s}.
 // Both are monotone in s (cdf is non-decreasing).
+int reference_sun_segment(float cos_theta) {
+    const float pi = 3.14159265358979323846f;
+    const float elevation = 0.5f * pi - acosf(cos_theta);
+    const float seg = cbrtf(2.f * elevation * (1.f / pi)) * (float)kNbSunSegments;
+    const int pos = seg > 0.f ? (int)floorf(seg) : 0;
+    return pos < kNbSunSegments - 1 ? pos : kNbSunSegments - 1;
+}
+
+const std::array<float, kNbSunSegments>& sun_segment_thresholds() {
+    // bisection over the fp32 bit patterns of [0, 1] (ordered like the values): the decision
+    // is monotone there (every fp32 checked against the thresholds in tests/test_capi_cpu.py)
+    static const std::array<float, kNbSunSegments> z = [] {
+        std::array<float, kNbSunSegments> t{};
+        auto val = [](uint32_t b) { float f; std::memcpy(&f, &b, 4); return f; };
+        const uint32_t one = 0x3f800000u;
+        for (int j = 1; j < kNbSunSegments; ++j) {
+            uint32_t lo = 0, hi = one;   // reference_sun_segment(val(hi)) >= j always (44 at 1)
+            while (lo < hi) {
+                const uint32_t mid = lo + (hi - lo) / 2;
+                if (reference_sun_segment(val(mid)) >= j) hi = mid; else lo = mid + 1;
+            }
+            t[j] = val(lo);
+        }
+        return t;
+    }();
+    return z;
+}
+
 int SunskyModel::gauss_search(float s) const {
     if (semantics_ == kJit) {
         int idx = 0;

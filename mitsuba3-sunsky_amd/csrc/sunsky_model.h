@@ -3,6 +3,7 @@
 // (sunsky.cpp:162-301, 772-978; sunsky.h:158-501).  Produces a SunskyKArgs
 // block plus the two small device tables; owns no device memory itself.
 #pragma once
+#include <array>
 #include <string>
 #include <vector>
 
@@ -30,6 +31,13 @@ struct EvalTangent {
     std::vector<float> dsun;   // d sun radiance table (turbidity), else all zero
     float dsun_local[3] = {0, 0, 0};   // d local sun direction (sun_direction)
 };
+
+// render_sun's elevation segment (sunsky.cpp:579-584) in fp32 as the reference forms it:
+// min(floor(cbrt(2 (pi/2 - acos z) / pi) 45), 44), libm acosf / cbrtf, no contraction.
+int reference_sun_segment(float cos_theta);
+// SunskyKArgs::sun_seg_z: [j] = the smallest fp32 cos theta in [0, 1] whose
+// reference_sun_segment is >= j ([0] = 0); computed once per process.
+const std::array<float, kNbSunSegments>& sun_segment_thresholds();
 
 class SunskyModel {
 public:

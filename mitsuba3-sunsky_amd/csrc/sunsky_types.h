@@ -109,12 +109,14 @@ struct SunskyKArgs {
     const float* sun_table;  // device: 45x3x4x6 (RGB) or 45x11x4 (spectral), turbidity-lerped
     const float* sun_ld;     // device: 11x6 limb darkening (spectral only)
     int   sun_row_lo;        // first elevation segment a direction inside the sun disc can reach
-    // Segment search by comparison (FAST sun-disc terms): a disc direction's segment is
-    // sun_row_lo + #{k < sun_seg_nb : elevation >= sun_seg_bound[k]}, the bounds being the
-    // elevations pi/2 (j / 45)^3 of the segment starts j the disc straddles; sun_seg_nb < 0
-    // (a disc over more than kSunRowsStaged segments) keeps the cbrt search.
-    int   sun_seg_nb;
-    float sun_seg_bound[kSunRowsStaged];
+    int   sun_row_hi;        // last one (both with a margin far above fp32 rounding)
+    // render_sun's segment decision (sunsky.cpp:579-584, pos = floor(cbrt(2 elevation / pi) 45)
+    // with elevation = pi/2 - acos(cos theta), all fp32) as cos theta thresholds: sun_seg_z[j]
+    // is the smallest fp32 cos theta whose decision is >= j (the decision is monotone in
+    // cos theta; checked for every fp32 in [0, 1] by tests/test_capi_cpu.py).  A disc
+    // direction's segment is sun_row_lo + #{sun_row_lo < j <= sun_row_hi : cos theta >=
+    // sun_seg_z[j]}: the reference's index bit for bit, without acos / cbrt.  [0] = 0.
+    float sun_seg_z[kNbSunSegments];
     // -------- sky sampling (TGMM + DiscreteDistribution)
     Gaussian gauss[kNbMixture];
     float gauss_cdf[kNbMixture];   // unnormalised inclusive prefix sum

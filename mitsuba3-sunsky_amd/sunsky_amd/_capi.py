@@ -22,7 +22,8 @@ VARIANT_RGB, VARIANT_SPECTRAL = 0, 1
 SEMANTICS_JIT, SEMANTICS_SCALAR = 0, 1
 PRECISION_FAST, PRECISION_REFERENCE = 0, 1
 TABLES = {"sky_params": 0, "sky_radiance": 1, "sun_radiance": 2, "sun_ld": 3, "gaussians": 4,
-          "gaussian_cdf": 5, "spectral_pdf": 6, "spectral_cdf": 7, "albedo": 8, "sun_sky_fit": 9}
+          "gaussian_cdf": 5, "spectral_pdf": 6, "spectral_cdf": 7, "albedo": 8, "sun_sky_fit": 9,
+          "sun_segments": 10}
 FLAG_INFINITE, FLAG_SPATIALLY_VARYING = 0x04, 0x10
 PARAMS = {"turbidity": 0, "albedo": 1, "sun_direction": 2}   # sunsky_param (differentiable, sunsky.cpp:220-240)
 MAX_LAMBDA_PER_RAY = 16   # kMaxLambdaPerRay (csrc/sunsky_types.h)
@@ -69,6 +70,7 @@ _SIGS = {
     "sunsky_emitter_parameters_changed": (C.c_int, [vp]),
     "sunsky_emitter_parameters_changed_async": (C.c_int, [vp, vp]),
     "sunsky_emitter_inject_staging_fault": (C.c_int, [vp, C.c_int]),
+    "sunsky_emitter_sun_segments": (C.c_int, [vp, vp, C.c_size_t, vp, vp]),
     "sunsky_emitter_get_param": (C.c_int, [vp, C.c_char_p, c_float_p, C.c_int, C.POINTER(C.c_int)]),
     "sunsky_emitter_set_scene": (C.c_int, [vp, C.c_int, c_float_p, C.c_float]),
     "sunsky_emitter_set_precision": (C.c_int, [vp, C.c_int]),

@@ -14,6 +14,7 @@ Slice starts are multiples of 4 rays so every rank's SoA planes keep the
 16-byte alignment the VEC=4 eval kernel needs.
 """
 import ctypes as C
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -60,27 +61,45 @@ def gather_shards(local, n_total, dst=0, group=None, bufs=None):
     return bufs if rank == dst else None
 
 
-_COMMS = {}
+_COMMS = {}   # key -> (RadianceComm, weak reference to the process group it was built over)
 
 
 def _group_key(group, dev):
     """Cache key of a communicator: the group object, the device and the group's current
-    rank / size, so a re-initialised world (destroy_process_group + init) never reuses a
-    communicator built for the old one."""
+    rank / size; a process without torch.distributed gets its own world-1 key."""
     if not dist.is_available() or not dist.is_initialized():
         return (None, dev.index, 0, 1)
     return (id(group) if group is not None else None, dev.index, dist.get_rank(group), dist.get_world_size(group))
 
 
-def radiance_comm(group=None, device=None):
+def _world_group(group):
+    """The process group object a communicator for `group` is built over (the default group
+    for None), or None without torch.distributed."""
+    if not dist.is_available() or not dist.is_initialized():
+        return None
+    return group if group is not None else dist.distributed_c10d._get_default_group()
+
+
+def radiance_comm(group=None, device=None, _factory=None):
     """The process's RadianceComm for (group, device), created on first use and kept: a
     communicator costs an RCCL init plus connection setup, far more than one gather.
-    Collective on first use (every rank of the group calls it)."""
+    Collective on first use (every rank of the group calls it).  A cached communicator is
+    reused only while the process group object it was built over is still the current one:
+    a world torn down and re-initialised with the same rank and size (a new group object,
+    whose id() may even equal the old one's) gets a new communicator, and the stale one is
+    closed.  _factory: the communicator class (tests)."""
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     key = _group_key(group, dev)
-    comm = _COMMS.get(key)
-    if comm is None or comm._h is None:
-        comm = _COMMS[key] = RadianceComm(group, dev)
+    g = _world_group(group)
+    entry = _COMMS.get(key)
+    if entry is not None:
+        comm, ref = entry
+        if comm._h is not None and ref() is g:
+            return comm
+        comm.close()
+        del _COMMS[key]
+    comm = (_factory or RadianceComm)(group, dev)
+    _COMMS[key] = (comm, weakref.ref(g) if g is not None else (lambda: None))
     return comm
 
 
@@ -89,7 +108,7 @@ def clear_radiance_comms():
     communicators must not outlive the world they were built for, nor run their
     destructors after RCCL itself is gone at interpreter teardown)."""
     while _COMMS:
-        _, comm = _COMMS.popitem()
+        _, (comm, _) = _COMMS.popitem()
         comm.close()
 
 

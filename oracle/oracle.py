@@ -68,6 +68,10 @@ def lib():
         _lib.oracle_hw_sun_radiance_f32.argtypes = [C.c_void_p] + [C.c_float] * 4
         _lib.oracle_hw_sun_radiance_f64.restype = C.c_double
         _lib.oracle_hw_sun_radiance_f64.argtypes = [C.c_void_p] + [C.c_double] * 4
+        _lib.oracle_sun_segment_f32.restype = C.c_int
+        _lib.oracle_sun_segment_f32.argtypes = [C.c_float]
+        _lib.oracle_check_sun_segment_thresholds.restype = C.c_long
+        _lib.oracle_check_sun_segment_thresholds.argtypes = [C.c_void_p, C.POINTER(C.c_uint)]
         _lib.oracle_sun_table_f32.restype = C.c_size_t
         _lib.oracle_sun_table_f64.restype = C.c_size_t
     return _lib
@@ -312,6 +316,22 @@ def gauss_legendre(n):
     w = np.zeros(n)
     lib().oracle_gauss_legendre(n, _ptr(x), _ptr(w))
     return x, w
+
+
+def sun_segment_f32(cos_theta):
+    """render_sun's fp32 elevation segment of each cos theta (sunsky.cpp:579-584)."""
+    z = np.atleast_1d(np.asarray(cos_theta, np.float32))
+    return np.array([lib().oracle_sun_segment_f32(float(v)) for v in z], np.int32)
+
+
+def check_sun_segment_thresholds(z):
+    """(mismatches, first bad fp32 bit pattern or None): every fp32 in [0, 1] through the fp32
+    segment decision against the threshold table z[0..44] (OpenMP)."""
+    z = np.ascontiguousarray(np.asarray(z, np.float32))
+    assert z.shape == (45,)
+    first = C.c_uint(0)
+    bad = lib().oracle_check_sun_segment_thresholds(z.ctypes.data, C.byref(first))
+    return int(bad), (None if first.value == 0xffffffff else int(first.value))
 
 
 def set_threads(n):

@@ -252,3 +252,31 @@ int oracle_get_quadrature_sum(void) { return g_quad_sum_sequential; }
 #undef R
 #undef SFX
 #undef F
+
+/* Every fp32 cos theta in [0, 1] (bit patterns 0 .. 0x3f800000): does the fp32 segment
+   decision (sun_segment_f32, sunsky.cpp:579-584) equal the count of thresholds z[1..44] it
+   passes (the product's SunskyKArgs::sun_seg_z)?  Returns the number of mismatches; first
+   mismatching bit pattern in *first (0xffffffff when none).  OpenMP over the range. */
+long oracle_check_sun_segment_thresholds(const float *z, unsigned *first) {
+    long bad = 0;
+    unsigned first_bad = 0xffffffffu;
+    const long n = 0x3f800001L;
+#pragma omp parallel for reduction(+ : bad) schedule(static)
+    for (long b = 0; b < n; ++b) {
+        unsigned u = (unsigned)b;
+        float f;
+        memcpy(&f, &u, 4);
+        int lo = 0, hi = 44;          /* largest j with f >= z[j] (z[0] = 0) */
+        while (lo < hi) {
+            int mid = (lo + hi + 1) / 2;
+            if (f >= z[mid]) lo = mid; else hi = mid - 1;
+        }
+        if (lo != oracle_sun_segment_f32(f)) {
+            ++bad;
+#pragma omp critical
+            if (u < first_bad) first_bad = u;
+        }
+    }
+    if (first) *first = first_bad;
+    return bad;
+}

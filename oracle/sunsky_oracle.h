@@ -112,10 +112,16 @@ void oracle_sun_coordinates(int year, int month, int day, float hour, float minu
     int oracle_override_spectral_distr_##SFX(oracle_##SFX *o, const double *pdf, int size);    \
     /* HW solar radiance (restates ArHosekSkyModel.c:686-784 on the packed tables) */          \
     R oracle_hw_sun_radiance_##SFX(const oracle_##SFX *o, R turbidity, R wavelength,            \
-                           R elevation, R gamma);
+                           R elevation, R gamma);                                                \
+    /* render_sun's elevation segment of a cos theta (sunsky.cpp:579-584) */                    \
+    int oracle_sun_segment_##SFX(R cos_theta);
 
 ORACLE_DECL(f32, float)
 ORACLE_DECL(f64, double)
+
+/* every fp32 cos theta in [0, 1] through the fp32 segment decision against a threshold
+   table z[0..44]: the number of mismatches (first bad bit pattern in *first) */
+long oracle_check_sun_segment_thresholds(const float *z, unsigned *first);
 
 #ifdef __cplusplus
 }

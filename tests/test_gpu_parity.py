@@ -414,6 +414,61 @@ def test_sun_disc_weights_across_elevations(elev_deg, precision):
     assert worst <= 1.0, f"sun-disc weights {worst:.2f}x over bound"
 
 
+def _meridian_wo(z, phi):
+    """Directions with cos theta exactly z on the meridian of azimuth phi (fp32)."""
+    z = np.asarray(z, np.float32)
+    st = np.sqrt(np.maximum(np.float32(0), np.float32(1) - z * z)).astype(np.float32)
+    return np.stack([st * np.float32(np.cos(phi)), st * np.float32(np.sin(phi)), z], 1).astype(np.float32)
+
+
+@pytest.mark.parametrize("variant", ["rgb", "spectral"])
+@pytest.mark.parametrize("precision", PRECISIONS)
+@pytest.mark.parametrize("j", [20, 28, 39])
+def test_sun_segment_index_at_segment_starts(j, precision, variant):
+    """render_sun's segment index (sunsky.cpp:579-584) where it flips.
+    The sun sits at segment start j (elevation pi/2 (j/45)^3: 7.90, 21.68, 58.59 deg), so its
+    disc straddles the start.  Every fp32 cos theta within 4096 ulps of the start's threshold,
+    plus random disc directions, goes through the index the kernels use
+    (sunsky_emitter_sun_segments, the add_sun_terms of each precision) and is compared with
+    the fp32 oracle's floor(cbrt(.)) decision: mismatches must be 0.  The same directions on
+    the sun's meridian are then evaluated and held to the parity bars."""
+    eta = np.pi / 2 * (j / 45.0) ** 3
+    d = angles_dict(3.0, 0.4, np.pi / 2 - eta, 0.3, 1.0, 1.0)
+    em = ss.SunskyEmitter(d, variant, precision=precision)
+    o32 = O.Oracle(d, variant, "jit", "f32")
+    o64 = O.Oracle(fp32_sun_input(d, o32), variant, "jit", "f64")
+    inf = o32.info()
+    zt = np.float32(em.table("sun_segments")[j])
+    bits = zt.view(np.int32) + np.arange(-4096, 4097, dtype=np.int32)
+    z_edge = bits.view(np.float32)
+    disc = sun_cone_wo(1 << 14, inf["sun_dir_local"], np.arccos(inf["cos_cutoff"]), seed=j, scale=0.999)
+    z = np.concatenate([z_edge, disc[:, 2]]).astype(np.float32)
+    pos = torch.empty(z.size, dtype=torch.int32, device="cuda")
+    zt_dev = torch.from_numpy(z).cuda()
+    ss._capi.check(ss.lib().sunsky_emitter_sun_segments(em._h, zt_dev.data_ptr(), z.size, pos.data_ptr(), None))
+    got = host(pos)
+    ref = O.sun_segment_f32(z)
+    assert np.all(ref[:4096] == j - 1) and np.all(ref[4096:8193] == j)   # the start lies in the window
+    mismatches = int((got != ref).sum())
+    print(f"segment start {j} ({np.rad2deg(eta):.2f} deg), {precision} {variant}: {mismatches} index mismatches "
+          f"in {z.size} lanes ({z_edge.size} within 4096 ulps of the start)")
+    assert mismatches == 0
+    # the lanes at the start, evaluated: directions on the sun's meridian inside the disc
+    wo = _meridian_wo(z_edge, float(np.arctan2(inf["sun_dir_local"][1], inf["sun_dir_local"][0])))
+    inside = wo.astype(np.float64) @ inf["sun_dir_local"] >= inf["cos_cutoff"]
+    assert inside.all()
+    wi = -wo
+    if variant == "rgb":
+        out = host(em.eval(ss.SurfaceInteraction3f(wi=soa(wi)))).T
+        a, b = o32.eval(wi), o64.eval(wi)
+    else:
+        lams = [float(x) for x in range(320, 721, 40)]
+        out = host(em.eval_spectral_broadcast(soa(wi), lams)).T
+        lam = np.repeat(np.array(lams, np.float32)[:, None], wi.shape[0], 1)
+        a, b = o32.eval(wi, lam).T, o64.eval(wi, lam).T
+    assert_parity(out, a, b, np.ones(wi.shape[0], bool), precision=precision)
+
+
 @pytest.mark.parametrize("turb", [3.0, 4.5])
 @pytest.mark.parametrize("semantics", ["jit", "scalar"])
 def test_discrete_inversion_at_guide_and_cdf_edges(semantics, turb):

@@ -83,8 +83,8 @@ def _key_worker(rank, world, port, out_path):
 
 def test_comm_cache_key_tracks_the_world(tmp_path):
     """the cached RCCL communicator is keyed by the group's rank and size, so a
-    re-initialised world (destroy_process_group + init) never reuses one built for another
-    world, and a process without torch.distributed gets its own world-1 key."""
+    world of another size never reuses one, and a process without torch.distributed gets its
+    own world-1 key (a same-size re-initialisation: the test below)."""
     import socket
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -94,3 +94,47 @@ def test_comm_cache_key_tracks_the_world(tmp_path):
     keys = [tuple(k) for k in np.load(out, allow_pickle=True)]
     assert keys[0] == (None, 0, 0, 1) and keys[2] == keys[0]
     assert keys[1] == (None, 0, 1, 2)
+
+
+class _FakeComm:
+    """Stands in for RadianceComm (no GPU here): counts constructions and closes."""
+    made = []
+
+    def __init__(self, group, dev):
+        self._h = len(_FakeComm.made) + 1
+        _FakeComm.made.append(self)
+
+    def close(self):
+        self._h = None
+
+
+def _reinit_worker(rank, world, port, out_path):
+    from sunsky_amd.sharding import clear_radiance_comms, radiance_comm
+    dev = torch.device("cuda", 0)               # a device object only: no GPU is touched
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a = radiance_comm(device=dev, _factory=_FakeComm)
+    a2 = radiance_comm(device=dev, _factory=_FakeComm)
+    dist.destroy_process_group()
+    dist.init_process_group("gloo", rank=rank, world_size=world)   # same rank, same size
+    b = radiance_comm(device=dev, _factory=_FakeComm)
+    res = [a is a2, b is not a, a._h is None, b._h is not None, len(_FakeComm.made)]
+    clear_radiance_comms()
+    res.append(b._h is None)
+    dist.destroy_process_group()
+    if rank == 1:
+        np.save(out_path, np.array(res, dtype=object), allow_pickle=True)
+
+
+def test_comm_cache_same_size_reinit_gets_a_new_communicator(tmp_path):
+    """a world destroyed and re-initialised with the same rank and size has a new
+    process group object; the cached communicator built over the old one is closed and a new
+    one created, never reused."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = str(tmp_path / "reinit.npy")
+    mp.start_processes(_reinit_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    res = list(np.load(out, allow_pickle=True))
+    assert res == [True, True, True, True, 2, True], res

@@ -107,7 +107,7 @@ enum KernelId {
     K_DIRECT_DIFFUSE_RGB, K_DIRECT_DIFFUSE_SPEC, K_SAMPLE_DIRECTION_RGB_LEAN, K_SAMPLE_DIRECTION_SPEC_LEAN,
     K_DIRECT_DIFFUSE_RAYS, K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN, K_DIRECT_CONDUCTOR_RGB, K_DIRECT_CONDUCTOR_SPEC,
     K_DIRECT_CONDUCTOR_RAYS, K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED, K_SAMPLE_RAY_RGB_SORTED,
-    K_SAMPLE_DIRECTION_RGB_FULL_SORTED, K_EVAL_SPEC_RAYS4_V4, K_DEBUG_SUN_SEGMENTS, K_COUNT
+    K_SAMPLE_DIRECTION_RGB_FULL_SORTED, K_EVAL_SPEC_RAYS4_V4, K_DEBUG_SUN_SEGMENTS, K_SAMPLE_DIRECTION_RGB_POS_SORTED, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
@@ -119,7 +119,8 @@ const char* kKernelNames[K_COUNT] = {
     "sunsky_sample_direction_rgb_lean", "sunsky_sample_direction_spec_lean", "sunsky_direct_diffuse_rays",
     "sunsky_sample_direction_rgb_lean_plain", "sunsky_direct_conductor_rgb", "sunsky_direct_conductor_spec",
     "sunsky_direct_conductor_rays", "sunsky_sample_direction_spec_lean4_sorted", "sunsky_sample_ray_rgb_sorted",
-    "sunsky_sample_direction_rgb_full_sorted", "sunsky_eval_spec_rays4_v4", "sunsky_debug_sun_segments"};
+    "sunsky_sample_direction_rgb_full_sorted", "sunsky_eval_spec_rays4_v4", "sunsky_debug_sun_segments",
+    "sunsky_sample_direction_rgb_pos_sorted"};
 
 // eval kernels instantiated twice: eval(si) negates wi at compile time,
 // eval_direction(ds) uses ds.d as is (the "_dir" kernels)
@@ -204,7 +205,7 @@ int blocks_per_cu(KernelId k) {
         case K_SAMPLE_DIRECTION_RGB: case K_SAMPLE_DIRECTION_SPEC: case K_PDF_DIRECTION_V4: case K_PDF_DIRECTION_V1:
         case K_SAMPLE_DIRECTION_RGB_LEAN: case K_SAMPLE_DIRECTION_SPEC_LEAN:
         case K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN: case K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED:
-        case K_SAMPLE_RAY_RGB_SORTED: case K_SAMPLE_DIRECTION_RGB_FULL_SORTED:
+        case K_SAMPLE_RAY_RGB_SORTED: case K_SAMPLE_DIRECTION_RGB_FULL_SORTED: case K_SAMPLE_DIRECTION_RGB_POS_SORTED:
             return 64;
         case K_BAKE_RGB: case K_BAKE_SPEC: return 64;
         case K_DIRECT_DIFFUSE_RGB: case K_DIRECT_DIFFUSE_SPEC: case K_DIRECT_DIFFUSE_RAYS: return 64;
@@ -987,18 +988,24 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
         // sorted-vs-unsorted tests); read per call so a test can switch it
         const char* uns = std::getenv("SUNSKY_AMD_UNSORTED_SAMPLING");
         const bool unsorted = uns && uns[0] == '1';
-        // SUNSKY_AMD_SORTED_GENERAL_SAMPLING=1: the general RGB call through the wave-sorted
+        // SUNSKY_AMD_SORTED_GENERAL_SAMPLING=1: the masked general RGB call through the wave-sorted
         // kernel (10 % slower than the unsorted one; bitwise tests only)
         const char* sgs = std::getenv("SUNSKY_AMD_SORTED_GENERAL_SAMPLING");
         const bool sorted_general = sgs && sgs[0] == '1' && !unsorted;
-        // spectral LEAN at Mitsuba's 4 wavelengths per sample: the wave-sorted kernel
+        // spectral LEAN at Mitsuba's 4 wavelengths per sample: the wave-sorted kernel.  RGB
+        // without a mask (Mitsuba's DirectionSample call: it.p in, ds.dist / ds.p out) takes the
+        // LEAN windows with it.p read at the store stage (kSortPos); with a mask, the unsorted
+        // general kernel.
         const KernelId k = spec ? (lean ? (nlam == 4 && !unsorted ? K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED
                                                                   : K_SAMPLE_DIRECTION_SPEC_LEAN)
                                         : K_SAMPLE_DIRECTION_SPEC)
                                 : (lean ? (unsorted ? K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN : K_SAMPLE_DIRECTION_RGB_LEAN)
-                                        : (sorted_general ? K_SAMPLE_DIRECTION_RGB_FULL_SORTED : K_SAMPLE_DIRECTION_RGB));
+                                        : sorted_general ? K_SAMPLE_DIRECTION_RGB_FULL_SORTED
+                                        : (!active && !unsorted) ? K_SAMPLE_DIRECTION_RGB_POS_SORTED
+                                                                 : K_SAMPLE_DIRECTION_RGB);
         // the wave-sorted kernels: one wave takes a window of 4 (RGB) or 3 (spectral) x 64 samples
-        const size_t items = (k == K_SAMPLE_DIRECTION_RGB_LEAN || k == K_SAMPLE_DIRECTION_RGB_FULL_SORTED) ? (n + 3) / 4
+        const size_t items = (k == K_SAMPLE_DIRECTION_RGB_LEAN || k == K_SAMPLE_DIRECTION_RGB_FULL_SORTED ||
+                              k == K_SAMPLE_DIRECTION_RGB_POS_SORTED) ? (n + 3) / 4
                              : k == K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED ? (n + 2) / 3 : n;
         launch(e->fn(k, (hipStream_t)stream), grid_for(e->mod, k, items), (hipStream_t)stream, args);
     });

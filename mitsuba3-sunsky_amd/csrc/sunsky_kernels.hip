@@ -397,6 +397,11 @@ __device__ __forceinline__ float sky_eval(const typename ChanSel<FAST>::T& k, co
     else return sky_ref(k, t, sky_scale);
 }
 
+// A channel gathered with a per-lane index: from an AoS table (eval kernels, sample_ray), or
+// from the FAST spectral samplers' SoA table (FastChanSoA, below).
+template <class T>
+__device__ __forceinline__ T chan_get(const T* chans, int c) { return chans[c]; }
+
 template <bool FAST>
 __device__ __forceinline__ const typename ChanSel<FAST>::T* chan_table(const SunskyKArgs& K) {
     if constexpr (FAST) return K.fsky;
@@ -1039,10 +1044,44 @@ __device__ __forceinline__ void stage_tgmm(const SunskyKArgs& K, TgmmLds<FAST>* 
 // fast kernels no reference-order gaussians.
 template <bool FAST, int N> struct ChanLdsN { typename ChanSel<FAST>::T c[N]; };
 
+// The 11 FAST spectral channels as a structure of arrays for the samplers' per-lane gathers
+// (4 wavelengths x 2 channels per sample).  Gathered from the 48-byte FastChannel records the
+// compiler split each gather into ds_read_b128 + ds_read_b96 + ds_read2_b32 (or a
+// ds_read2_b64 merging channels lo and lo + 1), whose banks are (a/4) mod 32: records 8
+// channels apart share them, a bank conflict whenever a lane group holds channels c and c + 8
+// (1.01e8 SQ_LDS_BANK_CONFLICT cycles per dispatch).  Here the parts are 16, 16
+// and 8 bytes at strides of 4, 4 and 2 dwords: the 11 channels of a part span 44 (b128, banks
+// mod 64) and 22 dwords (< 32), so every gather is conflict-free in any banking.
+struct FastChanSoA {
+    f32x4 q0[kNbWavelengths];   // A, Bl2, El2, P
+    f32x4 q1[kNbWavelengths];   // Q, Cs, Ds, Fs
+    f32x2 q2[kNbWavelengths];   // Gs, Hs
+};
+
+__device__ __forceinline__ FastChannel chan_get(const FastChanSoA* s, int c) {
+    const f32x4 a = s->q0[c], b = s->q1[c];
+    const f32x2 d = s->q2[c];
+    FastChannel k;
+    k.A = a.x; k.Bl2 = a.y; k.El2 = a.z; k.P = a.w;
+    k.Q = b.x; k.Cs = b.y; k.Ds = b.z; k.Fs = b.w;
+    k.Gs = d.x; k.Hs = d.y; k.pad[0] = k.pad[1] = 0.f;
+    return k;
+}
+
+__device__ __forceinline__ void stage_chan_soa(const FastChannel* src, FastChanSoA* s) {
+    for (int c = threadIdx.x; c < kNbWavelengths; c += blockDim.x) {
+        const FastChannel& k = src[c];
+        s->q0[c] = f32x4{k.A, k.Bl2, k.El2, k.P};
+        s->q1[c] = f32x4{k.Q, k.Cs, k.Ds, k.Fs};
+        s->q2[c] = f32x2{k.Gs, k.Hs};
+    }
+}
+
 template <bool FAST, bool SPEC>
 struct SamplerLds {
     TgmmLds<FAST> tgmm;
     ChanLdsN<FAST, SPEC ? kNbWavelengths : 3> chans;   // spectral: per-lane channel index
+    FastChanSoA chsoa[FAST && SPEC ? 1 : 0];           // FAST spectral: the same channels, SoA (gathers)
     SpecDistLds sdist[SPEC ? 1 : 0];
     alignas(16) float sun[SPEC ? kSunSpecTableSize : 0];   // spectral: the whole turbidity-lerped table
     SunRowsRgb rows[SPEC ? 0 : 1];                 // RGB: the disc's segments, channels interleaved
@@ -1054,6 +1093,7 @@ template <bool FAST, bool SPEC>
 __device__ __forceinline__ void stage_sampler_lds(const SunskyKArgs& K, SamplerLds<FAST, SPEC>* s) {
     stage_tgmm<FAST>(K, &s->tgmm);
     lds_copy(s->chans.c, chan_table<FAST>(K), SPEC ? kNbWavelengths : 3);
+    if constexpr (FAST && SPEC) stage_chan_soa(K.fsky, s->chsoa);
     if constexpr (SPEC) {
         stage_spec_dist(K, &s->sdist[0]);
         lds_copy(s->ld, K.sun_ld, kNbWavelengths * kNbSunLdParams);
@@ -1062,6 +1102,13 @@ __device__ __forceinline__ void stage_sampler_lds(const SunskyKArgs& K, SamplerL
     if constexpr (SPEC) lds_copy(s->sun, K.sun_table, kSunSpecTableSize);
     else stage_sun_rows(K, s->rows);
     __syncthreads();
+}
+
+// The channel table the spectral samplers gather from per lane: the SoA form in FAST.
+template <bool FAST, bool SPEC>
+__device__ __forceinline__ auto chan_src(const SamplerLds<FAST, SPEC>& S) {
+    if constexpr (FAST && SPEC) return &S.chsoa[0];
+    else return &S.chans.c[0];
 }
 
 // DiscreteDistribution::sample_reuse (distr_1d.h:173-183): JIT predicate
@@ -1354,10 +1401,9 @@ __device__ __forceinline__ float spectral_sample_pdf(const SunskyKArgs& K, const
 // wavelength; ldp in the LdPairs layout), taken by sample_ray (1.26x faster there, interleaved
 // A/B); the standalone sample_wavelengths kernel keeps the rolled eval_spec_one (ld_tab plain),
 // whose 67 VGPRs hold 7 waves/SIMD (eval_spec4: 121 VGPRs, 7 % slower).
-template <bool FAST>
-__device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
-                                           const float* sun_tab, const float* ldp, const DirTerms& t,
-                                           const float lam[4], float e[4]);
+template <bool FAST, class CH>
+__device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const CH* chans, const float* sun_tab,
+                                           const float* ldp, const DirTerms& t, const float lam[4], float e[4]);
 template <bool FAST, bool EVAL4>
 __device__ __forceinline__ void sample_wavelengths_one(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
                                                        const SpecDistLds& D, const float* sun_tab,
@@ -1391,10 +1437,9 @@ __device__ __forceinline__ void sample_wavelengths_one(const SunskyKArgs& K, con
 // LEAN: the host found it_p, ds.dist, ds.p and the active mask all NULL (the common
 // call, u -> d, pdf, weight); the optional pointers and their branches are compiled
 // out, which frees the SGPRs the kernel otherwise spills through v_writelane/v_readlane.
-template <bool FAST>
-__device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
-                                           const float* sun_tab, const float* ldp, const DirTerms& t,
-                                           const float lam[4], float e[4]);
+template <bool FAST, class CH>
+__device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const CH* chans, const float* sun_tab,
+                                           const float* ldp, const DirTerms& t, const float lam[4], float e[4]);
 template <bool FAST, bool SPEC, bool LEAN = false>
 __device__ __forceinline__ void sample_direction_body(
     const SunskyKArgs& K, const float* __restrict__ ux, const float* __restrict__ uy,
@@ -1477,7 +1522,7 @@ __device__ __forceinline__ void sample_direction_body(
             if (nlam == 4) {   // Mitsuba's Spectrum<Float, 4>: the LEAN kernel's eval, same bits
                 const float l4[4] = {lam[i], lam[lstride + i], lam[2 * lstride + i], lam[3 * lstride + i]};
                 float e[4];
-                eval_spec4<FAST>(K, S.chans.c, S.sun, S.ldp, t, l4, e);
+                eval_spec4<FAST>(K, chan_src(S), S.sun, S.ldp, t, l4, e);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const float w = FAST ? e[k] * inv_pd : e[k] / pd;
@@ -1500,10 +1545,9 @@ __device__ __forceinline__ void sample_direction_body(
 // b at t = 1 exactly, so a node (f = 0, where eval_spec_one skips the lerp) and 720 nm
 // (lo = 10, f = 0 there; lo = 9, f = 1 here) give eval_spec_one's bits; the sun-disc
 // terms of the 4 wavelengths run in one branch per lane.
-template <bool FAST>
-__device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
-                                           const float* sun_tab, const float* ldp, const DirTerms& t,
-                                           const float lam[4], float e[4]) {
+template <bool FAST, class CH>
+__device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const CH* chans, const float* sun_tab,
+                                           const float* ldp, const DirTerms& t, const float lam[4], float e[4]) {
     int lo[4];
     float f[4];
     bool ok[4];
@@ -1517,7 +1561,8 @@ __device__ __forceinline__ void eval_spec4(const SunskyKArgs& K, const typename 
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-        e[k] = lerpf_(sky_eval<FAST>(chans[lo[k]], t, K.sky_scale), sky_eval<FAST>(chans[lo[k] + 1], t, K.sky_scale),
+        e[k] = lerpf_(sky_eval<FAST>(chan_get(chans, lo[k]), t, K.sky_scale),
+                      sky_eval<FAST>(chan_get(chans, lo[k] + 1), t, K.sky_scale),
                       f[k]);
     if (t.hit_sun) {
         const SunPowers p = sun_powers(t.sun_x, t.sun_cpsi);
@@ -1572,7 +1617,7 @@ __device__ __forceinline__ void sample_direction_spec4_body(
         DirTerms t = dir_terms<FAST>(K, to_local(K, d), act);
         add_sun_terms<FAST>(K, t);
         float e[4];
-        eval_spec4<FAST>(K, S.chans.c, S.sun, S.ldp, t, l, e);
+        eval_spec4<FAST>(K, chan_src(S), S.sun, S.ldp, t, l, e);
         const float inv_pd = fdiv<FAST>(1.f, pd);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1614,7 +1659,7 @@ __device__ __forceinline__ void sample_one_spec4(const SunskyKArgs& K, const Sam
     DirTerms t = dir_terms<FAST>(K, to_local(K, d), act);
     add_sun_terms<FAST>(K, t);
     float e[4];
-    eval_spec4<FAST>(K, S.chans.c, S.sun, S.ldp, t, l, e);
+    eval_spec4<FAST>(K, chan_src(S), S.sun, S.ldp, t, l, e);
     const float inv_pd = fdiv<FAST>(1.f, pd);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -1757,20 +1802,27 @@ __device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const Sampl
 // functions of d and it.p, computed after the un-sort from each lane's own it.p.  Each
 // sample is computed by sample_one_rgb from its own u: bitwise the outputs of
 // sample_direction_body<FAST, false, !FULL>.
-template <bool FAST, int R, bool FULL>
+// MODE: kSortLean (u -> d, pdf, weight), kSortFull (+ it.p, mask, ds.dist, ds.p; it.p loaded
+// before the passes) or kSortPos (Mitsuba's unmasked DirectionSample call: it.p in, ds.dist and
+// ds.p out; the LEAN passes, it.p loaded only at the store stage, so nothing extra is held
+// across the passes).
+constexpr int kSortLean = 0, kSortFull = 1, kSortPos = 2;
+template <bool FAST, int R, int MODE>
 __device__ __forceinline__ void sample_direction_sorted_body(
     const SunskyKArgs& K, const float* __restrict__ ux, const float* __restrict__ uy,
     const float* __restrict__ px, const float* __restrict__ py, const float* __restrict__ pz,
     const uint8_t* __restrict__ active, size_t n, float* __restrict__ dx, float* __restrict__ dy,
     float* __restrict__ dz, float* __restrict__ pdf, float* __restrict__ dist, float* __restrict__ opx,
     float* __restrict__ opy, float* __restrict__ opz, float* __restrict__ weight, size_t wstride) {
-    if constexpr (!FULL) {
+    constexpr bool FULL = MODE == kSortFull;
+    if constexpr (MODE == kSortLean) {
         px = py = pz = nullptr;
-        active = nullptr;
         dist = opx = opy = opz = nullptr;
     }
+    if constexpr (!FULL) active = nullptr;
     constexpr int W = 64 * R;
-    // the LEAN form has VGPRs to spare below the 4-wave cap its LDS sets: hoist the sun-row reads
+    // the LEAN / POS forms have VGPRs to spare below the 4-wave cap their LDS sets: hoist the
+    // sun-row reads
     constexpr bool kHoist = !FULL;
     __shared__ SamplerLds<FAST, false> S;
     __shared__ float X[SS_BLOCK / 64][7][W];
@@ -1854,15 +1906,29 @@ __device__ __forceinline__ void sample_direction_sorted_body(
         }
         wave_lds_order();
         float* const planes[7] = {dx, dy, dz, pdf, weight, weight + wstride, weight + 2 * wstride};
+        // POS: this window's it.p, all R loads issued before the stores consume them
+        float qpx[MODE == kSortPos ? R : 1], qpy[MODE == kSortPos ? R : 1], qpz[MODE == kSortPos ? R : 1];
+        if constexpr (MODE == kSortPos) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const size_t i = base + (size_t)(r * 64 + lane);
+                const bool in = (dist || opx) && px && i < n;
+                qpx[r] = in ? px[i] : 0.f;
+                qpy[r] = in ? py[i] : 0.f;
+                qpz[r] = in ? pz[i] : 0.f;
+            }
+        }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const size_t i = base + (size_t)(r * 64 + lane);
             if (i < n) {
 #pragma unroll
                 for (int k = 0; k < 7; ++k) store_nt(Y[k][slot[r]], planes[k] + i);
-                if (FULL && (dist || opx)) {   // as sample_direction_body: ds.dist, ds.p (sunsky.cpp:417-420)
+                if (MODE != kSortLean && (dist || opx)) {   // as sample_direction_body: ds.dist, ds.p (sunsky.cpp:417-420)
                     const float3_ d = mk3(Y[0][slot[r]], Y[1][slot[r]], Y[2][slot[r]]);
-                    float3_ itp = mk3(ipx[FULL ? r : 0], ipy[FULL ? r : 0], ipz[FULL ? r : 0]);
+                    float3_ itp = MODE == kSortPos ? mk3(qpx[MODE == kSortPos ? r : 0], qpy[MODE == kSortPos ? r : 0],
+                                                         qpz[MODE == kSortPos ? r : 0])
+                                                   : mk3(ipx[FULL ? r : 0], ipy[FULL ? r : 0], ipz[FULL ? r : 0]);
                     float3_ rel = mk3(itp.x - K.bs_center[0], itp.y - K.bs_center[1], itp.z - K.bs_center[2]);
                     float dd = 2.f * fmaxf(K.bs_radius, sqrtf(dot3(rel, rel)));
                     if (dist) dist[i] = dd;
@@ -2286,7 +2352,7 @@ __device__ __forceinline__ void eval_spec_point(const SunskyKArgs& K, const Samp
                                                 const DirTerms& t, const float wl[C], int nlam, float e[C]) {
     static_assert(C == 4, "up to 4 wavelengths per point");
     if (nlam == 4) {
-        eval_spec4<FAST>(K, S.chans.c, S.sun, S.ldp, t, wl, e);
+        eval_spec4<FAST>(K, chan_src(S), S.sun, S.ldp, t, wl, e);
     } else {
 #pragma unroll
         for (int c = 0; c < C; ++c) e[c] = c < nlam ? eval_spec_one<FAST>(K, S.chans.c, S.sun, S.ld, t, wl[c]) : 0.f;
@@ -3517,12 +3583,12 @@ SS_SAMPLE_DIRECTION_SPEC4_SORTED(sunsky_sample_direction_spec_lean4_sorted_ref, 
 // the previous LEAN spectral form (wavelength loop, lambda not prefetched), for A/B timing
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_loop_fast, true, true, true)
 
-#define SS_SAMPLE_DIRECTION_SORTED(NAME, FAST, R, FULL)                                                           \
+#define SS_SAMPLE_DIRECTION_SORTED(NAME, FAST, R, MODE)                                                           \
     extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_RGB_SORTED_ATTR void NAME(                            \
         const SunskyKArgs* __restrict__ Kp, const float* ux, const float* uy, const float* px, const float* py, const float* pz,   \
         const float* lam, size_t lstride, int nlam, const uint8_t* active, size_t n, float* dx, float* dy,     \
         float* dz, float* pdf, float* dist, float* opx, float* opy, float* opz, float* weight, size_t wstride) { \
-        sample_direction_sorted_body<FAST, R, FULL>(*Kp, ux, uy, px, py, pz, active, n, dx, dy, dz, pdf, dist, \
+        sample_direction_sorted_body<FAST, R, MODE>(*Kp, ux, uy, px, py, pz, active, n, dx, dy, dz, pdf, dist, \
                                                     opx, opy, opz, weight, wstride);                           \
     }
 // LEAN RGB sample_direction (the C ABI's common call): wave-sorted windows of 4 x 64
@@ -3531,16 +3597,20 @@ SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_loop_fast, true, true, tru
 // precisions reproduce the general kernel's bits (test_sample_direction_lean_kernel_bitwise,
 // test_wave_sorted_rgb_kernels_bitwise_vs_unsorted) since the file contracts within
 // expressions only (the pragma at the top).
-SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_fast, true, SS_SORT_R, false)
-SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_ref, false, SS_SORT_R, false)
+SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_fast, true, SS_SORT_R, kSortLean)
+SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_ref, false, SS_SORT_R, kSortLean)
 // The general call (it.p, ds.dist, ds.p, mask) in the same windows: bitwise the unsorted kernel
 // (test_wave_sorted_rgb_kernels_bitwise_vs_unsorted) but slower: 2 % in round 2 (125 VGPRs and 28
 // SGPR spills, profiles/r02_v13_ab_sample_full.log), 14 % against the round-3 unsorted general kernel,
 // 10 % with the mask and it.p prefetched (114 VGPRs, 42 SGPR spills;
 // profiles/r03_v23_ab_sample_full.log), so the C ABI keeps the unsorted general kernel and takes this one
 // only with SUNSKY_AMD_SORTED_GENERAL_SAMPLING=1 (test_wave_sorted_rgb_kernels_bitwise_vs_unsorted).
-SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_full_sorted_fast, true, 4, true)
-SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_full_sorted_ref, false, 4, true)
+SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_full_sorted_fast, true, 4, kSortFull)
+SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_full_sorted_ref, false, 4, kSortFull)
+// Mitsuba's DirectionSample call (it.p in, ds.dist / ds.p out, no mask: path.cpp:216 ->
+// scene.cpp:295-348) in the LEAN windows, it.p read at the store stage.
+SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_pos_sorted_fast, true, SS_SORT_R, kSortPos)
+SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_pos_sorted_ref, false, SS_SORT_R, kSortPos)
 
 
 #define SS_PDF_DIRECTION(NAME, VEC, FAST)                                                                     \

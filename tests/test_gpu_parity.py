@@ -276,7 +276,9 @@ def test_wave_sorted_rgb_kernels_bitwise_vs_unsorted(precision, monkeypatch):
     (SUNSKY_AMD_UNSORTED_SAMPLING=1) the outputs d, pdf and weight are bit for bit the same,
     and both equal the general call's (+ it.p, ds.dist, ds.p, an active mask), for batch
     sizes that end inside a window, a row or a lane (1 ... 2^20 + 1), all-sky and all-sun
-    windows, u.x at w_sky and next to it, at 0 and at 1 - ulp, and a rotated emitter."""
+    windows, u.x at w_sky and next to it, at 0 and at 1 - ulp, and a rotated emitter.  The
+    unmasked general call (the wave-sorted kSortPos kernel) equals the unsorted general kernel
+    on every output, ds.p and ds.dist included."""
     d = angles_dict(3.0, 1.1, np.deg2rad(60), 0.3, 1.0, 1.0)
     d["to_world"] = np.array([[0, 0, 1, 0], [1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 0, 1]], np.float64)
     em = ss.SunskyEmitter(d, "rgb", precision=precision)
@@ -306,10 +308,18 @@ def test_wave_sorted_rgb_kernels_bitwise_vs_unsorted(precision, monkeypatch):
         monkeypatch.delenv("SUNSKY_AMD_UNSORTED_SAMPLING", raising=False)
         lean = run(ut, ss.Interaction3f(), None, False)
         full = run(ut, ss.Interaction3f(p=p), None, True)
+        origin = run(ut, ss.Interaction3f(), None, True)     # ds.dist / ds.p requested, it.p = origin
         monkeypatch.setenv("SUNSKY_AMD_UNSORTED_SAMPLING", "1")
         plain = run(ut, ss.Interaction3f(), None, False)
         for a_, b_, c_ in zip(lean, plain, full):
             assert np.array_equal(a_, b_) and np.array_equal(a_, c_), n
+        # Mitsuba's unmasked DirectionSample call runs in the LEAN windows with it.p read at the
+        # store stage (kSortPos): every output, ds.p and ds.dist included, is the unsorted
+        # general kernel's (SUNSKY_AMD_UNSORTED_SAMPLING=1 selects that one)
+        for a_, b_ in zip(full, run(ut, ss.Interaction3f(p=p), None, True)):
+            assert np.array_equal(a_, b_), n
+        for a_, b_ in zip(origin, run(ut, ss.Interaction3f(), None, True)):
+            assert np.array_equal(a_, b_), n
         # the general call with a mask: masked samples carry zero weight, the others the LEAN values
         masked = run(ut, ss.Interaction3f(p=p), mask, True)
         mk = host(mask)

@@ -1,0 +1,185 @@
+// c5_probe.hip -- access-shape ceiling of configs[4]'s per-rank leg (the C3 node kernel at
+// 64M directions): read 3 fp32 planes, write 11, trivial compute.  At 64M the 805 MB of
+// inputs and 2.95 GB of outputs exceed the 256 MiB Infinity Cache, so every launch is cold.
+// Variants of the store shape: lanes x directions per lane, plain /
+// non-temporal stores, grid-stride vs contiguous spans per workgroup, and LDS-staged writes
+// that emit each plane in whole contiguous rows.  Also the reads-only and writes-only legs.
+// usage: c5_probe [n_dirs]   (prints one line per variant and grid; best per variant last)
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); std::exit(1); } } while (0)
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+constexpr int K = 11;
+
+template <int VEC> struct V;
+template <> struct V<1> { typedef float t; };
+template <> struct V<2> { typedef f2 t; };
+template <> struct V<4> { typedef f4 t; };
+
+// grid-stride, VEC directions per lane, one store per plane (the node kernel's shape at VEC 4)
+template <int VEC, bool NT>
+__global__ __launch_bounds__(256) void gs(const float* x, const float* y, const float* z, float* out, size_t n,
+                                          size_t ostride) {
+    typedef typename V<VEC>::t fv;
+    size_t nv = n / VEC, stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+        fv a = *(const fv*)(x + VEC * v), b = *(const fv*)(y + VEC * v), c = *(const fv*)(z + VEC * v);
+        fv s = a + b + c;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            fv o = s * (float)(k + 1);
+            if (NT) __builtin_nontemporal_store(o, (fv*)(out + (size_t)k * ostride + VEC * v));
+            else *(fv*)(out + (size_t)k * ostride + VEC * v) = o;
+        }
+    }
+}
+
+// contiguous span per workgroup: workgroup b owns directions [b * span, (b + 1) * span),
+// walked in 1024-direction steps (VEC = 4)
+__global__ __launch_bounds__(256) void span4(const float* x, const float* y, const float* z, float* out, size_t n,
+                                             size_t ostride) {
+    const size_t nv = n / 4, per = (nv + gridDim.x - 1) / gridDim.x;
+    const size_t v0 = (size_t)blockIdx.x * per, v1 = v0 + per < nv ? v0 + per : nv;
+    for (size_t v = v0 + threadIdx.x; v < v1; v += blockDim.x) {
+        f4 a = *(const f4*)(x + 4 * v), b = *(const f4*)(y + 4 * v), c = *(const f4*)(z + 4 * v);
+        f4 s = a + b + c;
+#pragma unroll
+        for (int k = 0; k < K; ++k) __builtin_nontemporal_store(s * (float)(k + 1), (f4*)(out + (size_t)k * ostride + 4 * v));
+    }
+}
+
+// loads of the next group issued before this group's stores (software pipelined, VEC 4)
+__global__ __launch_bounds__(256) void gs4_pf(const float* x, const float* y, const float* z, float* out, size_t n,
+                                              size_t ostride) {
+    size_t nv = n / 4, stride = (size_t)gridDim.x * blockDim.x;
+    size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    f4 a = 0, b = 0, c = 0;
+    if (v < nv) { a = *(const f4*)(x + 4 * v); b = *(const f4*)(y + 4 * v); c = *(const f4*)(z + 4 * v); }
+    for (; v < nv; v += stride) {
+        f4 s = a + b + c;
+        size_t w = v + stride;
+        if (w < nv) { a = *(const f4*)(x + 4 * w); b = *(const f4*)(y + 4 * w); c = *(const f4*)(z + 4 * w); }
+#pragma unroll
+        for (int k = 0; k < K; ++k) __builtin_nontemporal_store(s * (float)(k + 1), (f4*)(out + (size_t)k * ostride + 4 * v));
+    }
+}
+
+// two groups of 4 directions per lane per iteration, 1024 directions apart: 22 stores in flight
+__global__ __launch_bounds__(256) void gs4x2(const float* x, const float* y, const float* z, float* out, size_t n,
+                                             size_t ostride) {
+    size_t nv = n / 4, stride = (size_t)gridDim.x * blockDim.x * 2;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x * 2 + threadIdx.x; v < nv; v += stride) {
+        size_t w = v + blockDim.x;
+        f4 s0 = *(const f4*)(x + 4 * v) + *(const f4*)(y + 4 * v) + *(const f4*)(z + 4 * v);
+        f4 s1 = w < nv ? *(const f4*)(x + 4 * w) + *(const f4*)(y + 4 * w) + *(const f4*)(z + 4 * w) : f4{0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            __builtin_nontemporal_store(s0 * (float)(k + 1), (f4*)(out + (size_t)k * ostride + 4 * v));
+            if (w < nv) __builtin_nontemporal_store(s1 * (float)(k + 1), (f4*)(out + (size_t)k * ostride + 4 * w));
+        }
+    }
+}
+
+// plane-outer: each lane writes plane k for its 4 directions, all lanes of the workgroup
+// before the next plane (a __syncthreads between planes orders the workgroup's streams)
+__global__ __launch_bounds__(256) void gs4_sync(const float* x, const float* y, const float* z, float* out, size_t n,
+                                                size_t ostride) {
+    size_t nv = n / 4, stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v0 = (size_t)blockIdx.x * blockDim.x; v0 < nv; v0 += stride) {
+        size_t v = v0 + threadIdx.x;
+        f4 s = 0;
+        if (v < nv) s = *(const f4*)(x + 4 * v) + *(const f4*)(y + 4 * v) + *(const f4*)(z + 4 * v);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (v < nv) __builtin_nontemporal_store(s * (float)(k + 1), (f4*)(out + (size_t)k * ostride + 4 * v));
+            if (k == 5) __syncthreads();
+        }
+    }
+}
+
+// reads only (the 3 input planes; one conditional store that never fires keeps them live)
+__global__ __launch_bounds__(256) void rd4(const float* x, const float* y, const float* z, float* out, size_t n,
+                                           size_t) {
+    size_t nv = n / 4, stride = (size_t)gridDim.x * blockDim.x;
+    f4 acc = 0;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride)
+        acc += *(const f4*)(x + 4 * v) + *(const f4*)(y + 4 * v) + *(const f4*)(z + 4 * v);
+    if (acc.x == -1234.5f) out[0] = acc.y;
+}
+
+// writes only (the 11 output planes)
+__global__ __launch_bounds__(256) void wr4(const float*, const float*, const float*, float* out, size_t n,
+                                           size_t ostride) {
+    size_t nv = n / 4, stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+        f4 s = {(float)v, 1.f, 2.f, 3.f};
+#pragma unroll
+        for (int k = 0; k < K; ++k) __builtin_nontemporal_store(s * (float)(k + 1), (f4*)(out + (size_t)k * ostride + 4 * v));
+    }
+}
+
+typedef void (*Kern)(const float*, const float*, const float*, float*, size_t, size_t);
+
+double run(const char* name, Kern kern, int vec, const float* x, const float* y, const float* z, float* out, size_t n,
+           int cu, double bytes_per_dir, std::vector<int> mults = {4, 8, 16, 32, 64}) {
+    double best = 1e30;
+    int bm = 0;
+    for (int mult : mults) {
+        unsigned grid = (unsigned)std::min<size_t>((n / vec + 255) / 256, (size_t)cu * mult);
+        for (int w = 0; w < 2; ++w) kern<<<grid, 256>>>(x, y, z, out, n, n);
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        const int it = 10;
+        CK(hipEventRecord(e0));
+        for (int i = 0; i < it; ++i) kern<<<grid, 256>>>(x, y, z, out, n, n);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        double us = 1e3 * ms / it;
+        printf("%-10s vec=%d bpcu=%-3d %9.1f us  %7.1f GB/s\n", name, vec, mult, us, bytes_per_dir * n / (us * 1e-6) / 1e9);
+        if (us < best) { best = us; bm = mult; }
+        CK(hipEventDestroy(e0));
+        CK(hipEventDestroy(e1));
+    }
+    printf("BEST %-10s %9.1f us at bpcu=%d  %7.1f GB/s\n", name, best, bm, bytes_per_dir * n / (best * 1e-6) / 1e9);
+    fflush(stdout);
+    return best;
+}
+
+int main(int argc, char** argv) {
+    const size_t n = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : ((size_t)1 << 26);
+    int cu = 0;
+    CK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0));
+    float *x, *y, *z, *out;
+    CK(hipMalloc(&x, n * 4));
+    CK(hipMalloc(&y, n * 4));
+    CK(hipMalloc(&z, n * 4));
+    CK(hipMalloc(&out, n * 4 * K));
+    CK(hipMemset(x, 0, n * 4));
+    CK(hipMemset(y, 0, n * 4));
+    CK(hipMemset(z, 0, n * 4));
+    printf("n = %zu directions, 3 read + %d write planes (%.1f MB in, %.1f MB out)\n", n, K, 12.0 * n / 1e6,
+           4.0 * K * n / 1e6);
+    const double b = 12.0 + 4.0 * K;
+    double rd = run("reads", rd4, 4, x, y, z, out, n, cu, 12.0);
+    double wr = run("writes", wr4, 4, x, y, z, out, n, cu, 4.0 * K);
+    printf("SERIAL_SUM %9.1f us  %7.1f GB/s\n", rd + wr, b * n / ((rd + wr) * 1e-6) / 1e9);
+    run("gs4_nt", gs<4, true>, 4, x, y, z, out, n, cu, b);
+    run("gs2_nt", gs<2, true>, 2, x, y, z, out, n, cu, b);
+    run("gs1_nt", gs<1, true>, 1, x, y, z, out, n, cu, b);
+    run("gs4_plain", gs<4, false>, 4, x, y, z, out, n, cu, b);
+    run("span4", span4, 4, x, y, z, out, n, cu, b, {1, 2, 4, 8});
+    run("gs4_pf", gs4_pf, 4, x, y, z, out, n, cu, b);
+    run("gs4x2", gs4x2, 8, x, y, z, out, n, cu, b);
+    run("gs4_sync", gs4_sync, 4, x, y, z, out, n, cu, b);
+    return 0;
+}

@@ -881,7 +881,12 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
 
 // Broadcast at exactly the 11 model wavelengths 320:40:720 nm (lerp factor 0,
 // sunsky.cpp:332-343): channel c -> plane c with compile-time channel indices.
-template <int VEC, bool FAST, bool NEG>
+// G: groups of VEC directions per lane per grid-stride step, blockDim * VEC directions apart,
+// so a workgroup writes G * 1 KB contiguous per plane per step (SS_NODES_G, tools/c5_probe.hip).
+#ifndef SS_NODES_G
+#define SS_NODES_G 1
+#endif
+template <int VEC, bool FAST, bool NEG, int G = SS_NODES_G>
 __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                                      const float* __restrict__ wy, const float* __restrict__ wz,
                                                      const uint8_t* __restrict__ active, size_t n,
@@ -890,8 +895,12 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
     const auto* chans = stage_chans<FAST>(K, &S);
     __syncthreads();
     const size_t nvec = n / VEC;
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x * G;
+    for (size_t v0 = (size_t)blockIdx.x * blockDim.x * G + threadIdx.x; v0 < nvec; v0 += stride) {
+#pragma unroll 1
+      for (int g = 0; g < G; ++g) {
+        const size_t v = v0 + (size_t)g * blockDim.x;
+        if (v >= nvec) break;
         const size_t i = v * VEC;
         float x[VEC], y[VEC], z[VEC];
         bool m[VEC];
@@ -924,6 +933,7 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
             for (int j = 0; j < VEC; ++j) o[j] = t[j].active ? o[j] : 0.f;
             store_vec<VEC>(out + (size_t)c * ostride, i, o);
         }
+      }
     }
 }
 
@@ -1635,6 +1645,15 @@ __device__ __forceinline__ void wave_lds_order() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// Window storage of the wave-sorted kernels: sky picks at ascending addresses from 0, sun picks
+// at descending addresses from W - 1.  A 32-lane group's sky run and sun run then cover
+// complementary banks of the 32-bank rows ((a/4) mod 32; W a multiple of 32), so the ranked
+// writes, the passes' reads and writes and the un-sort reads are all conflict-free (with both
+// classes at ascending addresses the two runs overlapped: up to 2-way conflicts on every row
+// access, 2.9e7 SQ_LDS_BANK_CONFLICT cycles per 64M-sample spectral dispatch).  Combined rank
+// q (sky picks first) -> address.
+__device__ __forceinline__ int win_addr(int q, int nsky, int W) { return q < nsky ? q : (W - 1 + nsky) - q; }
+
 __device__ __forceinline__ int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
@@ -1706,7 +1725,6 @@ __device__ __forceinline__ void sample_direction_spec4_sorted_body(
     for (; w < nwin; w += wstep) {
         const size_t base = w * W;
         int slot[R], nsky = 0;
-        (void)nsky;
         {
             float a[R], b[R], l[4][R];
             uint64_t m[R];
@@ -1720,14 +1738,11 @@ __device__ __forceinline__ void sample_direction_spec4_sorted_body(
             if (w + wstep < nwin) load_window(w + wstep);
 #pragma unroll
             for (int r = 0; r < R; ++r) m[r] = __ballot(a[r] < K.w_sky);
-            int psun = 0;
-#pragma unroll
-            for (int r = 0; r < R; ++r) psun += __popcll(m[r]);
-            int psky = 0;
+            int psky = 0, psun = 0;   // sky / sun picks of the rows before this one
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const bool sky = (m[r] >> lane) & 1;
-                slot[r] = sky ? psky + lanes_below(m[r]) : psun + lanes_below(~m[r]);
+                slot[r] = sky ? psky + lanes_below(m[r]) : (W - 1) - (psun + lanes_below(~m[r]));   // win_addr
                 Y[0][slot[r]] = a[r];
                 Y[1][slot[r]] = b[r];
 #pragma unroll
@@ -1741,7 +1756,7 @@ __device__ __forceinline__ void sample_direction_spec4_sorted_body(
         wave_lds_order();
 #pragma unroll 1
         for (int p = 0; p < R; ++p) {
-            const int q = p * 64 + lane;
+            const int q = win_addr(p * 64 + lane, nsky, W);
             const float l4[4] = {Y[2][q], Y[3][q], Y[4][q], Y[5][q]};
             float o[8];
             sample_one_spec4<FAST>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);
@@ -1860,14 +1875,11 @@ __device__ __forceinline__ void sample_direction_sorted_body(
             if (w + wstep < nwin) load_window(w + wstep);
 #pragma unroll
             for (int r = 0; r < R; ++r) m[r] = __ballot(a[r] < K.w_sky);
-            int psun = 0;
-#pragma unroll
-            for (int r = 0; r < R; ++r) psun += __popcll(m[r]);
-            int psky = 0;
+            int psky = 0, psun = 0;   // sky / sun picks of the rows before this one
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const bool sky = (m[r] >> lane) & 1;
-                slot[r] = sky ? psky + lanes_below(m[r]) : psun + lanes_below(~m[r]);
+                slot[r] = sky ? psky + lanes_below(m[r]) : (W - 1) - (psun + lanes_below(~m[r]));   // win_addr
                 Y[0][slot[r]] = a[r];
                 Y[1][slot[r]] = b[r];
                 if (FULL && active) Y[2][slot[r]] = nm[r];
@@ -1892,7 +1904,7 @@ __device__ __forceinline__ void sample_direction_sorted_body(
         wave_lds_order();
 #pragma unroll 1
         for (int p = 0; p < R; ++p) {
-            const int q = p * 64 + lane;
+            const int q = win_addr(p * 64 + lane, nsky, W);
             const bool act = FULL && active ? Y[2][q] != 0.f : true;
             float o[7];
             // ranks [0, nsky) are the window's sky picks: a pass wholly on one side takes the
@@ -2169,7 +2181,7 @@ __device__ __forceinline__ void sample_ray_rgb_sorted_body(
     if (w < nwin) load_window(w);
     for (; w < nwin; w += wstep) {
         const size_t base = w * W;
-        int slot[R];
+        int slot[R], nsky = 0;
         float c2[R], d2[R];
         {
             float a[R], b[R];
@@ -2184,25 +2196,23 @@ __device__ __forceinline__ void sample_ray_rgb_sorted_body(
             if (w + wstep < nwin) load_window(w + wstep);
 #pragma unroll
             for (int r = 0; r < R; ++r) m[r] = __ballot(a[r] < K.w_sky);
-            int psun = 0;
-#pragma unroll
-            for (int r = 0; r < R; ++r) psun += __popcll(m[r]);
-            int psky = 0;
+            int psky = 0, psun = 0;   // sky / sun picks of the rows before this one
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 const bool sky = (m[r] >> lane) & 1;
-                slot[r] = sky ? psky + lanes_below(m[r]) : psun + lanes_below(~m[r]);
+                slot[r] = sky ? psky + lanes_below(m[r]) : (W - 1) - (psun + lanes_below(~m[r]));   // win_addr
                 Y[0][slot[r]] = a[r];
                 Y[1][slot[r]] = b[r];
                 const int c = __popcll(m[r]);
                 psky += c;
                 psun += 64 - c;
             }
+            nsky = psky;
         }
         wave_lds_order();
 #pragma unroll 1
         for (int p = 0; p < R; ++p) {
-            const int q = p * 64 + lane;
+            const int q = win_addr(p * 64 + lane, nsky, W);
             const float sx = Y[0][q], sy = Y[1][q];
             const bool pick_sky = sx < K.w_sky;
             float sun_a = 0.f, sun_b = 0.f;

@@ -87,6 +87,58 @@ __global__ __launch_bounds__(256) void gs4x2(const float* x, const float* y, con
     }
 }
 
+// G groups of 4 directions per lane per iteration, 1024 directions apart (a workgroup covers
+// 1024 G contiguous directions per iteration); SEQ: each group's 11 stores before the next
+// group's loads (the node kernel computing one group at a time), else all loads first and the
+// stores interleaved by plane
+template <int G, bool SEQ>
+__global__ __launch_bounds__(256) void gs4xg(const float* x, const float* y, const float* z, float* out, size_t n,
+                                             size_t ostride) {
+    size_t nv = n / 4, stride = (size_t)gridDim.x * blockDim.x * G;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x * G + threadIdx.x; v < nv; v += stride) {
+        if constexpr (SEQ) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const size_t w = v + (size_t)g * blockDim.x;
+                if (w >= nv) break;
+                f4 s0 = *(const f4*)(x + 4 * w) + *(const f4*)(y + 4 * w) + *(const f4*)(z + 4 * w);
+#pragma unroll
+                for (int k = 0; k < K; ++k) __builtin_nontemporal_store(s0 * (float)(k + 1), (f4*)(out + (size_t)k * ostride + 4 * w));
+            }
+        } else {
+            f4 s[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const size_t w = v + (size_t)g * blockDim.x;
+                s[g] = w < nv ? *(const f4*)(x + 4 * w) + *(const f4*)(y + 4 * w) + *(const f4*)(z + 4 * w) : f4{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    const size_t w = v + (size_t)g * blockDim.x;
+                    if (w < nv) __builtin_nontemporal_store(s[g] * (float)(k + 1), (f4*)(out + (size_t)k * ostride + 4 * w));
+                }
+        }
+    }
+}
+
+// 8 consecutive directions per lane (two 16-byte stores per plane, adjacent)
+__global__ __launch_bounds__(256) void gs8(const float* x, const float* y, const float* z, float* out, size_t n,
+                                           size_t ostride) {
+    size_t nv = n / 8, stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+        const f4* X = (const f4*)(x + 8 * v); const f4* Y = (const f4*)(y + 8 * v); const f4* Z = (const f4*)(z + 8 * v);
+        f4 s0 = X[0] + Y[0] + Z[0], s1 = X[1] + Y[1] + Z[1];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            f4* o = (f4*)(out + (size_t)k * ostride + 8 * v);
+            __builtin_nontemporal_store(s0 * (float)(k + 1), o);
+            __builtin_nontemporal_store(s1 * (float)(k + 1), o + 1);
+        }
+    }
+}
+
 // plane-outer: each lane writes plane k for its 4 directions, all lanes of the workgroup
 // before the next plane (a __syncthreads between planes orders the workgroup's streams)
 __global__ __launch_bounds__(256) void gs4_sync(const float* x, const float* y, const float* z, float* out, size_t n,
@@ -180,6 +232,10 @@ int main(int argc, char** argv) {
     run("span4", span4, 4, x, y, z, out, n, cu, b, {1, 2, 4, 8});
     run("gs4_pf", gs4_pf, 4, x, y, z, out, n, cu, b);
     run("gs4x2", gs4x2, 8, x, y, z, out, n, cu, b);
+    run("gs4x2_seq", gs4xg<2, true>, 8, x, y, z, out, n, cu, b);
+    run("gs4x4", gs4xg<4, false>, 16, x, y, z, out, n, cu, b);
+    run("gs4x4_seq", gs4xg<4, true>, 16, x, y, z, out, n, cu, b);
+    run("gs8", gs8, 8, x, y, z, out, n, cu, b);
     run("gs4_sync", gs4_sync, 4, x, y, z, out, n, cu, b);
     return 0;
 }

@@ -30,6 +30,9 @@ PROBES = {
          "__device__ __forceinline__ void store_nt(float v, float* p) {\n"
          "    if (v != -1234.5f) return;\n"),
     ],
+    # the C3 / C5 node kernel with 2 / 4 groups of 4 directions per lane per grid-stride step
+    "nodes_g2": [("#define SS_NODES_G 1\n", "#define SS_NODES_G 2\n")],
+    "nodes_g4": [("#define SS_NODES_G 1\n", "#define SS_NODES_G 4\n")],
 }
 
 

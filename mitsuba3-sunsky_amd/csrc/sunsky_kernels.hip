@@ -881,12 +881,12 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
 
 // Broadcast at exactly the 11 model wavelengths 320:40:720 nm (lerp factor 0,
 // sunsky.cpp:332-343): channel c -> plane c with compile-time channel indices.
-// G: groups of VEC directions per lane per grid-stride step, blockDim * VEC directions apart,
-// so a workgroup writes G * 1 KB contiguous per plane per step (SS_NODES_G, tools/c5_probe.hip).
-#ifndef SS_NODES_G
-#define SS_NODES_G 1
-#endif
-template <int VEC, bool FAST, bool NEG, int G = SS_NODES_G>
+// Work split: workgroup b owns a contiguous span of G = ceil(n / (VEC x the grid's lanes))
+// steps of blockDim x VEC directions, walked one step (4 KB per plane per workgroup) at a
+// time, instead of a grid-stride loop.  At configs[4]'s 64M directions per GPU (G = 4) each
+// workgroup writes 16 KB contiguous per plane; at 16M (G = 1) the split is the grid-stride
+// loop's.  (tools/c5_probe.hip: 3-read / 11-write shapes at 64M, cold; A/B in DESIGN.md §3.)
+template <int VEC, bool FAST, bool NEG>
 __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                                      const float* __restrict__ wy, const float* __restrict__ wz,
                                                      const uint8_t* __restrict__ active, size_t n,
@@ -895,11 +895,12 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
     const auto* chans = stage_chans<FAST>(K, &S);
     __syncthreads();
     const size_t nvec = n / VEC;
-    const size_t stride = (size_t)gridDim.x * blockDim.x * G;
-    for (size_t v0 = (size_t)blockIdx.x * blockDim.x * G + threadIdx.x; v0 < nvec; v0 += stride) {
+    const size_t lanes = (size_t)gridDim.x * blockDim.x;
+    const size_t G = (nvec + lanes - 1) / lanes;
+    {
 #pragma unroll 1
-      for (int g = 0; g < G; ++g) {
-        const size_t v = v0 + (size_t)g * blockDim.x;
+      for (size_t g = 0; g < G; ++g) {
+        const size_t v = ((size_t)blockIdx.x * G + g) * blockDim.x + threadIdx.x;
         if (v >= nvec) break;
         const size_t i = v * VEC;
         float x[VEC], y[VEC], z[VEC];

@@ -30,9 +30,18 @@ PROBES = {
          "__device__ __forceinline__ void store_nt(float v, float* p) {\n"
          "    if (v != -1234.5f) return;\n"),
     ],
-    # the C3 / C5 node kernel with 2 / 4 groups of 4 directions per lane per grid-stride step
-    "nodes_g2": [("#define SS_NODES_G 1\n", "#define SS_NODES_G 2\n")],
-    "nodes_g4": [("#define SS_NODES_G 1\n", "#define SS_NODES_G 4\n")],
+    # the C3 / C5 node kernel's grid-stride loop (the split before round 5), for A/B
+    "nodes_gridstride": [
+        ("""    const size_t G = (nvec + lanes - 1) / lanes;
+    {
+#pragma unroll 1
+      for (size_t g = 0; g < G; ++g) {
+        const size_t v = ((size_t)blockIdx.x * G + g) * blockDim.x + threadIdx.x;
+        if (v >= nvec) break;
+""", """    {
+#pragma unroll 1
+      for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += lanes) {
+""")],
 }
 
 

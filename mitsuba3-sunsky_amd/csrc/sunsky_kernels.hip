@@ -1512,8 +1512,8 @@ __device__ __forceinline__ void sample_direction_body(
         if (dist || opx) {
             float3_ rel = mk3(itp.x - K.bs_center[0], itp.y - K.bs_center[1], itp.z - K.bs_center[2]);
             float dd = 2.f * fmaxf(K.bs_radius, sqrtf(dot3(rel, rel)));
-            if (dist) dist[i] = dd;
-            if (opx) { opx[i] = fmaf(d.x, dd, itp.x); opy[i] = fmaf(d.y, dd, itp.y); opz[i] = fmaf(d.z, dd, itp.z); }
+            if (dist) store_nt(dd, dist + i);
+            if (opx) { store_nt(fmaf(d.x, dd, itp.x), opx + i); store_nt(fmaf(d.y, dd, itp.y), opy + i); store_nt(fmaf(d.z, dd, itp.z), opz + i); }
         }
         // weight = eval(si{wi = -d}) / pdf, zeroed when not finite (sunsky.cpp:430-439)
         float3_ wo = to_local(K, d);
@@ -1537,14 +1537,14 @@ __device__ __forceinline__ void sample_direction_body(
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const float w = FAST ? e[k] * inv_pd : e[k] / pd;
-                    weight[(size_t)k * wstride + i] = isfinite(w) ? w : 0.f;
+                    store_nt(isfinite(w) ? w : 0.f, weight + (size_t)k * wstride + i);
                 }
                 continue;
             }
             for (int k = 0; k < nlam; ++k) {
                 float e = eval_spec_one<FAST>(K, S.chans.c, S.sun, S.ld, t, lam[(size_t)k * lstride + i]);
                 float w = FAST ? e * inv_pd : e / pd;
-                weight[(size_t)k * wstride + i] = isfinite(w) ? w : 0.f;
+                store_nt(isfinite(w) ? w : 0.f, weight + (size_t)k * wstride + i);
             }
         }
     }
@@ -1944,8 +1944,8 @@ __device__ __forceinline__ void sample_direction_sorted_body(
                                                    : mk3(ipx[FULL ? r : 0], ipy[FULL ? r : 0], ipz[FULL ? r : 0]);
                     float3_ rel = mk3(itp.x - K.bs_center[0], itp.y - K.bs_center[1], itp.z - K.bs_center[2]);
                     float dd = 2.f * fmaxf(K.bs_radius, sqrtf(dot3(rel, rel)));
-                    if (dist) dist[i] = dd;
-                    if (opx) { opx[i] = fmaf(d.x, dd, itp.x); opy[i] = fmaf(d.y, dd, itp.y); opz[i] = fmaf(d.z, dd, itp.z); }
+                    if (dist) store_nt(dd, dist + i);
+                    if (opx) { store_nt(fmaf(d.x, dd, itp.x), opx + i); store_nt(fmaf(d.y, dd, itp.y), opy + i); store_nt(fmaf(d.z, dd, itp.z), opz + i); }
                 }
             }
         }
@@ -2067,8 +2067,8 @@ __device__ __forceinline__ void sample_wavelengths_body(const SunskyKArgs& K, co
         if constexpr (!SPEC) {
             float e[3];
             eval_rgb_local<FAST>(K, K.sun_table, wo, act, e);
-            for (int c = 0; c < 3; ++c) weight[(size_t)c * wstride + i] = e[c];
-            for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = 0.f;
+            for (int c = 0; c < 3; ++c) store_nt(e[c], weight + (size_t)c * wstride + i);
+            for (int k = 0; k < 4; ++k) store_nt(0.f, lam_out + (size_t)k * lstride + i);
         } else {
             DirTerms t = dir_terms<FAST>(K, wo, act);
             add_sun_terms<FAST>(K, t);
@@ -2121,26 +2121,26 @@ __device__ __forceinline__ void sample_ray_body(const SunskyKArgs& K, const floa
         if constexpr (!SPEC) {
             eval_rgb_local<FAST>(K, S.chans.c, K.sun_table, wo, act, w, S.rows);
             nw = 3;
-            for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = 0.f;
+            for (int k = 0; k < 4; ++k) store_nt(0.f, lam_out + (size_t)k * lstride + i);
         } else {
             DirTerms t = dir_terms<FAST>(K, wo, act);
             add_sun_terms<FAST>(K, t);
             float lam[4];
             sample_wavelengths_one<FAST, true>(K, S.chans.c, S.sdist[0], S.sun, S.ldp, t, wls[i], lam, w);
-            for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = lam[k];
+            for (int k = 0; k < 4; ++k) store_nt(lam[k], lam_out + (size_t)k * lstride + i);
             nw = 4;
         }
         float3_ fs, ft;
         coordinate_system(dw, &fs, &ft);
         float3_ po = frame_to_world(fs, ft, dw, mk3(offx, offy, 0.f));
-        ox[i] = K.bs_center[0] + (po.x - dw.x) * K.bs_radius;
-        oy[i] = K.bs_center[1] + (po.y - dw.y) * K.bs_radius;
-        oz[i] = K.bs_center[2] + (po.z - dw.z) * K.bs_radius;
-        dxo[i] = dw.x; dyo[i] = dw.y; dzo[i] = dw.z;
+        store_nt(K.bs_center[0] + (po.x - dw.x) * K.bs_radius, ox + i);
+        store_nt(K.bs_center[1] + (po.y - dw.y) * K.bs_radius, oy + i);
+        store_nt(K.bs_center[2] + (po.z - dw.z) * K.bs_radius, oz + i);
+        store_nt(dw.x, dxo + i); store_nt(dw.y, dyo + i); store_nt(dw.z, dzo + i);
         const float inv_pd = fdiv<FAST>(1.f, pd);
         for (int k = 0; k < nw; ++k) {
             float v = FAST ? w[k] * inv_pd : w[k] / pd;
-            weight[(size_t)k * wstride + i] = isfinite(v) ? v : 0.f;
+            store_nt(isfinite(v) ? v : 0.f, weight + (size_t)k * wstride + i);
         }
     }
 }
@@ -2246,14 +2246,14 @@ __device__ __forceinline__ void sample_ray_rgb_sorted_body(
                 float3_ fs, ft;
                 coordinate_system(dw, &fs, &ft);
                 const float3_ po = frame_to_world(fs, ft, dw, mk3(offx, offy, 0.f));
-                ox[i] = K.bs_center[0] + (po.x - dw.x) * K.bs_radius;
-                oy[i] = K.bs_center[1] + (po.y - dw.y) * K.bs_radius;
-                oz[i] = K.bs_center[2] + (po.z - dw.z) * K.bs_radius;
-                dxo[i] = dw.x; dyo[i] = dw.y; dzo[i] = dw.z;
+                store_nt(K.bs_center[0] + (po.x - dw.x) * K.bs_radius, ox + i);
+                store_nt(K.bs_center[1] + (po.y - dw.y) * K.bs_radius, oy + i);
+                store_nt(K.bs_center[2] + (po.z - dw.z) * K.bs_radius, oz + i);
+                store_nt(dw.x, dxo + i); store_nt(dw.y, dyo + i); store_nt(dw.z, dzo + i);
 #pragma unroll
-                for (int k = 0; k < 4; ++k) lam_out[(size_t)k * lstride + i] = 0.f;
+                for (int k = 0; k < 4; ++k) store_nt(0.f, lam_out + (size_t)k * lstride + i);
 #pragma unroll
-                for (int k = 0; k < 3; ++k) weight[(size_t)k * wstride + i] = Y[3 + k][slot[r]];
+                for (int k = 0; k < 3; ++k) store_nt(Y[3 + k][slot[r]], weight + (size_t)k * wstride + i);
             }
         }
         wave_lds_order();

@@ -1820,8 +1820,11 @@ __device__ __forceinline__ void sample_one_rgb(const SunskyKArgs& K, const Sampl
 // sample_direction_body<FAST, false, !FULL>.
 // MODE: kSortLean (u -> d, pdf, weight), kSortFull (+ it.p, mask, ds.dist, ds.p; it.p loaded
 // before the passes) or kSortPos (Mitsuba's unmasked DirectionSample call: it.p in, ds.dist and
-// ds.p out; the LEAN passes, it.p loaded only at the store stage, so nothing extra is held
-// across the passes).
+// ds.p out).  kSortPos loads the next window's it.p with its u (its HBM latency overlaps this
+// window's passes) and gives up the hoisted sun-row reads for the 12 VGPRs (119 VGPRs, 10 SGPR
+// spills): interleaved A/B per 64M samples (profiles/r05_v4_ab_general_call_itp_prefetch.log)
+// 946 us against 1011 us with it.p read at the store stage, 1044 us with it.p read before the
+// last pass (154 VGPRs), 1028 us for the unsorted general kernel.
 constexpr int kSortLean = 0, kSortFull = 1, kSortPos = 2;
 template <bool FAST, int R, int MODE>
 __device__ __forceinline__ void sample_direction_sorted_body(
@@ -1831,15 +1834,15 @@ __device__ __forceinline__ void sample_direction_sorted_body(
     float* __restrict__ dz, float* __restrict__ pdf, float* __restrict__ dist, float* __restrict__ opx,
     float* __restrict__ opy, float* __restrict__ opz, float* __restrict__ weight, size_t wstride) {
     constexpr bool FULL = MODE == kSortFull;
+    constexpr bool POS = MODE == kSortPos;
     if constexpr (MODE == kSortLean) {
         px = py = pz = nullptr;
         dist = opx = opy = opz = nullptr;
     }
     if constexpr (!FULL) active = nullptr;
     constexpr int W = 64 * R;
-    // the LEAN / POS forms have VGPRs to spare below the 4-wave cap their LDS sets: hoist the
-    // sun-row reads
-    constexpr bool kHoist = !FULL;
+    // the LEAN form has VGPRs to spare below the 4-wave cap its LDS sets: hoist the sun-row reads
+    constexpr bool kHoist = MODE == kSortLean;
     __shared__ SamplerLds<FAST, false> S;
     __shared__ float X[SS_BLOCK / 64][7][W];
     stage_sampler_lds<FAST, false>(K, &S);
@@ -1851,6 +1854,7 @@ __device__ __forceinline__ void sample_direction_sorted_body(
     // the next window's u (FULL: and mask) is loaded before this window's passes (its HBM
     // latency overlaps them)
     float na[R], nb[R], nm[R];
+    float npx[POS ? R : 1], npy[POS ? R : 1], npz[POS ? R : 1];   // POS: the next window's it.p, loaded with its u
     auto load_window = [&](size_t w) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -1858,6 +1862,12 @@ __device__ __forceinline__ void sample_direction_sorted_body(
             na[r] = i < n ? ux[i] : 1.f;   // past the end: a sun pick, computed and not stored
             nb[r] = i < n ? uy[i] : 0.5f;
             if (FULL && active) nm[r] = (i < n && active[i] != 0) ? 1.f : 0.f;
+            if constexpr (POS) {
+                const bool in = (dist || opx) && px && i < n;
+                npx[r] = in ? px[i] : 0.f;
+                npy[r] = in ? py[i] : 0.f;
+                npz[r] = in ? pz[i] : 0.f;
+            }
         }
     };
     size_t w = (size_t)blockIdx.x * (SS_BLOCK / 64) + wv;
@@ -1865,6 +1875,7 @@ __device__ __forceinline__ void sample_direction_sorted_body(
     for (; w < nwin; w += wstep) {
         const size_t base = w * W;
         int slot[R], nsky = 0;
+        float qpx[POS ? R : 1], qpy[POS ? R : 1], qpz[POS ? R : 1];   // POS: this window's it.p
         {
             float a[R], b[R];
             uint64_t m[R];
@@ -1872,6 +1883,11 @@ __device__ __forceinline__ void sample_direction_sorted_body(
             for (int r = 0; r < R; ++r) {
                 a[r] = na[r];
                 b[r] = nb[r];
+                if constexpr (POS) {
+                    qpx[r] = npx[r];
+                    qpy[r] = npy[r];
+                    qpz[r] = npz[r];
+                }
             }
             if (w + wstep < nwin) load_window(w + wstep);
 #pragma unroll
@@ -1919,18 +1935,6 @@ __device__ __forceinline__ void sample_direction_sorted_body(
         }
         wave_lds_order();
         float* const planes[7] = {dx, dy, dz, pdf, weight, weight + wstride, weight + 2 * wstride};
-        // POS: this window's it.p, all R loads issued before the stores consume them
-        float qpx[MODE == kSortPos ? R : 1], qpy[MODE == kSortPos ? R : 1], qpz[MODE == kSortPos ? R : 1];
-        if constexpr (MODE == kSortPos) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const size_t i = base + (size_t)(r * 64 + lane);
-                const bool in = (dist || opx) && px && i < n;
-                qpx[r] = in ? px[i] : 0.f;
-                qpy[r] = in ? py[i] : 0.f;
-                qpz[r] = in ? pz[i] : 0.f;
-            }
-        }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const size_t i = base + (size_t)(r * 64 + lane);
@@ -1939,9 +1943,8 @@ __device__ __forceinline__ void sample_direction_sorted_body(
                 for (int k = 0; k < 7; ++k) store_nt(Y[k][slot[r]], planes[k] + i);
                 if (MODE != kSortLean && (dist || opx)) {   // as sample_direction_body: ds.dist, ds.p (sunsky.cpp:417-420)
                     const float3_ d = mk3(Y[0][slot[r]], Y[1][slot[r]], Y[2][slot[r]]);
-                    float3_ itp = MODE == kSortPos ? mk3(qpx[MODE == kSortPos ? r : 0], qpy[MODE == kSortPos ? r : 0],
-                                                         qpz[MODE == kSortPos ? r : 0])
-                                                   : mk3(ipx[FULL ? r : 0], ipy[FULL ? r : 0], ipz[FULL ? r : 0]);
+                    float3_ itp = POS ? mk3(qpx[POS ? r : 0], qpy[POS ? r : 0], qpz[POS ? r : 0])
+                                      : mk3(ipx[FULL ? r : 0], ipy[FULL ? r : 0], ipz[FULL ? r : 0]);
                     float3_ rel = mk3(itp.x - K.bs_center[0], itp.y - K.bs_center[1], itp.z - K.bs_center[2]);
                     float dd = 2.f * fmaxf(K.bs_radius, sqrtf(dot3(rel, rel)));
                     if (dist) store_nt(dd, dist + i);
@@ -3619,7 +3622,7 @@ SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_lean_ref, false, SS_SORT_
 SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_full_sorted_fast, true, 4, kSortFull)
 SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_full_sorted_ref, false, 4, kSortFull)
 // Mitsuba's DirectionSample call (it.p in, ds.dist / ds.p out, no mask: path.cpp:216 ->
-// scene.cpp:295-348) in the LEAN windows, it.p read at the store stage.
+// scene.cpp:295-348) in the LEAN windows, the next window's it.p prefetched with its u.
 SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_pos_sorted_fast, true, SS_SORT_R, kSortPos)
 SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_pos_sorted_ref, false, SS_SORT_R, kSortPos)
 

@@ -23,4 +23,6 @@ run pdf pdf 67108864 sunsky_pdf_direction_v4_fast && \
 run rgb rgb 16777216 sunsky_eval_rgb_v4_fast && \
 run spec spec 16777216 sunsky_eval_spec_nodes_v4_fast && \
 run rays rays 16777216 sunsky_eval_spec_rays4_v4_fast && \
-KB_SAMPLE_SPEC=1 run sample_spec sample 67108864 sunsky_sample_direction_spec_lean4_sorted_fast
+KB_SAMPLE_SPEC=1 run sample_spec sample 67108864 sunsky_sample_direction_spec_lean4_sorted_fast && \
+KB_SAMPLE_FULL=1 run sample_pos sample 67108864 sunsky_sample_direction_rgb_pos_sorted_fast && \
+run spec64 spec 67108864 sunsky_eval_spec_nodes_v4_fast

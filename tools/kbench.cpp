@@ -196,8 +196,13 @@ int main(int argc, char** argv) {
     const bool full = std::getenv("KB_SAMPLE_FULL") != nullptr;
     const float *fpx = nullptr, *fpy = nullptr, *fpz = nullptr;
     float *fdist = nullptr, *fox = nullptr, *foy = nullptr, *foz = nullptr;
-    if (full) {   // it.p: the direction buffers (any finite points do); outputs: 4 more planes
-        fpx = wz; fpy = wz; fpz = wz;
+    if (full) {   // it.p: 3 distinct planes of random points (as bench.py's general call); outputs: 4 more planes
+        std::vector<float> hp(3 * n);
+        for (auto& v : hp) v = 20.f * U(rng) - 10.f;
+        float* pin = nullptr;
+        CK(hipMalloc(&pin, 3 * n * 4));
+        CK(hipMemcpy(pin, hp.data(), 3 * n * 4, hipMemcpyHostToDevice));
+        fpx = pin; fpy = pin + n; fpz = pin + 2 * n;
         float* buf = nullptr;
         CK(hipMalloc(&buf, 4 * n * 4));
         fdist = buf; fox = buf + n; foy = buf + 2 * n; foz = buf + 3 * n;

@@ -30,6 +30,11 @@ PROBES = {
          "__device__ __forceinline__ void store_nt(float v, float* p) {\n"
          "    if (v != -1234.5f) return;\n"),
     ],
+    # the general RGB call (kSortPos) in windows of 3 / 2 x 64 samples
+    "pos_r3": [("SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_pos_sorted_fast, true, SS_SORT_R, kSortPos)",
+                "SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_pos_sorted_fast, true, 3, kSortPos)")],
+    "pos_r2": [("SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_pos_sorted_fast, true, SS_SORT_R, kSortPos)",
+                "SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_pos_sorted_fast, true, 2, kSortPos)")],
     # the C3 / C5 node kernel's grid-stride loop (the split before round 5), for A/B
     "nodes_gridstride": [
         ("""    const size_t G = (nvec + lanes - 1) / lanes;

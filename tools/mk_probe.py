@@ -35,6 +35,18 @@ PROBES = {
                 "SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_pos_sorted_fast, true, 3, kSortPos)")],
     "pos_r2": [("SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_pos_sorted_fast, true, SS_SORT_R, kSortPos)",
                 "SS_SAMPLE_DIRECTION_SORTED(sunsky_sample_direction_rgb_pos_sorted_fast, true, 2, kSortPos)")],
+    # pdf_direction with the node kernel's contiguous span per workgroup instead of its grid-stride loop
+    "pdf_span": [("""    const float3_ sn = mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]);
+    const size_t nvec = n / VEC;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+""", """    const float3_ sn = mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]);
+    const size_t nvec = n / VEC;
+    const size_t lanes_ = (size_t)gridDim.x * blockDim.x, G_ = (nvec + lanes_ - 1) / lanes_;
+    for (size_t g_ = 0; g_ < G_; ++g_) {
+        const size_t v = ((size_t)blockIdx.x * G_ + g_) * blockDim.x + threadIdx.x;
+        if (v >= nvec) break;
+""")],
     # the C3 / C5 node kernel's grid-stride loop (the split before round 5), for A/B
     "nodes_gridstride": [
         ("""    const size_t G = (nvec + lanes - 1) / lanes;

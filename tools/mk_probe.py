@@ -47,6 +47,19 @@ PROBES = {
         const size_t v = ((size_t)blockIdx.x * G_ + g_) * blockDim.x + threadIdx.x;
         if (v >= nvec) break;
 """)],
+    # cost split of the general RGB call (kSortPos): no it.p loads (it.p = 0) / no ds.dist, ds.p stores
+    "pos_noload": [("""                npx[r] = in ? px[i] : 0.f;
+                npy[r] = in ? py[i] : 0.f;
+                npz[r] = in ? pz[i] : 0.f;
+""", """                npx[r] = 0.f * (float)in;
+                npy[r] = 0.f;
+                npz[r] = 0.f;
+""")],
+    "pos_nostore": [("""                    if (dist) store_nt(dd, dist + i);
+                    if (opx) { store_nt(fmaf(d.x, dd, itp.x), opx + i); store_nt(fmaf(d.y, dd, itp.y), opy + i); store_nt(fmaf(d.z, dd, itp.z), opz + i); }
+""", """                    const float s_ = fmaf(d.x, dd, itp.x) + fmaf(d.y, dd, itp.y) + fmaf(d.z, dd, itp.z);
+                    if (dist && s_ == -1234.5f) store_nt(dd, dist + i);
+""")],
     # the C3 / C5 node kernel's grid-stride loop (the split before round 5), for A/B
     "nodes_gridstride": [
         ("""    const size_t G = (nvec + lanes - 1) / lanes;

@@ -22,6 +22,7 @@ import argparse
 import ctypes
 import json
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -752,15 +753,36 @@ def spawn_ranks(n, argv, grace_s=SPAWN_GRACE_S):
     torchrun --standalone sets).  The parent never touches the GPU: it starts the children before
     any HIP call and only waits (a process that has initialised HIP must never exec another).
     Rank 0 prints the bench line.  When a rank fails, the others get `grace_s` to finish (the
-    C5 watchdog ends a rank stuck in a collective) and are then killed.  Returns the exit code:
+    C5 watchdog ends a rank stuck in a collective) and are then killed.  A SIGTERM / SIGINT to the
+    parent is forwarded to the ranks, and a rank gets SIGTERM if the parent dies (PR_SET_PDEATHSIG),
+    so no rank outlives the launch.  Returns the exit code:
     0 when every rank exited 0, else the first failing rank's code (a signal as 128 + signo)."""
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
                 LOCAL_WORLD_SIZE=str(n))
+    def die_with_parent():   # runs in the child before exec (no GPU touched yet): SIGTERM when the parent dies
+        import ctypes as C
+        C.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)   # PR_SET_PDEATHSIG
+
     procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
-                              env=dict(base, RANK=str(r), LOCAL_RANK=str(r))) for r in range(n)]
+                              env=dict(base, RANK=str(r), LOCAL_RANK=str(r)), preexec_fn=die_with_parent)
+             for r in range(n)]
+
+    def forward(signum, _frame):   # a launcher's SIGTERM / SIGINT ends the ranks too, then the parent
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        sys.exit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, forward)
     code, failed_at = 0, None
     while True:
         for p in procs:
@@ -835,8 +857,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.launch_check:
         print(json.dumps({"plan": plan, "gpus": args.gpus, "world": world, "rank": int(os.environ.get("RANK", "0")),
-                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                          "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "pid": os.getpid(),
                           "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
+        time.sleep(float(os.environ.get("SUNSKY_BENCH_TEST_HOLD", "0")))   # tests: a rank that is still running
         return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -165,3 +165,33 @@ def test_c5_failure_on_one_rank_ends_every_rank_nonzero():
         assert line["value"] == 3.0 and "error" in line["c5_spectral_shard_gather"]
         if bad == 0:
             assert "comm setup failed" in line["c5_spectral_shard_gather"]["error"]
+
+
+def test_sigterm_to_the_spawning_parent_ends_every_rank():
+    """A launcher's timeout (SIGTERM to `bench.py --gpus N`) must not leave rank processes behind:
+    the parent forwards the signal and exits 128 + 15.  CPU: the ranks sleep in --launch-check
+    (SUNSKY_BENCH_TEST_HOLD), so they are still running when the signal comes."""
+    import signal as sg
+    import time as tm
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["SUNSKY_BENCH_TEST_HOLD"] = "60"
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check"], env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    pids = []
+    deadline = tm.time() + 120
+    while len(pids) < 2 and tm.time() < deadline:
+        line = p.stdout.readline()
+        if line.startswith("{"):
+            pids.append(json.loads(line)["pid"])
+    assert len(pids) == 2
+    p.send_signal(sg.SIGTERM)
+    assert p.wait(timeout=60) == 128 + sg.SIGTERM
+    for pid in pids:
+        for _ in range(100):
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                break
+            tm.sleep(0.1)
+        else:
+            raise AssertionError(f"rank pid {pid} outlived the parent")

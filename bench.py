@@ -1186,7 +1186,8 @@ def main():
                                                pdf_s, wgt, pdf_q, semantics=sem)
             if sem == "jit":
                 # the general call a Mitsuba integrator makes (DirectionSample3f with p and dist): it.p
-                # in, ds.p and ds.dist out as well (+28 B per sample); the unsorted general kernel
+                # in, ds.p and ds.dist out as well (+28 B per sample); the wave-sorted kSortPos kernel
+                # (the next window's it.p prefetched with its u), bitwise the unsorted general kernel
                 itp = torch.randn((3, ns), generator=g, device=dev)
                 dist_o = torch.empty(ns, dtype=torch.float32, device=dev)
                 pos_o = torch.empty((3, ns), dtype=torch.float32, device=dev)
@@ -1208,8 +1209,9 @@ def main():
                 ms_g = t_g.mean_ms()
                 sec[key]["sample_direction_general_ms"] = ms_g
                 sec[key]["sample_direction_general_note"] = (
-                    "the same samples with it.p in and ds.p, ds.dist out (64 B per sample), the unsorted general "
-                    "kernel; not part of samples_per_s")
+                    "the same samples with it.p in and ds.p, ds.dist out (64 B per sample), the wave-sorted "
+                    "kernel with it.p prefetched per window (sunsky_sample_direction_rgb_pos_sorted); not part of "
+                    "samples_per_s")
                 del itp, dist_o, pos_o
             del u, d, pdf_s, wgt, pdf_q
             if sem == "jit":

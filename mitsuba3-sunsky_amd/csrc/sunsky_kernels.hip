@@ -699,6 +699,20 @@ __device__ __forceinline__ void load_vec(const float* p, size_t i, float v[VEC])
     }
 }
 
+// Work split of the per-ray spectral eval and the node kernel: workgroup b walks the contiguous
+// span of `span_steps` steps of blockDim x VEC directions starting at step b x steps, instead of
+// a grid-stride loop.  Beyond one step per lane (batches over ~16M directions at 64 workgroups
+// per CU) each workgroup then writes contiguous 16 KB+ runs per plane: at 64M the per-ray
+// spectral eval 1.09-1.11x and the node kernel 1.05-1.09x faster, equal at 16M (interleaved
+// A/B, profiles/r05_v11_ab_span_split.log, r05_v12_ab_span_split_rays_nodes.log).  The headline
+// RGB eval keeps its grid-stride loop: in this form it measured 4 % slower at 16M (one step per
+// lane; tools/mk_probe.py rgb_span) and equal at 64M.  The step count
+// is uniform: 1 without a 64-bit division for batches the grid covers in one step.
+__device__ __forceinline__ size_t span_steps(size_t nvec) {
+    const size_t lanes = (size_t)gridDim.x * blockDim.x;
+    return nvec <= lanes ? 1 : (nvec + lanes - 1) / lanes;
+}
+
 // Outputs are written once and not re-read by this kernel: non-temporal.
 template <int VEC>
 __device__ __forceinline__ void store_vec(float* p, size_t i, const float v[VEC]) {
@@ -881,11 +895,9 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
 
 // Broadcast at exactly the 11 model wavelengths 320:40:720 nm (lerp factor 0,
 // sunsky.cpp:332-343): channel c -> plane c with compile-time channel indices.
-// Work split: workgroup b owns a contiguous span of G = ceil(n / (VEC x the grid's lanes))
-// steps of blockDim x VEC directions, walked one step (4 KB per plane per workgroup) at a
-// time, instead of a grid-stride loop.  At configs[4]'s 64M directions per GPU (G = 4) each
-// workgroup writes 16 KB contiguous per plane; at 16M (G = 1) the split is the grid-stride
-// loop's.  (tools/c5_probe.hip: 3-read / 11-write shapes at 64M, cold; A/B in DESIGN.md §3.)
+// Work split: span_steps (contiguous spans per workgroup); at configs[4]'s 64M directions per
+// GPU (4 steps) each workgroup writes 16 KB contiguous per plane (tools/c5_probe.hip: 3-read /
+// 11-write shapes at 64M, cold).
 template <int VEC, bool FAST, bool NEG>
 __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                                      const float* __restrict__ wy, const float* __restrict__ wz,
@@ -894,9 +906,7 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
     __shared__ ChanLds<FAST> S;
     const auto* chans = stage_chans<FAST>(K, &S);
     __syncthreads();
-    const size_t nvec = n / VEC;
-    const size_t lanes = (size_t)gridDim.x * blockDim.x;
-    const size_t G = (nvec + lanes - 1) / lanes;
+    const size_t nvec = n / VEC, G = span_steps(nvec);
     {
 #pragma unroll 1
       for (size_t g = 0; g < G; ++g) {
@@ -955,9 +965,10 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
     // Spectrum<Float, 4>): the chunk loop and its bounds fold away (4.4 % faster,
     // profiles/r04_v15_ab_rays_nl4.log)
     if constexpr (NL > 0) nlam = NL;
-    const size_t nvec = n / VEC;
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+    const size_t nvec = n / VEC, G = span_steps(nvec);
+    for (size_t gs = 0; gs < G; ++gs) {
+        const size_t v = ((size_t)blockIdx.x * G + gs) * blockDim.x + threadIdx.x;
+        if (v >= nvec) break;
         const size_t i = v * VEC;
         float x[VEC], y[VEC], z[VEC];
         bool m[VEC];

@@ -60,18 +60,40 @@ PROBES = {
 """, """                    const float s_ = fmaf(d.x, dd, itp.x) + fmaf(d.y, dd, itp.y) + fmaf(d.z, dd, itp.z);
                     if (dist && s_ == -1234.5f) store_nt(dd, dist + i);
 """)],
-    # the C3 / C5 node kernel's grid-stride loop (the split before round 5), for A/B
-    "nodes_gridstride": [
-        ("""    const size_t G = (nvec + lanes - 1) / lanes;
+    # the RGB eval in span_steps form (measured 4 % slower at 16M; the product keeps grid-stride)
+    "rgb_span": [("""                                              float* __restrict__ out, size_t ostride) {
+    const size_t nvec = n / VEC;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+        const size_t i = v * VEC;
+        float x[VEC], y[VEC], z[VEC], r[VEC], g[VEC], b[VEC];""", """                                              float* __restrict__ out, size_t ostride) {
+    const size_t nvec = n / VEC, G = span_steps(nvec);
+    for (size_t gs = 0; gs < G; ++gs) {
+        const size_t v = ((size_t)blockIdx.x * G + gs) * blockDim.x + threadIdx.x;
+        if (v >= nvec) break;
+        const size_t i = v * VEC;
+        float x[VEC], y[VEC], z[VEC], r[VEC], g[VEC], b[VEC];""")],
+    # the per-ray spectral eval's and the node kernel's grid-stride loops (the split before round 5), for A/B
+    "evals_gridstride": [
+        ("""    if constexpr (NL > 0) nlam = NL;
+    const size_t nvec = n / VEC, G = span_steps(nvec);
+    for (size_t gs = 0; gs < G; ++gs) {
+        const size_t v = ((size_t)blockIdx.x * G + gs) * blockDim.x + threadIdx.x;
+        if (v >= nvec) break;""",
+         """    if constexpr (NL > 0) nlam = NL;
+    const size_t nvec = n / VEC;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (size_t)gridDim.x * blockDim.x) {"""),
+        ("""    const size_t nvec = n / VEC, G = span_steps(nvec);
     {
 #pragma unroll 1
       for (size_t g = 0; g < G; ++g) {
         const size_t v = ((size_t)blockIdx.x * G + g) * blockDim.x + threadIdx.x;
-        if (v >= nvec) break;
-""", """    {
+        if (v >= nvec) break;""",
+         """    const size_t nvec = n / VEC;
+    {
 #pragma unroll 1
-      for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += lanes) {
-""")],
+      for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (size_t)gridDim.x * blockDim.x) {"""),
+    ],
 }
 
 

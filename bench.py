@@ -97,6 +97,38 @@ class KernelTimer:
         return self.mean_ms(), (float(np.median(clk)) if clk else None)
 
 
+SETTLE_MS = 60.0   # untimed launches before each secondary burst (settle())
+
+
+def settle(*steps, ms=SETTLE_MS):
+    """Untimed rounds of `steps` until `ms` of wall time has passed (at least 5 rounds), so that a
+    secondary burst measures the settled shader clock rather than the power-management transient
+    that follows a load step (returns ms per round): in a kernel trace of this bench, launches of one kernel ran 1.3-1.4x
+    longer for 5-20 ms after their burst began, then recovered (profiles/r05_v14_bench_launch_sequence.json).
+    The headline has its own --warmup steps."""
+    torch.cuda.synchronize()
+    t0, k = time.perf_counter(), 0
+    while True:
+        for _ in range(5):
+            for st in steps:
+                st()
+        k += 5
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) * 1e3
+        if el >= ms:
+            return el / k   # ms per round of `steps`
+
+
+SECONDARY_TIMED_MS = 200.0   # each secondary burst spans at least this much launch time
+
+
+def timed_reps(round_ms, base):
+    """Timed rounds for a secondary burst: `base`, or enough rounds of `round_ms` (settle()'s
+    estimate) to span SECONDARY_TIMED_MS, whichever is more -- the shader clock drifts by up to
+    ~20 % over tens of ms under sustained VALU load, and a longer burst averages over it."""
+    return max(base, int(np.ceil(SECONDARY_TIMED_MS / max(round_ms, 1e-3))))
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/rNN_*pmc_traffic.json, written by tools/gpu_pmc.sh: separate
@@ -998,10 +1030,9 @@ def main():
         # caller: 8192 x 4096 lat-long RGB bake of the sky (write-only, 12 B per pixel)
         bw, bh = 8192, 4096
         bake_out = torch.empty((3, bh, bw), dtype=torch.float32, device=dev)
-        for _ in range(5):
-            ems[0].bake_latlong(bw, bh, out=bake_out)
+        est = settle(lambda: ems[0].bake_latlong(bw, bh, out=bake_out))
         tm = KernelTimer()
-        reps = max(10, args.steps // 4)
+        reps = timed_reps(est, max(10, args.steps // 4))
         tm.begin()
         for _ in range(reps):
             ems[0].bake_latlong(bw, bh, out=bake_out)
@@ -1016,9 +1047,9 @@ def main():
         d_out = torch.ones((3, n), dtype=torch.float32, device=dev)
         si_v = ss.SurfaceInteraction3f(wi=wi)
         grad = ems[0].eval_vjp(si_v, d_out)[0]
-        ems[0].eval_vjp(si_v, d_out, grad=grad)
+        est = settle(lambda: ems[0].eval_vjp(si_v, d_out, grad=grad))
         tm = KernelTimer()
-        reps = max(10, args.steps // 4)
+        reps = timed_reps(est, max(10, args.steps // 4))
         tm.begin()
         for _ in range(reps):
             ems[0].eval_vjp(si_v, d_out, grad=grad)
@@ -1036,17 +1067,16 @@ def main():
         spec = ss.SunskyEmitter(dict(sun_dict(3.0), albedo=0.3), "spectral", precision=args.precision, device=dev)
         lams = [float(x) for x in range(320, 721, 40)]
         spec_out = torch.empty((11, n), dtype=torch.float32, device=dev)
-        for _ in range(5):
-            spec.eval_spectral_broadcast(wi, lams, out=spec_out)
+        est = settle(lambda: spec.eval_spectral_broadcast(wi, lams, out=spec_out))
         tm = KernelTimer()
-        reps = max(10, args.steps // 4)
+        reps = timed_reps(est, max(10, args.steps // 4))
         tm.begin()
         for _ in range(reps):
             spec.eval_spectral_broadcast(wi, lams, out=spec_out)
         tm.end(reps)
         ms_warm = tm.mean_ms()
         tm = KernelTimer()
-        reps_c = max(3, args.steps // 16)
+        reps_c = timed_reps(est * len(batches), max(3, args.steps // 16))
         tm.begin()
         for _ in range(reps_c):
             for b in batches:
@@ -1079,10 +1109,10 @@ def main():
             if rc:
                 raise RuntimeError(lib.sunsky_last_error().decode())
 
-        for _ in range(5):
-            rays_step()
+        est = settle(rays_step)
         tm = KernelTimer()
-        reps = max(10, args.steps // 4)
+        reps = timed_reps(est, max(10, args.steps // 4))
+        reps_c = timed_reps(est * NB, max(3, args.steps // 16))
         tm.begin()
         for _ in range(reps):
             rays_step()
@@ -1146,10 +1176,7 @@ def main():
                 if rc:
                     raise RuntimeError(lib.sunsky_last_error().decode())
 
-            for _ in range(5):
-                sample_step()
-                pdf_step()
-            reps = max(10, args.steps // 4)
+            reps = timed_reps(settle(sample_step, pdf_step), max(10, args.steps // 4))
             t_s, t_p = KernelTimer(), KernelTimer()
             cd = ClockDuring(dev)
             t_s.begin()
@@ -1200,12 +1227,12 @@ def main():
                                                      wgt.data_ptr(), ns, stream)
                     if rc:
                         raise RuntimeError(lib.sunsky_last_error().decode())
-                general_step()
+                reps_g = timed_reps(settle(general_step), reps)
                 t_g = KernelTimer()
                 t_g.begin()
-                for _ in range(reps):
+                for _ in range(reps_g):
                     general_step()
-                t_g.end(reps)
+                t_g.end(reps_g)
                 ms_g = t_g.mean_ms()
                 sec[key]["sample_direction_general_ms"] = ms_g
                 sec[key]["sample_direction_general_note"] = (
@@ -1245,9 +1272,7 @@ def main():
             if rc:
                 raise RuntimeError(lib.sunsky_last_error().decode())
 
-        for _ in range(5):
-            spec_sample_step()
-            spec_pdf_step()
+        reps = timed_reps(settle(spec_sample_step, spec_pdf_step), max(10, args.steps // 4))
         t_ss, t_sq = KernelTimer(), KernelTimer()
         cd = ClockDuring(dev)
         t_ss.begin()
@@ -1297,8 +1322,7 @@ def main():
             if rc:
                 raise RuntimeError(lib.sunsky_last_error().decode())
 
-        for _ in range(5):
-            direct_step()
+        reps = timed_reps(settle(direct_step), max(10, args.steps // 4))
         t_d = KernelTimer()
         t_d.begin()
         for _ in range(reps):
@@ -1328,8 +1352,7 @@ def main():
             if rc:
                 raise RuntimeError(lib.sunsky_last_error().decode())
 
-        for _ in range(5):
-            conductor_step()
+        reps = timed_reps(settle(conductor_step), max(10, args.steps // 4))
         t_c = KernelTimer()
         t_c.begin()
         for _ in range(reps):

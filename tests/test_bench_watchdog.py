@@ -8,6 +8,8 @@ import socket
 import subprocess
 import sys
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 _ONE = """
@@ -195,3 +197,13 @@ def test_sigterm_to_the_spawning_parent_ends_every_rank():
             tm.sleep(0.1)
         else:
             raise AssertionError(f"rank pid {pid} outlived the parent")
+
+
+def test_secondary_bursts_span_the_timed_window():
+    """Round 5: each secondary burst runs at least SECONDARY_TIMED_MS of launches (the shader clock
+    drifts over tens of ms under sustained load), never fewer than the step-derived count."""
+    bench = _bench()
+    assert bench.timed_reps(0.8, 25) == int(np.ceil(bench.SECONDARY_TIMED_MS / 0.8))
+    assert bench.timed_reps(0.8, 25) * 0.8 >= bench.SECONDARY_TIMED_MS
+    assert bench.timed_reps(100.0, 25) == 25
+    assert bench.timed_reps(0.0, 3) >= 3

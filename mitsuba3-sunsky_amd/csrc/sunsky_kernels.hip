@@ -707,7 +707,8 @@ __device__ __forceinline__ void load_vec(const float* p, size_t i, float v[VEC])
 // A/B, profiles/r05_v11_ab_span_split.log, r05_v12_ab_span_split_rays_nodes.log).  The headline
 // RGB eval keeps its grid-stride loop: in this form it measured 4 % slower at 16M (one step per
 // lane; tools/mk_probe.py rgb_span) and equal at 64M.  The step count
-// is uniform: 1 without a 64-bit division for batches the grid covers in one step.
+// is uniform: 1 without a 64-bit division for batches the grid covers in one step.  Two or
+// more steps give the one-step split's bits (tests/test_gpu_span.py).
 __device__ __forceinline__ size_t span_steps(size_t nvec) {
     const size_t lanes = (size_t)gridDim.x * blockDim.x;
     return nvec <= lanes ? 1 : (nvec + lanes - 1) / lanes;

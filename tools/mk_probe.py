@@ -60,6 +60,19 @@ PROBES = {
 """, """                    const float s_ = fmaf(d.x, dd, itp.x) + fmaf(d.y, dd, itp.y) + fmaf(d.z, dd, itp.z);
                     if (dist && s_ == -1234.5f) store_nt(dd, dist + i);
 """)],
+    # the wave-sorted RGB kernels' un-sort stores as plain stores: ds.dist / ds.p only, or all planes
+    "sorted_plain_pos": [("""                    if (dist) store_nt(dd, dist + i);
+                    if (opx) { store_nt(fmaf(d.x, dd, itp.x), opx + i); store_nt(fmaf(d.y, dd, itp.y), opy + i); store_nt(fmaf(d.z, dd, itp.z), opz + i); }
+                }""", """                    if (dist) dist[i] = dd;
+                    if (opx) { opx[i] = fmaf(d.x, dd, itp.x); opy[i] = fmaf(d.y, dd, itp.y); opz[i] = fmaf(d.z, dd, itp.z); }
+                }""")],
+    "sorted_plain_all": [("""                    if (dist) store_nt(dd, dist + i);
+                    if (opx) { store_nt(fmaf(d.x, dd, itp.x), opx + i); store_nt(fmaf(d.y, dd, itp.y), opy + i); store_nt(fmaf(d.z, dd, itp.z), opz + i); }
+                }""", """                    if (dist) dist[i] = dd;
+                    if (opx) { opx[i] = fmaf(d.x, dd, itp.x); opy[i] = fmaf(d.y, dd, itp.y); opz[i] = fmaf(d.z, dd, itp.z); }
+                }"""),
+        ("""                for (int k = 0; k < 7; ++k) store_nt(Y[k][slot[r]], planes[k] + i);""",
+         """                for (int k = 0; k < 7; ++k) planes[k][i] = Y[k][slot[r]];""")],
     # the RGB eval in span_steps form (measured 4 % slower at 16M; the product keeps grid-stride)
     "rgb_span": [("""                                              float* __restrict__ out, size_t ostride) {
     const size_t nvec = n / VEC;

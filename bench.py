@@ -618,9 +618,9 @@ def run_c5(args, world, rank, dev, coll_dev, rehearsal):
     wavelengths, the C3 node kernel), then the gather of every rank's (11, n) radiance
     planes into rank 0's (11, N) planes through the C ABI (sunsky_gather_radiance; at one
     rank the copy of the rank's own shard into the output planes).  Per-GPU eval time (max
-    over ranks), whole-job evals/s, gather time and GB/s; on rank 0 the own shard checked
-    bitwise after the gather and every rank's columns sampled against the oracle
-    (parity_c5).  Returns the report on rank 0, None elsewhere."""
+    over ranks), whole-job evals/s, gather time and GB/s; on rank 0 every rank's gathered
+    columns checked bitwise against the root's own evaluation of that rank's inputs and sampled
+    against the oracle (parity_c5).  Returns the report on rank 0, None elsewhere."""
     n5 = args.c5_dirs
     wi5 = -hemisphere_dirs(n5, seed=C5_SEED + rank, device=dev)
     spec5 = ss.SunskyEmitter(c5_scene(), "spectral", precision=args.precision, device=dev)
@@ -693,11 +693,20 @@ def run_c5(args, world, rank, dev, coll_dev, rehearsal):
             torch.cuda.synchronize()
             tcat = time.perf_counter() - t0
         del bufs, send
+    shards_ok = 0
     if rank == 0:
         # the root's own columns after the gathers, bitwise against its shard evaluated alone
         ref5 = torch.empty((11, n5), dtype=torch.float32, device=dev)
         spec5.eval_spectral_broadcast(wi5, lams, out=ref5)
         own_ok = bool(torch.equal(full[:, :n5].to(dev), ref5))
+        shards_ok = int(own_ok)
+        # the gathered planes are the one-GPU result bit for bit -- every other
+        # rank's columns against the root's own evaluation of that rank's regenerated inputs
+        for r in range(1, world):
+            wr = -hemisphere_dirs(n5, seed=C5_SEED + r, device=dev)
+            spec5.eval_spectral_broadcast(wr, lams, out=ref5)
+            shards_ok += int(torch.equal(full[:, r * n5:(r + 1) * n5].to(dev), ref5))
+            del wr
         del ref5
     del wi5
     tg = sorted(tgs)[1]
@@ -716,6 +725,7 @@ def run_c5(args, world, rank, dev, coll_dev, rehearsal):
             "gather_path": gpath,
             "gather_timing": "median of 3 gathers into preallocated buffers after one untimed call",
             "reassemble_planes_s": tcat, "end_to_end_s": te + tg + tcat, "bitwise_own_shard": own_ok,
+            "shards_bitwise_vs_one_gpu": f"{shards_ok}/{world}",
             "parity": parity,
             "note": "configs[4]: per-GPU spectral eval (weak scaling) then gather of the radiance to rank 0"}
     del full

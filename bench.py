@@ -1315,7 +1315,32 @@ def main():
         if rank == 0:
             sec["sampling_C4_spectral_4lambda"]["parity"] = parity_c4(
                 smp_sp, dict(sun_dict(3.0, eta_deg=30.0), albedo=0.3), u_sp, d_sp, p_sp, w_sp, q_sp, lam=lam_sp)
-        del u_sp, lam_sp, d_sp, p_sp, w_sp, q_sp
+        # Mitsuba's general call in the spectral variants (it.p in, ds.p and ds.dist out): the
+        # wave-sorted kernel with ds.dist / ds.p formed at the store stage
+        itp_sp = torch.randn((3, ns), generator=g_sp, device=dev)
+        dist_sp = torch.empty(ns, dtype=torch.float32, device=dev)
+        pos_sp = torch.empty((3, ns), dtype=torch.float32, device=dev)
+        psp_in = ss._capi.Vec3In(itp_sp[0].data_ptr(), itp_sp[1].data_ptr(), itp_sp[2].data_ptr())
+        psp_out = ss._capi.Vec3Out(pos_sp[0].data_ptr(), pos_sp[1].data_ptr(), pos_sp[2].data_ptr())
+
+        def spec_general_step():
+            rc = lib.sunsky_sample_direction(smp_sp._h, u_sp[0].data_ptr(), u_sp[1].data_ptr(), psp_in,
+                                             lam_sp.data_ptr(), 4, ns, None, ns, dsp_out, p_sp.data_ptr(),
+                                             dist_sp.data_ptr(), psp_out, w_sp.data_ptr(), ns, stream)
+            if rc:
+                raise RuntimeError(lib.sunsky_last_error().decode())
+
+        reps_g = timed_reps(settle(spec_general_step), max(10, args.steps // 4))
+        t_g = KernelTimer()
+        t_g.begin()
+        for _ in range(reps_g):
+            spec_general_step()
+        t_g.end(reps_g)
+        sec["sampling_C4_spectral_4lambda"]["sample_direction_general_ms"] = t_g.mean_ms()
+        sec["sampling_C4_spectral_4lambda"]["sample_direction_general_note"] = (
+            "the same samples with it.p in and ds.p, ds.dist out, the wave-sorted kernel "
+            "(sunsky_sample_direction_spec_pos_sorted); not part of samples_per_s")
+        del u_sp, lam_sp, d_sp, p_sp, w_sp, q_sp, itp_sp, dist_sp, pos_sp
         # caller (§8f row 4): direct sun+sky light at 16M diffuse points x 4 spp, emitter + BSDF
         # sampling with MIS fused in one kernel (sunsky_direct_diffuse); reads 12 B normal, writes 12 B RGB
         npts, spp = n, 4

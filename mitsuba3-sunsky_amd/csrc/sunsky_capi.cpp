@@ -107,7 +107,8 @@ enum KernelId {
     K_DIRECT_DIFFUSE_RGB, K_DIRECT_DIFFUSE_SPEC, K_SAMPLE_DIRECTION_RGB_LEAN, K_SAMPLE_DIRECTION_SPEC_LEAN,
     K_DIRECT_DIFFUSE_RAYS, K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN, K_DIRECT_CONDUCTOR_RGB, K_DIRECT_CONDUCTOR_SPEC,
     K_DIRECT_CONDUCTOR_RAYS, K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED, K_SAMPLE_RAY_RGB_SORTED,
-    K_SAMPLE_DIRECTION_RGB_FULL_SORTED, K_EVAL_SPEC_RAYS4_V4, K_DEBUG_SUN_SEGMENTS, K_SAMPLE_DIRECTION_RGB_POS_SORTED, K_COUNT
+    K_SAMPLE_DIRECTION_RGB_FULL_SORTED, K_EVAL_SPEC_RAYS4_V4, K_DEBUG_SUN_SEGMENTS, K_SAMPLE_DIRECTION_RGB_POS_SORTED,
+    K_SAMPLE_DIRECTION_SPEC_POS_SORTED, K_COUNT
 };
 const char* kKernelNames[K_COUNT] = {
     "sunsky_eval_rgb_v4", "sunsky_eval_rgb_v1", "sunsky_eval_spec_bcast_v4", "sunsky_eval_spec_bcast_v1",
@@ -120,7 +121,7 @@ const char* kKernelNames[K_COUNT] = {
     "sunsky_sample_direction_rgb_lean_plain", "sunsky_direct_conductor_rgb", "sunsky_direct_conductor_spec",
     "sunsky_direct_conductor_rays", "sunsky_sample_direction_spec_lean4_sorted", "sunsky_sample_ray_rgb_sorted",
     "sunsky_sample_direction_rgb_full_sorted", "sunsky_eval_spec_rays4_v4", "sunsky_debug_sun_segments",
-    "sunsky_sample_direction_rgb_pos_sorted"};
+    "sunsky_sample_direction_rgb_pos_sorted", "sunsky_sample_direction_spec_pos_sorted"};
 
 // eval kernels instantiated twice: eval(si) negates wi at compile time,
 // eval_direction(ds) uses ds.d as is (the "_dir" kernels)
@@ -206,6 +207,7 @@ int blocks_per_cu(KernelId k) {
         case K_SAMPLE_DIRECTION_RGB_LEAN: case K_SAMPLE_DIRECTION_SPEC_LEAN:
         case K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN: case K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED:
         case K_SAMPLE_RAY_RGB_SORTED: case K_SAMPLE_DIRECTION_RGB_FULL_SORTED: case K_SAMPLE_DIRECTION_RGB_POS_SORTED:
+        case K_SAMPLE_DIRECTION_SPEC_POS_SORTED:
             return 64;
         case K_BAKE_RGB: case K_BAKE_SPEC: return 64;
         case K_DIRECT_DIFFUSE_RGB: case K_DIRECT_DIFFUSE_SPEC: case K_DIRECT_DIFFUSE_RAYS: return 64;
@@ -992,13 +994,15 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
         // kernel (10 % slower than the unsorted one; bitwise tests only)
         const char* sgs = std::getenv("SUNSKY_AMD_SORTED_GENERAL_SAMPLING");
         const bool sorted_general = sgs && sgs[0] == '1' && !unsorted;
-        // spectral LEAN at Mitsuba's 4 wavelengths per sample: the wave-sorted kernel.  RGB
+        // spectral at Mitsuba's 4 wavelengths per sample: the wave-sorted kernel, LEAN or (no mask)
+        // with ds.dist / ds.p from it.p read at the store stage.  RGB
         // without a mask (Mitsuba's DirectionSample call: it.p in, ds.dist / ds.p out) takes the
-        // LEAN windows with it.p read at the store stage (kSortPos); with a mask, the unsorted
-        // general kernel.
+        // LEAN windows with each window's it.p loaded with its u, one window ahead (kSortPos); with
+        // a mask, the unsorted general kernel.
         const KernelId k = spec ? (lean ? (nlam == 4 && !unsorted ? K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED
                                                                   : K_SAMPLE_DIRECTION_SPEC_LEAN)
-                                        : K_SAMPLE_DIRECTION_SPEC)
+                                        : (nlam == 4 && !active && !unsorted) ? K_SAMPLE_DIRECTION_SPEC_POS_SORTED
+                                                                              : K_SAMPLE_DIRECTION_SPEC)
                                 : (lean ? (unsorted ? K_SAMPLE_DIRECTION_RGB_LEAN_PLAIN : K_SAMPLE_DIRECTION_RGB_LEAN)
                                         : sorted_general ? K_SAMPLE_DIRECTION_RGB_FULL_SORTED
                                         : (!active && !unsorted) ? K_SAMPLE_DIRECTION_RGB_POS_SORTED
@@ -1006,7 +1010,8 @@ int sunsky_sample_direction(const sunsky_emitter* e, const float* ux, const floa
         // the wave-sorted kernels: one wave takes a window of 4 (RGB) or 3 (spectral) x 64 samples
         const size_t items = (k == K_SAMPLE_DIRECTION_RGB_LEAN || k == K_SAMPLE_DIRECTION_RGB_FULL_SORTED ||
                               k == K_SAMPLE_DIRECTION_RGB_POS_SORTED) ? (n + 3) / 4
-                             : k == K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED ? (n + 2) / 3 : n;
+                             : (k == K_SAMPLE_DIRECTION_SPEC_LEAN4_SORTED || k == K_SAMPLE_DIRECTION_SPEC_POS_SORTED)
+                                   ? (n + 2) / 3 : n;
         launch(e->fn(k, (hipStream_t)stream), grid_for(e->mod, k, items), (hipStream_t)stream, args);
     });
 }

@@ -1708,11 +1708,17 @@ __device__ __forceinline__ void sample_one_spec4(const SunskyKArgs& K, const Sam
 // loads and non-temporal stores stay coalesced in sample order.  The 6 inputs (u, 4 lambda)
 // and the 8 outputs share the rows: pass p reads its columns' inputs, then writes their
 // outputs.  Each sample goes through sample_one_spec4: bitwise the unsorted kernel.
-template <bool FAST, int R>
+// POS: Mitsuba's unmasked DirectionSample call in the spectral variants (it.p in, ds.dist and ds.p
+// out, sunsky.cpp:416-428): ds.dist and ds.p are functions of d and it.p, computed at the store
+// stage from it.p read there (the windows' VGPRs and LDS are full: no prefetch); bitwise the
+// unsorted general kernel, which takes the same eval_spec4 for 4 wavelengths.
+template <bool FAST, int R, bool POS = false>
 __device__ __forceinline__ void sample_direction_spec4_sorted_body(
     const SunskyKArgs& K, const float* __restrict__ ux, const float* __restrict__ uy, const float* __restrict__ lam,
     size_t lstride, size_t n, float* __restrict__ dx, float* __restrict__ dy, float* __restrict__ dz,
-    float* __restrict__ pdf, float* __restrict__ weight, size_t wstride) {
+    float* __restrict__ pdf, float* __restrict__ weight, size_t wstride, const float* __restrict__ px = nullptr,
+    const float* __restrict__ py = nullptr, const float* __restrict__ pz = nullptr, float* __restrict__ dist = nullptr,
+    float* __restrict__ opx = nullptr, float* __restrict__ opy = nullptr, float* __restrict__ opz = nullptr) {
     constexpr int W = 64 * R;
     __shared__ SamplerLds<FAST, true> S;
     __shared__ float X[SS_BLOCK / 64][8][W];
@@ -1784,6 +1790,14 @@ __device__ __forceinline__ void sample_direction_spec4_sorted_body(
             if (i < n) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) store_nt(Y[k][slot[r]], planes[k] + i);
+                if (POS && (dist || opx)) {   // as sample_direction_body: ds.dist, ds.p
+                    const float3_ d = mk3(Y[0][slot[r]], Y[1][slot[r]], Y[2][slot[r]]);
+                    const float3_ itp = px ? mk3(px[i], py[i], pz[i]) : mk3(0.f, 0.f, 0.f);
+                    const float3_ rel = mk3(itp.x - K.bs_center[0], itp.y - K.bs_center[1], itp.z - K.bs_center[2]);
+                    const float dd = 2.f * fmaxf(K.bs_radius, sqrtf(dot3(rel, rel)));
+                    if (dist) store_nt(dd, dist + i);
+                    if (opx) { store_nt(fmaf(d.x, dd, itp.x), opx + i); store_nt(fmaf(d.y, dd, itp.y), opy + i); store_nt(fmaf(d.z, dd, itp.z), opz + i); }
+                }
             }
         }
         wave_lds_order();
@@ -3606,6 +3620,17 @@ SS_SAMPLE_DIRECTION_SPEC_LEAN(sunsky_sample_direction_spec_lean_ref, false)
     }
 SS_SAMPLE_DIRECTION_SPEC4_SORTED(sunsky_sample_direction_spec_lean4_sorted_fast, true, SS_SPEC_SORT_R)
 SS_SAMPLE_DIRECTION_SPEC4_SORTED(sunsky_sample_direction_spec_lean4_sorted_ref, false, SS_SPEC_SORT_R)
+// Mitsuba's unmasked spectral DirectionSample call (it.p in, ds.dist / ds.p out), 4 wavelengths
+#define SS_SAMPLE_DIRECTION_SPEC4_POS_SORTED(NAME, FAST, R)                                                   \
+    extern "C" __global__ __launch_bounds__(SS_BLOCK) SS_SPEC_SORTED_ATTR void NAME(                           \
+        const SunskyKArgs* __restrict__ Kp, const float* ux, const float* uy, const float* px, const float* py, const float* pz,   \
+        const float* lam, size_t lstride, int nlam, const uint8_t* active, size_t n, float* dx, float* dy,     \
+        float* dz, float* pdf, float* dist, float* opx, float* opy, float* opz, float* weight, size_t wstride) { \
+        sample_direction_spec4_sorted_body<FAST, R, true>(*Kp, ux, uy, lam, lstride, n, dx, dy, dz, pdf, weight, \
+                                                          wstride, px, py, pz, dist, opx, opy, opz);          \
+    }
+SS_SAMPLE_DIRECTION_SPEC4_POS_SORTED(sunsky_sample_direction_spec_pos_sorted_fast, true, SS_SPEC_SORT_R)
+SS_SAMPLE_DIRECTION_SPEC4_POS_SORTED(sunsky_sample_direction_spec_pos_sorted_ref, false, SS_SPEC_SORT_R)
 // the previous LEAN spectral form (wavelength loop, lambda not prefetched), for A/B timing
 SS_SAMPLE_DIRECTION(sunsky_sample_direction_spec_lean_loop_fast, true, true, true)
 

@@ -344,7 +344,9 @@ def test_spectral_sorted_kernel_bitwise_vs_unsorted(precision, monkeypatch):
     weights are bit for bit the same, and both equal the general call's (+ it.p, ds.p,
     ds.dist), for batch sizes ending inside a window, a pass or a lane, all-sky and all-sun
     windows, u.x at and next to w_sky, at 0 and 1 - ulp, out-of-range u, wavelengths at the
-    nodes, at 360 / 720 nm and outside [360, 720], and a rotated emitter."""
+    nodes, at 360 / 720 nm and outside [360, 720], and a rotated emitter.  The unmasked general
+    call (the wave-sorted kernel with ds.dist / ds.p) equals the unsorted general kernel on
+    every output."""
     d = angles_dict(3.0, 1.1, np.deg2rad(60), 0.3, 1.0, 1.0)
     d["to_world"] = np.array([[0, 0, 1, 0], [1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 0, 1]], np.float64)
     em = ss.SunskyEmitter(d, "spectral", precision=precision)
@@ -357,7 +359,7 @@ def test_spectral_sorted_kernel_bitwise_vs_unsorted(precision, monkeypatch):
 
     def run(ut, lam, p, positions):
         ds, wt = em.sample_direction(ss.Interaction3f(p=p, wavelengths=lam), ut, positions=positions)
-        return [host(x).view(np.uint32).copy() for x in [ds.d, ds.pdf, wt]]
+        return [host(x).view(np.uint32).copy() for x in [ds.d, ds.pdf, wt] + ([ds.p, ds.dist] if positions else [])]
 
     for n in (1, 5, 63, 64, 65, 191, 192, 193, 1000, 1024, 4097, 65537, (1 << 20) + 1):
         u = rng.random((n, 2), dtype=np.float32)
@@ -375,10 +377,18 @@ def test_spectral_sorted_kernel_bitwise_vs_unsorted(precision, monkeypatch):
         monkeypatch.delenv("SUNSKY_AMD_UNSORTED_SAMPLING", raising=False)
         srt = run(ut, lt, None, False)
         full = run(ut, lt, p, True)
+        origin = run(ut, lt, None, True)   # ds.dist / ds.p requested, it.p = origin
         monkeypatch.setenv("SUNSKY_AMD_UNSORTED_SAMPLING", "1")
         plain = run(ut, lt, None, False)
         for a_, b_, c_ in zip(srt, plain, full):
             assert np.array_equal(a_, b_) and np.array_equal(a_, c_), n
+        # Mitsuba's unmasked spectral DirectionSample call runs in the wave-sorted windows with
+        # ds.dist / ds.p formed at the store stage: every output, ds.p and ds.dist included, is
+        # the unsorted general kernel's (SUNSKY_AMD_UNSORTED_SAMPLING=1 selects that one)
+        for a_, b_ in zip(full, run(ut, lt, p, True)):
+            assert np.array_equal(a_, b_), n
+        for a_, b_ in zip(origin, run(ut, lt, None, True)):
+            assert np.array_equal(a_, b_), n
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)

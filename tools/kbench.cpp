@@ -228,7 +228,8 @@ int main(int argc, char** argv) {
                                    sspec ? (void*)&n : (void*)&zero, sspec ? (void*)&nl4 : (void*)&nl0, &active, &n,
                                    &dd, &ddy, &ddz, &pdf, &nullo, &nullo, &nullo, &nullo, &wgt, &n};
             // KB_SAMPLE_FULL=1: the general call, it.p in, ds.dist and ds.p out (Mitsuba's DirectionSample)
-            void* args_sample_full[] = {&K, &wx, &wy, &fpx, &fpy, &fpz, &nullf, &zero, &nl0, &active, &n,
+            void* args_sample_full[] = {&K, &wx, &wy, &fpx, &fpy, &fpz, sspec ? (void*)&lamp : (void*)&nullf,
+                                        sspec ? (void*)&n : (void*)&zero, sspec ? (void*)&nl4 : (void*)&nl0, &active, &n,
                                         &dd, &ddy, &ddz, &pdf, &fdist, &fox, &foy, &foz, &wgt, &n};
             void* args_pdf[] = {&K, &dd, &ddy, &ddz, &active, &n, &pdf};
             void* args_rays[] = {&K, &wx, &wy, &wz, &lamp, &n, &nl4, &active, &n, &out, &ostride, &sign};

@@ -73,6 +73,36 @@ PROBES = {
                 }"""),
         ("""                for (int k = 0; k < 7; ++k) store_nt(Y[k][slot[r]], planes[k] + i);""",
          """                for (int k = 0; k < 7; ++k) planes[k][i] = Y[k][slot[r]];""")],
+    # the spectral general call with it.p prefetched one window ahead (as the RGB kSortPos) instead
+    # of read at the store stage: +3 R VGPRs over the passes
+    "spec_pos_prefetch": [
+        ("""    float na[R], nb[R], nl[4][R];""",
+         """    float na[R], nb[R], nl[4][R];
+    float npx[POS ? R : 1], npy[POS ? R : 1], npz[POS ? R : 1];"""),
+        ("""            for (int k = 0; k < 4; ++k) nl[k][r] = i < n ? lam[(size_t)k * lstride + i] : 500.f;""",
+         """            for (int k = 0; k < 4; ++k) nl[k][r] = i < n ? lam[(size_t)k * lstride + i] : 500.f;
+            if constexpr (POS) {
+                const bool in = px && i < n;
+                npx[r] = in ? px[i] : 0.f;
+                npy[r] = in ? py[i] : 0.f;
+                npz[r] = in ? pz[i] : 0.f;
+            }"""),
+        ("""        const size_t base = w * W;
+        int slot[R], nsky = 0;
+        {
+            float a[R], b[R], l[4][R];""",
+         """        const size_t base = w * W;
+        int slot[R], nsky = 0;
+        float qpx[POS ? R : 1], qpy[POS ? R : 1], qpz[POS ? R : 1];
+        if constexpr (POS) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) { qpx[r] = npx[r]; qpy[r] = npy[r]; qpz[r] = npz[r]; }
+        }
+        {
+            float a[R], b[R], l[4][R];"""),
+        ("""                    const float3_ itp = px ? mk3(px[i], py[i], pz[i]) : mk3(0.f, 0.f, 0.f);""",
+         """                    const float3_ itp = mk3(qpx[POS ? r : 0], qpy[POS ? r : 0], qpz[POS ? r : 0]);"""),
+    ],
     # the RGB eval in span_steps form (measured 4 % slower at 16M; the product keeps grid-stride)
     "rgb_span": [("""                                              float* __restrict__ out, size_t ostride) {
     const size_t nvec = n / VEC;

@@ -25,4 +25,5 @@ run spec spec 16777216 sunsky_eval_spec_nodes_v4_fast && \
 run rays rays 16777216 sunsky_eval_spec_rays4_v4_fast && \
 KB_SAMPLE_SPEC=1 run sample_spec sample 67108864 sunsky_sample_direction_spec_lean4_sorted_fast && \
 KB_SAMPLE_FULL=1 run sample_pos sample 67108864 sunsky_sample_direction_rgb_pos_sorted_fast && \
-run spec64 spec 67108864 sunsky_eval_spec_nodes_v4_fast
+run spec64 spec 67108864 sunsky_eval_spec_nodes_v4_fast && \
+KB_SAMPLE_SPEC=1 KB_SAMPLE_FULL=1 run sample_spec_pos sample 67108864 sunsky_sample_direction_spec_pos_sorted_fast

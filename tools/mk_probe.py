@@ -103,6 +103,13 @@ PROBES = {
         ("""                    const float3_ itp = px ? mk3(px[i], py[i], pz[i]) : mk3(0.f, 0.f, 0.f);""",
          """                    const float3_ itp = mk3(qpx[POS ? r : 0], qpy[POS ? r : 0], qpz[POS ? r : 0]);"""),
     ],
+    # the spectral sorted passes specialised by class (as the RGB kernel's KIND 1 / 2 passes)
+    "spec_kind_passes": [
+        ("""            sample_one_spec4<FAST>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);""",
+         """            if (p * 64 + 64 <= nsky) sample_one_spec4<FAST, 1>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);
+            else if (p * 64 >= nsky) sample_one_spec4<FAST, 2>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);
+            else sample_one_spec4<FAST, 0>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);"""),
+    ],
     # the RGB eval in span_steps form (measured 4 % slower at 16M; the product keeps grid-stride)
     "rgb_span": [("""                                              float* __restrict__ out, size_t ostride) {
     const size_t nvec = n / VEC;

@@ -110,6 +110,31 @@ PROBES = {
             else if (p * 64 >= nsky) sample_one_spec4<FAST, 2>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);
             else sample_one_spec4<FAST, 0>(K, S, Y[0][q], Y[1][q], l4, inv_w, inv_w_sun, o);"""),
     ],
+    # pdf_direction with the next grid-stride step's directions loaded before this step's work
+    "pdf_prefetch": [
+        ("""    const float3_ sn = mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]);
+    const size_t nvec = n / VEC;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
+        const size_t i = v * VEC;
+        float x[VEC], y[VEC], z[VEC];
+        bool m[VEC];
+        load_dirs<VEC>(dx, dy, dz, active, i, x, y, z, m);""",
+         """    const float3_ sn = mk3(K.sun_n[0], K.sun_n[1], K.sun_n[2]);
+    const size_t nvec = n / VEC;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    float nx[VEC], ny[VEC], nz[VEC];
+    bool nm[VEC];
+    const size_t v0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v0 < nvec) load_dirs<VEC>(dx, dy, dz, active, v0 * VEC, nx, ny, nz, nm);
+    for (size_t v = v0; v < nvec; v += stride) {
+        const size_t i = v * VEC;
+        float x[VEC], y[VEC], z[VEC];
+        bool m[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) { x[j] = nx[j]; y[j] = ny[j]; z[j] = nz[j]; m[j] = nm[j]; }
+        if (v + stride < nvec) load_dirs<VEC>(dx, dy, dz, active, (v + stride) * VEC, nx, ny, nz, nm);"""),
+    ],
     # the RGB eval in span_steps form (measured 4 % slower at 16M; the product keeps grid-stride)
     "rgb_span": [("""                                              float* __restrict__ out, size_t ostride) {
     const size_t nvec = n / VEC;

@@ -135,6 +135,15 @@ PROBES = {
         for (int j = 0; j < VEC; ++j) { x[j] = nx[j]; y[j] = ny[j]; z[j] = nz[j]; m[j] = nm[j]; }
         if (v + stride < nvec) load_dirs<VEC>(dx, dy, dz, active, (v + stride) * VEC, nx, ny, nz, nm);"""),
     ],
+    # the general RGB call (kSortPos) with the hoisted sun rows, held to 4 waves/SIMD
+    "pos_hoist": [
+        ("""    constexpr bool kHoist = MODE == kSortLean;""", """    constexpr bool kHoist = MODE != kSortFull;"""),
+        ("""#ifndef SS_RGB_SORTED_ATTR   // probe builds (tools/build) set occupancy attributes here
+#define SS_RGB_SORTED_ATTR
+""", """#ifndef SS_RGB_SORTED_ATTR   // probe builds (tools/build) set occupancy attributes here
+#define SS_RGB_SORTED_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+"""),
+    ],
     # the RGB eval in span_steps form (measured 4 % slower at 16M; the product keeps grid-stride)
     "rgb_span": [("""                                              float* __restrict__ out, size_t ostride) {
     const size_t nvec = n / VEC;

@@ -298,6 +298,27 @@ class Oracle:
         if self.spectral:
             self.override_spectral_distr(em.table("spectral_pdf"))
 
+    def round_staged_tables(self):
+        """Round the staged radiance tables to fp32 (the reference's staging precision,
+        sunsky.cpp:182-195) and take the fp32 segment decision: with precision 'f64', the exact
+        value of the fp32-staged algorithm."""
+        self._fn("round_staged_tables")(self._h)
+
+    def adopt_tables(self, em):
+        """Evaluate on the product's own staged fp32 tables (sky coefficients, sky radiance,
+        sun table, limb darkening) with the fp32 segment decision: with precision 'f64', the
+        exact value of what the kernels compute, so GPU - this is the kernels' arithmetic
+        error alone.  em: a sunsky_amd emitter."""
+        t = [np.ascontiguousarray(em.table(k), dtype=np.float32)
+             for k in ("sky_params", "sky_radiance", "sun_radiance", "sun_ld")]
+        f = self._fn("adopt_tables")
+        f.argtypes = [C.c_void_p] + [C.c_void_p, C.c_size_t] * 4
+        args = []
+        for a in t:
+            args += [_ptr(a), a.size]
+        if f(self._h, *args) != 0:
+            raise ValueError(lib().oracle_last_error().decode())
+
     def hw_sun_radiance(self, turbidity, wavelength, elevation, gamma):
         return self._fn("hw_sun_radiance")(self._h, turbidity, wavelength, elevation, gamma)
 

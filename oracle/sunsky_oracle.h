@@ -110,6 +110,13 @@ void oracle_sun_coordinates(int year, int month, int day, float hour, float minu
        pdf values of sunsky.cpp:870-885) and rebuild the CDF from them (distr_1d.h:513-585);  \
        returns 0, or 1 if size is not 2..10 or a value is negative / not finite */            \
     int oracle_override_spectral_distr_##SFX(oracle_##SFX *o, const double *pdf, int size);    \
+    /* test hooks: evaluate with fp32 staged tables (the reference's staging precision,      \
+       sunsky.cpp:182-195): round this oracle's own in place, or adopt another                 \
+       implementation's (returns 1 on a size mismatch); both take the fp32 segment decision */\
+    void oracle_round_staged_tables_##SFX(oracle_##SFX *o);                                      \
+    int oracle_adopt_tables_##SFX(oracle_##SFX *o, const float *sky_params, size_t n_sky,        \
+                           const float *sky_rad, size_t n_rad, const float *sun_rad,             \
+                           size_t n_sun, const float *sun_ld, size_t n_ld);                      \
     /* HW solar radiance (restates ArHosekSkyModel.c:686-784 on the packed tables) */          \
     R oracle_hw_sun_radiance_##SFX(const oracle_##SFX *o, R turbidity, R wavelength,            \
                            R elevation, R gamma);                                                \

@@ -177,21 +177,69 @@ __global__ __launch_bounds__(256) void wr4(const float*, const float*, const flo
     }
 }
 
+// writes only, KP planes of `n` floats each at plane pitch `ostride` (VERDICT r05 next 1:
+// the same total bytes as 11 planes of the node kernel, split over 1 / 3 / 6 / 11 streams)
+template <int KP>
+__global__ __launch_bounds__(256) void wrk(const float*, const float*, const float*, float* out, size_t n,
+                                           size_t ostride) {
+    size_t nv = n / 4, stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+        f4 s = {(float)v, 1.f, 2.f, 3.f};
+#pragma unroll
+        for (int k = 0; k < KP; ++k) __builtin_nontemporal_store(s * (float)(k + 1), (f4*)(out + (size_t)k * ostride + 4 * v));
+    }
+}
+
+// full shape with the outputs interleaved [N][11]: lane's 4 directions x 11 values are 44
+// consecutive floats; store j of the wave covers f4 index (64 * 11) * wave + 64 * j + lane,
+// i.e. the wave writes 11 KB contiguously (the layout re-indexed so each store is coalesced;
+// the element order inside a direction's record is a relabelling, not a transpose)
+__global__ __launch_bounds__(256) void gs4_aos(const float* x, const float* y, const float* z, float* out, size_t n,
+                                               size_t) {
+    size_t nv = n / 4, stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+        f4 s = *(const f4*)(x + 4 * v) + *(const f4*)(y + 4 * v) + *(const f4*)(z + 4 * v);
+        const size_t wave = v / 64, lane = v % 64;
+        f4* o = (f4*)out + wave * 64 * K + lane;
+#pragma unroll
+        for (int k = 0; k < K; ++k) __builtin_nontemporal_store(s * (float)(k + 1), o + 64 * k);
+    }
+}
+
+// the node kernel's shape with NF dependent FMAs per output element (VALU work between
+// the loads and each plane's store): does the time grow as max(memory, VALU) or as their sum?
+template <int NF>
+__global__ __launch_bounds__(256) void gs4_alu(const float* x, const float* y, const float* z, float* out, size_t n,
+                                               size_t ostride) {
+    size_t nv = n / 4, stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += stride) {
+        f4 s = *(const f4*)(x + 4 * v) + *(const f4*)(y + 4 * v) + *(const f4*)(z + 4 * v);
+#pragma unroll 1
+        for (int k = 0; k < K; ++k) {
+            f4 o = s;
+#pragma unroll
+            for (int i = 0; i < NF; ++i) o = o * 1.0001f + (float)k;
+            __builtin_nontemporal_store(o, (f4*)(out + (size_t)k * ostride + 4 * v));
+        }
+    }
+}
+
 typedef void (*Kern)(const float*, const float*, const float*, float*, size_t, size_t);
 
 double run(const char* name, Kern kern, int vec, const float* x, const float* y, const float* z, float* out, size_t n,
-           int cu, double bytes_per_dir, std::vector<int> mults = {4, 8, 16, 32, 64}) {
+           int cu, double bytes_per_dir, std::vector<int> mults = {4, 8, 16, 32, 64}, size_t ostride = 0) {
+    if (ostride == 0) ostride = n;
     double best = 1e30;
     int bm = 0;
     for (int mult : mults) {
         unsigned grid = (unsigned)std::min<size_t>((n / vec + 255) / 256, (size_t)cu * mult);
-        for (int w = 0; w < 2; ++w) kern<<<grid, 256>>>(x, y, z, out, n, n);
+        for (int w = 0; w < 2; ++w) kern<<<grid, 256>>>(x, y, z, out, n, ostride);
         hipEvent_t e0, e1;
         CK(hipEventCreate(&e0));
         CK(hipEventCreate(&e1));
         const int it = 10;
         CK(hipEventRecord(e0));
-        for (int i = 0; i < it; ++i) kern<<<grid, 256>>>(x, y, z, out, n, n);
+        for (int i = 0; i < it; ++i) kern<<<grid, 256>>>(x, y, z, out, n, ostride);
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms;
@@ -207,7 +255,10 @@ double run(const char* name, Kern kern, int vec, const float* x, const float* y,
     return best;
 }
 
+int pitch_main(size_t n);
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "pitch") return pitch_main(argc > 2 ? std::strtoull(argv[2], nullptr, 0) : ((size_t)1 << 26));
     const size_t n = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : ((size_t)1 << 26);
     int cu = 0;
     CK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0));
@@ -237,5 +288,50 @@ int main(int argc, char** argv) {
     run("gs4x4_seq", gs4xg<4, true>, 16, x, y, z, out, n, cu, b);
     run("gs8", gs8, 8, x, y, z, out, n, cu, b);
     run("gs4_sync", gs4_sync, 4, x, y, z, out, n, cu, b);
+    return 0;
+}
+
+// is the 11-plane write ceiling (4.9 TB/s at 64M, pitch n = 2^28 B) a
+// property of the power-of-two plane pitch or of the stream count?  Write-only legs at
+// equal total bytes over K = 1, 3, 6, 11 planes and four pitches, then the full shapes
+// (gs4_nt, gs4x4_seq) at the same pitches and the interleaved [N][11] layout.
+int pitch_main(size_t n) {
+    int cu = 0;
+    CK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, 0));
+    const size_t pads[] = {0, 64, 1024 + 16, (2u << 20) / 4 + 4096 / 4};
+    const size_t maxpad = (2u << 20) / 4 + 4096 / 4;
+    float *x, *y, *z, *out;
+    CK(hipMalloc(&x, n * 4));
+    CK(hipMalloc(&y, n * 4));
+    CK(hipMalloc(&z, n * 4));
+    const size_t total = (size_t)K * n;   // floats written per launch
+    CK(hipMalloc(&out, (total + (size_t)K * maxpad) * 4));
+    CK(hipMemset(x, 0, n * 4));
+    CK(hipMemset(y, 0, n * 4));
+    CK(hipMemset(z, 0, n * 4));
+    printf("pitch probe: n = %zu directions, %zu floats written per launch (%.1f MB)\n", n, total, 4.0 * total / 1e6);
+    const std::vector<int> mults = {8, 16, 32, 64};
+    char name[64];
+    for (size_t pad : pads) {
+        // write-only, KP planes of total / KP floats each (rounded down to a multiple of 4)
+        const int kps[] = {1, 3, 6, 11};
+        const Kern kk[] = {wrk<1>, wrk<3>, wrk<6>, wrk<11>};
+        for (int i = 0; i < 4; ++i) {
+            const size_t len = (total / kps[i]) & ~(size_t)3;
+            snprintf(name, sizeof name, "wr_K%d_p+%zu", kps[i], pad);
+            run(name, kk[i], 4, x, y, z, out, len, cu, 4.0 * kps[i], mults, len + pad);
+        }
+        snprintf(name, sizeof name, "gs4_nt_p+%zu", pad);
+        run(name, gs<4, true>, 4, x, y, z, out, n, cu, 12.0 + 4.0 * K, mults, n + pad);
+        snprintf(name, sizeof name, "gs4x4seq_p+%zu", pad);
+        run(name, gs4xg<4, true>, 16, x, y, z, out, n, cu, 12.0 + 4.0 * K, mults, n + pad);
+    }
+    run("rd_only", rd4, 4, x, y, z, out, n, cu, 12.0, mults);
+    run("gs4_alu0", gs4_alu<0>, 4, x, y, z, out, n, cu, 12.0 + 4.0 * K, mults);
+    run("gs4_alu8", gs4_alu<8>, 4, x, y, z, out, n, cu, 12.0 + 4.0 * K, mults);
+    run("gs4_alu16", gs4_alu<16>, 4, x, y, z, out, n, cu, 12.0 + 4.0 * K, mults);
+    run("gs4_alu32", gs4_alu<32>, 4, x, y, z, out, n, cu, 12.0 + 4.0 * K, mults);
+    run("gs4_alu64", gs4_alu<64>, 4, x, y, z, out, n, cu, 12.0 + 4.0 * K, mults);
+    run("gs4_aos", gs4_aos, 4, x, y, z, out, n & ~(size_t)255, cu, 12.0 + 4.0 * K, mults);
     return 0;
 }

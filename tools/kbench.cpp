@@ -121,7 +121,9 @@ int main(int argc, char** argv) {
     }
     float *wx, *wy, *wz, *out;
     CK(hipMalloc(&wx, n * 4)); CK(hipMalloc(&wy, n * 4)); CK(hipMalloc(&wz, n * 4));
-    CK(hipMalloc(&out, n * 4 * nout));
+    // KB_OPAD=p: output planes at pitch n + p floats (eval modes; p a multiple of 4)
+    const size_t opad = std::getenv("KB_OPAD") ? std::strtoull(std::getenv("KB_OPAD"), nullptr, 10) : 0;
+    CK(hipMalloc(&out, (n + opad) * 4 * nout));
     CK(hipMemcpy(wx, hx.data(), n * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(wy, hy.data(), n * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(wz, hz.data(), n * 4, hipMemcpyHostToDevice));
@@ -133,7 +135,7 @@ int main(int argc, char** argv) {
     L.m = 11;
     for (int k = 0; k < 11; ++k) { L.lo[k] = k; L.f[k] = 0.f; }
     const uint8_t* active = nullptr;
-    size_t ostride = n;
+    size_t ostride = n + opad;
     float sign = -1.f;
     const double bytes = spec ? (12.0 + 44.0) * n : rays ? 44.0 * n : mode == "sample" ? 36.0 * n : mode == "pdf" ? 16.0 * n : 24.0 * n;
     // sampling inputs: u in [0,1)^2 (reuses wx / wy), outputs d (3 planes), pdf, RGB weight
@@ -277,7 +279,11 @@ int main(int argc, char** argv) {
                 CK(hipMemcpy(h.data() + 3 * n, pdf, n * 4, hipMemcpyDeviceToHost));
                 CK(hipMemcpy(h.data() + 4 * n, wgt, 3 * n * 4, hipMemcpyDeviceToHost));
             } else {
-                CK(hipMemcpy(h.data(), sampling && !cond ? (mode == "pdf" ? pdf : wgt) : out, h.size() * 4, hipMemcpyDeviceToHost));
+                if (opad && !(sampling && !cond))
+                    for (int c = 0; c < nout; ++c)
+                        CK(hipMemcpy(h.data() + (size_t)c * n, out + (size_t)c * ostride, n * 4, hipMemcpyDeviceToHost));
+                else
+                    CK(hipMemcpy(h.data(), sampling && !cond ? (mode == "pdf" ? pdf : wgt) : out, h.size() * 4, hipMemcpyDeviceToHost));
             }
             double maxrel = 0;
             size_t ndiff = 0;
@@ -323,6 +329,21 @@ int main(int argc, char** argv) {
                 auto median = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
                 std::printf("  A/B %-30s this %8.2f us  other(%s) %8.2f us  median(other/this) %.4f  (%d rounds x %d)\n",
                             argv[a], median(ta), bname, median(tb), median(ratio), rounds, iters);
+                if (!sampling) {   // eval modes: the two code objects' outputs, bit for bit
+                    std::vector<float> ha(h.size()), hb(h.size());
+                    auto grab = [&](hipFunction_t fn, std::vector<float>& dst) {
+                        CK(hipMemset(out, 0xFF, (n + opad) * 4 * nout));
+                        CK(hipModuleLaunchKernel(fn, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
+                        CK(hipDeviceSynchronize());
+                        for (int c = 0; c < nout; ++c)
+                            CK(hipMemcpy(dst.data() + (size_t)c * n, out + (size_t)c * ostride, n * 4, hipMemcpyDeviceToHost));
+                    };
+                    grab(f, ha);
+                    grab(fb, hb);
+                    size_t nd = 0;
+                    for (size_t q = 0; q < ha.size(); ++q) nd += std::memcmp(&ha[q], &hb[q], 4) != 0;
+                    std::printf("  A/B outputs: %zu of %zu floats differ\n", nd, ha.size());
+                }
                 std::fflush(stdout);
                 CK(hipModuleUnload(mod_b));
             }

@@ -20,6 +20,48 @@ CSRC = os.path.join(ROOT, "mitsuba3-sunsky_amd", "csrc")
 
 # name -> [(anchor, replacement)]: each anchor must occur exactly once in the product source
 PROBES = {
+    # round 6 fp64 disc fix-up variants (A/B against the product build)
+    "rgb_jbarrier": [("""            float o[3];
+            if constexpr (FAST) {
+                bool h;""", """            float o[3];
+            if constexpr (FAST) {
+                __builtin_amdgcn_sched_barrier(0);
+                bool h;""")],
+    "rays_nofix": [("""        // FAST: the disc lanes again with the fp64 disc term (fixup_rgb_disc)
+        if (FAST && any_sun) {""", """        if (false && FAST && any_sun) {""")],
+    "rays_noinline_fix": [("""        // FAST: the disc lanes again with the fp64 disc term (fixup_rgb_disc)
+        if (FAST && any_sun) {
+#pragma unroll 1
+            for (int j = 0; j < VEC; ++j) {""", """        // FAST: the disc lanes again with the fp64 disc term (fixup_rgb_disc)
+        if (FAST && any_sun) fixup_rays_noinline<VEC, FAST, NEG>(K, chans, wx, wy, wz, active, i, lam, lstride, nlam, out, ostride);
+        if (false) {
+#pragma unroll 1
+            for (int j = 0; j < VEC; ++j) {"""),
+        ("""// ======================================================================
+// eval(): spectral with per-ray wavelengths (Mitsuba Spectrum<Float, k>):""", """template <int VEC, bool FAST, bool NEG>
+__device__ __noinline__ void fixup_rays_noinline(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
+    const float* __restrict__ wx, const float* __restrict__ wy, const float* __restrict__ wz, const uint8_t* __restrict__ active,
+    size_t i, const float* __restrict__ lam, size_t lstride, int nlam, float* __restrict__ out, size_t ostride) {
+#pragma unroll 1
+    for (int j = 0; j < VEC; ++j) {
+        const size_t q = i + j;
+        const DirTerms tj = refetch_terms<NEG>(K, wx, wy, wz, active, q);
+        if (!tj.hit_sun) continue;
+        const SunDisc64 d = sun_disc64(K, tj.wx, tj.wy, tj.cos_theta);
+#pragma unroll 1
+        for (int k = 0; k < nlam; ++k)
+            out[(size_t)k * ostride + q] = eval_spec_one_flat<FAST, kSunF64>(K, chans, K.sun_table, K.sun_ld, tj,
+                                                                              lam[(size_t)k * lstride + q], &d, &K);
+    }
+}
+
+// ======================================================================
+// eval(): spectral with per-ray wavelengths (Mitsuba Spectrum<Float, k>):""")],
+    # VERDICT r05 next 1: the node kernel with the next step's directions loaded before this
+    # step's 11 stores (vmcnt counts loads and stores in order: a load issued after the stores
+    # waits for them); rolled channel loop / unrolled with a scheduling barrier per channel
+    "nodes_pf": [('    const size_t nvec = n / VEC, G = span_steps(nvec);\n    {\n#pragma unroll 1\n      for (size_t g = 0; g < G; ++g) {', '    const size_t nvec = n / VEC, G = span_steps(nvec);\n    {\n      float px_[VEC], py_[VEC], pz_[VEC];\n      bool pm_[VEC];\n#pragma unroll 1\n      for (size_t g = 0; g < G; ++g) {'), ("        const size_t v = ((size_t)blockIdx.x * G + g) * blockDim.x + threadIdx.x;\n        if (v >= nvec) break;\n        const size_t i = v * VEC;\n        float x[VEC], y[VEC], z[VEC];\n        bool m[VEC];\n        load_dirs<VEC>(wx, wy, wz, active, i, x, y, z, m);\n        DirTerms t[VEC];\n        bool any_sun = false;\n#pragma unroll\n        for (int j = 0; j < VEC; ++j) {\n            t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);\n            any_sun |= t[j].hit_sun;\n        }\n        if (any_sun) {\n#pragma unroll\n            for (int j = 0; j < VEC; ++j) add_sun_terms<FAST>(K, t[j]);\n        }\n        // Rolled: one channel's constants (LDS broadcast reads) live at a time;\n        // unrolling lets the compiler hoist all 110 out of the ray loop (184 VGPRs).\n#pragma unroll 1\n        for (int c = 0; c < kNbWavelengths; ++c) {", "        const size_t v = ((size_t)blockIdx.x * G + g) * blockDim.x + threadIdx.x;\n        if (v >= nvec) break;\n        const size_t i = v * VEC;\n        if (g == 0) load_dirs<VEC>(wx, wy, wz, active, i, px_, py_, pz_, pm_);\n        DirTerms t[VEC];\n        bool any_sun = false;\n#pragma unroll\n        for (int j = 0; j < VEC; ++j) {\n            t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(px_[j], py_[j], pz_[j])), pm_[j]);\n            any_sun |= t[j].hit_sun;\n        }\n        // the next step's directions, issued before this step's stores\n        if (g + 1 < G && v + blockDim.x < nvec) load_dirs<VEC>(wx, wy, wz, active, i + (size_t)blockDim.x * VEC, px_, py_, pz_, pm_);\n        if (any_sun) {\n#pragma unroll\n            for (int j = 0; j < VEC; ++j) add_sun_terms<FAST>(K, t[j]);\n        }\n#pragma unroll 1\n        for (int c = 0; c < kNbWavelengths; ++c) {\n            ")],
+    "nodes_pf_unroll": [('    const size_t nvec = n / VEC, G = span_steps(nvec);\n    {\n#pragma unroll 1\n      for (size_t g = 0; g < G; ++g) {', '    const size_t nvec = n / VEC, G = span_steps(nvec);\n    {\n      float px_[VEC], py_[VEC], pz_[VEC];\n      bool pm_[VEC];\n#pragma unroll 1\n      for (size_t g = 0; g < G; ++g) {'), ("        const size_t v = ((size_t)blockIdx.x * G + g) * blockDim.x + threadIdx.x;\n        if (v >= nvec) break;\n        const size_t i = v * VEC;\n        float x[VEC], y[VEC], z[VEC];\n        bool m[VEC];\n        load_dirs<VEC>(wx, wy, wz, active, i, x, y, z, m);\n        DirTerms t[VEC];\n        bool any_sun = false;\n#pragma unroll\n        for (int j = 0; j < VEC; ++j) {\n            t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);\n            any_sun |= t[j].hit_sun;\n        }\n        if (any_sun) {\n#pragma unroll\n            for (int j = 0; j < VEC; ++j) add_sun_terms<FAST>(K, t[j]);\n        }\n        // Rolled: one channel's constants (LDS broadcast reads) live at a time;\n        // unrolling lets the compiler hoist all 110 out of the ray loop (184 VGPRs).\n#pragma unroll 1\n        for (int c = 0; c < kNbWavelengths; ++c) {", "        const size_t v = ((size_t)blockIdx.x * G + g) * blockDim.x + threadIdx.x;\n        if (v >= nvec) break;\n        const size_t i = v * VEC;\n        if (g == 0) load_dirs<VEC>(wx, wy, wz, active, i, px_, py_, pz_, pm_);\n        DirTerms t[VEC];\n        bool any_sun = false;\n#pragma unroll\n        for (int j = 0; j < VEC; ++j) {\n            t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(px_[j], py_[j], pz_[j])), pm_[j]);\n            any_sun |= t[j].hit_sun;\n        }\n        // the next step's directions, issued before this step's stores\n        if (g + 1 < G && v + blockDim.x < nvec) load_dirs<VEC>(wx, wy, wz, active, i + (size_t)blockDim.x * VEC, px_, py_, pz_, pm_);\n        if (any_sun) {\n#pragma unroll\n            for (int j = 0; j < VEC; ++j) add_sun_terms<FAST>(K, t[j]);\n        }\n#pragma unroll \n        for (int c = 0; c < kNbWavelengths; ++c) {\n            __builtin_amdgcn_sched_barrier(0);")],
     # compute-only: every global store suppressed (kept live by an impossible compare), for
     # the roofline splits of DESIGN.md §3
     "nostore": [

@@ -366,7 +366,7 @@ def cpu_baseline(wi_host, budget_s=12.0):
     return out
 
 
-def lane_stats(got, a, b, sun, rtol=1e-5):
+def lane_stats(got, a, b, sun, rtol=1e-5, t=None):
     """Parity figures of tests/helpers.py, per lane population:
     sky lanes against the fp32 oracle (bound rtol|o32| + |o32 - o64|), sun-disc lanes
     against the fp64 oracle (bound rtol|o64| + k|o32 - o64|, k = SUN_SLACK), each with its worst lane
@@ -376,7 +376,13 @@ def lane_stats(got, a, b, sun, rtol=1e-5):
     rounding, or the limb's ill-conditioned cos psi) are left out of the max-rel figures; the
     mask flips among them (one side zero or > 2x the other) are counted with how many the GPU
     puts on the fp32 reference's side (its fp32 horizon / disc test; the tests require all).
-    *_over_1e-5_* count the lanes (any channel) beyond a literal 1e-5 of o32 / o64."""
+    *_over_1e-5_* count the lanes (any channel) beyond a literal 1e-5 of o32 / o64.
+    t: the fp64 evaluation of the product's own staged fp32 tables (oracle64(..., em)); with
+    it the sun lanes also carry the literal 1e-5 count against it (the FAST eval kernels'
+    own arithmetic; VERDICT r05 next 2, tests/test_gpu_disc_literal.py) and |o64 - o64t|
+    beside it (the fp32 staged state itself: tables ~1e-7, and the fp32 sun frame, which
+    an fp64 renormalisation moves by ~1e-8 -- up to ~5e-5 at the limb), and pass requires no
+    sun lane over 1e-5 of o64t."""
     got, a, b = (np.asarray(x, np.float64) for x in (got, a, b))
     den64 = np.maximum(np.abs(b), 1e-6 * np.abs(b).max())
     den32 = np.maximum(np.abs(a), 1e-6 * np.abs(a).max())
@@ -410,8 +416,17 @@ def lane_stats(got, a, b, sun, rtol=1e-5):
                      "sun_o32_lanes_over_1e-5_vs_o64": int((ra[keep] > rtol).any(axis=1).sum())},
                   sun_worst_vs_bound=float((np.abs(g - r64) / (rtol * np.abs(r64) + SUN_SLACK[0] * np.abs(r32 - r64)
                                                                   + 1e-30)).max()))
+        if t is not None:
+            rt = np.asarray(t, np.float64)[sun]
+            dt = np.maximum(np.abs(rt), 1e-30)
+            rgt = (np.abs(g - rt) / dt)[keep]
+            st.update(sun_max_rel_vs_o64t=float(rgt.max()),
+                      **{"sun_lanes_over_1e-5_vs_o64t": int((rgt > rtol).any(axis=1).sum()),
+                         "sun_o32_lanes_over_1e-5_vs_o64t": int(((np.abs(r32 - rt) / dt)[keep] > rtol).any(axis=1).sum())},
+                      sun_o64_vs_o64t_max_rel=float((np.abs(r64 - rt) / dt)[keep].max()))
     st["pass"] = (st.get("sky_worst_vs_bound", 0) <= 1 and st.get("sun_worst_vs_bound", 0) <= 1
-                  and st["mask_flip_lanes_on_o32_side"] == st["mask_flip_lanes"])
+                  and st["mask_flip_lanes_on_o32_side"] == st["mask_flip_lanes"]
+                  and st.get("sun_lanes_over_1e-5_vs_o64t", 0) == 0)
     return st
 
 
@@ -452,6 +467,22 @@ def _oracle():
     return O
 
 
+def oracle64(O, d, variant, semantics, o32, em=None):
+    """The fp64 oracle of the parity blocks, given the fp32-normalised sun direction the
+    reference and the product compute (dr::normalize, sunsky.cpp:923; tests/helpers.py
+    fp32_sun_input): from the unrounded direction the disc moves by ~1e-8 rad, which at the
+    limb moves a lane by up to ~5e-5 for any fp32 implementation.  em: also adopt that
+    emitter's staged fp32 tables (o64t, lane_stats' t)."""
+    if "sun_direction" in d:
+        d = dict(d, sun_direction=[float(x) for x in o32.info()["sun_dir_world"]])
+    if em is not None and em.info()["precision"] != "fast":
+        return None                  # the reference-precision kernels keep the fp32 disc term
+    o = O.Oracle(d, variant, semantics, "f64")
+    if em is not None:
+        o.adopt_tables(em)
+    return o
+
+
 def parity_check(ems, wi, outs, n_check=1 << 20, n_sun=1 << 14):
     """Headline parity: GPU radiance vs the oracle on the first n_check directions of
     each turbidity plus n_sun directions in and around the sun cone (the sun-disc
@@ -460,24 +491,29 @@ def parity_check(ems, wi, outs, n_check=1 << 20, n_sun=1 << 14):
     parts = []
     wi_h = wi[:, :n_check].T.cpu().numpy()
     for t, em, out in zip(TURBIDITIES, ems, outs):
-        o32, o64 = O.Oracle(sun_dict(t), "rgb", "jit", "f32"), O.Oracle(sun_dict(t), "rgb", "jit", "f64")
+        o32 = O.Oracle(sun_dict(t), "rgb", "jit", "f32")
+        o64, o64t = oracle64(O, sun_dict(t), "rgb", "jit", o32), oracle64(O, sun_dict(t), "rgb", "jit", o32, em)
         inf = o32.info()
         cone = -sun_cone_dirs(inf["sun_dir_local"], inf["cos_cutoff"], n_sun, seed=int(t))
         g_cone = em.eval(ss.SurfaceInteraction3f(wi=torch.from_numpy(cone.T.copy()).to(wi.device)))
         wi_all = np.concatenate([wi_h, cone])
         got = np.concatenate([out[:, :n_check].T.cpu().numpy(), g_cone.T.cpu().numpy()])
         sun = (-wi_all @ inf["sun_dir_local"] >= inf["cos_cutoff"]) & (wi_all[:, 2] <= 0)
-        parts.append(lane_stats(got, o32.eval(wi_all), o64.eval(wi_all), sun))
+        parts.append(lane_stats(got, o32.eval(wi_all), o64.eval(wi_all), sun,
+                                t=None if o64t is None else o64t.eval(wi_all)))
     st = merge_stats(parts)
     return dict(st, checked_dirs=(n_check + n_sun) * len(TURBIDITIES),
-                bound=f"sky: |gpu-o32| <= 1e-5|o32| + |o32-o64|; sun disc: |gpu-o64| <= 1e-5|o64| + {SUN_SLACK[0]:g}|o32-o64|")
+                bound=f"sky: |gpu-o32| <= 1e-5|o32| + |o32-o64|; sun disc: |gpu-o64| <= 1e-5|o64| + {SUN_SLACK[0]:g}|o32-o64|"
+                      "; fast: every sun-disc lane within a literal 1e-5 of o64t (the fp64 evaluation of the "
+                      "product's staged fp32 tables)")
 
 
 def parity_c3(em, d_scene, wi, out, n_check=1 << 19, n_sun=1 << 13):
     """C3 (node kernel) parity: the first n_check directions x 11 nodes plus sun-cone lanes."""
     O = _oracle()
     lams = np.arange(320, 721, 40, dtype=np.float32)
-    o32, o64 = O.Oracle(d_scene, "spectral", "jit", "f32"), O.Oracle(d_scene, "spectral", "jit", "f64")
+    o32 = O.Oracle(d_scene, "spectral", "jit", "f32")
+    o64, o64t = oracle64(O, d_scene, "spectral", "jit", o32), oracle64(O, d_scene, "spectral", "jit", o32, em)
     inf = o32.info()
     cone = -sun_cone_dirs(inf["sun_dir_local"], inf["cos_cutoff"], n_sun, seed=3)
     g_cone = em.eval_spectral_broadcast(torch.from_numpy(cone.T.copy()).to(wi.device), lams.tolist())
@@ -485,7 +521,8 @@ def parity_c3(em, d_scene, wi, out, n_check=1 << 19, n_sun=1 << 13):
     got = np.concatenate([out[:, :n_check].T.cpu().numpy(), g_cone.T.cpu().numpy()])
     lam = np.repeat(lams[:, None], wi_all.shape[0], 1)
     sun = (-wi_all @ inf["sun_dir_local"] >= inf["cos_cutoff"]) & (wi_all[:, 2] <= 0)
-    st = lane_stats(got, o32.eval(wi_all, lam).T, o64.eval(wi_all, lam).T, sun)
+    st = lane_stats(got, o32.eval(wi_all, lam).T, o64.eval(wi_all, lam).T, sun,
+                    t=None if o64t is None else o64t.eval(wi_all, lam).T)
     return dict(st, checked_dirs=wi_all.shape[0], kernel="sunsky_eval_spec_nodes_v4")
 
 
@@ -494,7 +531,8 @@ def parity_rays(em, d_scene, wi, lam, out, n_check=1 << 19, n_sun=1 << 13):
     first n_check rays with their 4 random wavelengths, plus n_sun rays in and around the sun
     cone with random wavelengths (the sun-disc lanes, against fp64)."""
     O = _oracle()
-    o32, o64 = O.Oracle(d_scene, "spectral", "jit", "f32"), O.Oracle(d_scene, "spectral", "jit", "f64")
+    o32 = O.Oracle(d_scene, "spectral", "jit", "f32")
+    o64, o64t = oracle64(O, d_scene, "spectral", "jit", o32), oracle64(O, d_scene, "spectral", "jit", o32, em)
     inf = o32.info()
     cone = -sun_cone_dirs(inf["sun_dir_local"], inf["cos_cutoff"], n_sun, seed=5)
     lam_c = np.random.default_rng(6).uniform(360, 720, (4, n_sun)).astype(np.float32)
@@ -504,7 +542,8 @@ def parity_rays(em, d_scene, wi, lam, out, n_check=1 << 19, n_sun=1 << 13):
     lam_all = np.concatenate([lam[:, :n_check].cpu().numpy(), lam_c], axis=1)
     got = np.concatenate([out[:, :n_check].T.cpu().numpy(), g_cone.T.cpu().numpy()])
     sun = (-wi_all @ inf["sun_dir_local"] >= inf["cos_cutoff"]) & (wi_all[:, 2] <= 0)
-    st = lane_stats(got, o32.eval(wi_all, lam_all).T, o64.eval(wi_all, lam_all).T, sun)
+    st = lane_stats(got, o32.eval(wi_all, lam_all).T, o64.eval(wi_all, lam_all).T, sun,
+                    t=None if o64t is None else o64t.eval(wi_all, lam_all).T)
     return dict(st, checked_rays=wi_all.shape[0], kernel="sunsky_eval_spec_rays4_v4")
 
 
@@ -514,7 +553,8 @@ def parity_c4(em, d_scene, u, d, pdf_s, wgt, pdf_q, n_check=1 << 19, semantics="
     spectral variant's (4, n) per-sample wavelengths (RGB when None)."""
     O = _oracle()
     variant = "rgb" if lam is None else "spectral"
-    o32, o64 = O.Oracle(d_scene, variant, semantics, "f32"), O.Oracle(d_scene, variant, semantics, "f64")
+    o32 = O.Oracle(d_scene, variant, semantics, "f32")
+    o64 = oracle64(O, d_scene, variant, semantics, o32)
     o32.override_w_sky(em.sky_sampling_w)
     o64.override_w_sky(em.sky_sampling_w)
     uh = u[:, :n_check].T.cpu().numpy()
@@ -582,7 +622,7 @@ def c5_scene():
     return dict(sun_dict(3.0), albedo=0.3)
 
 
-def parity_c5(planes, n5, world, dev, per_rank=1 << 14):
+def parity_c5(planes, n5, world, dev, per_rank=1 << 14, em=None):
     """configs[4] output parity on rank 0: for every rank k, a strided sample of per_rank
     directions of k's batch plus every sun-disc direction in it (regenerated here from k's
     seed), read from k's columns of the gathered (11, n5 * world) planes and compared with
@@ -590,7 +630,9 @@ def parity_c5(planes, n5, world, dev, per_rank=1 << 14):
     range or plane would fail here (the sampled columns would hold another rank's rays)."""
     O = _oracle()
     lams = np.arange(320, 721, 40, dtype=np.float32)
-    o32, o64 = O.Oracle(c5_scene(), "spectral", "jit", "f32"), O.Oracle(c5_scene(), "spectral", "jit", "f64")
+    o32 = O.Oracle(c5_scene(), "spectral", "jit", "f32")
+    o64 = oracle64(O, c5_scene(), "spectral", "jit", o32)
+    o64t = oracle64(O, c5_scene(), "spectral", "jit", o32, em) if em is not None else None
     inf = o32.info()
     s = torch.tensor(inf["sun_dir_local"], dtype=torch.float32, device=dev)
     parts, checked = [], 0
@@ -604,13 +646,14 @@ def parity_c5(planes, n5, world, dev, per_rank=1 << 14):
         del wi_k, disc
         lam = np.repeat(lams[:, None], w.shape[0], 1)
         sun = (-w @ inf["sun_dir_local"] >= inf["cos_cutoff"]) & (w[:, 2] <= 0)
-        parts.append(lane_stats(got, o32.eval(w, lam).T, o64.eval(w, lam).T, sun))
+        parts.append(lane_stats(got, o32.eval(w, lam).T, o64.eval(w, lam).T, sun,
+                                t=None if o64t is None else o64t.eval(w, lam).T))
         checked += w.shape[0]
     return dict(merge_stats(parts), checked_dirs=checked, ranks_checked=world,
                 sample=f"per rank: every {max(1, n5 // per_rank)}th direction + every sun-disc direction, "
                        "x 11 nodes, read from that rank's columns of the gathered planes",
                 bound=f"sky: |gpu-o32| <= 1e-5|o32| + |o32-o64|; sun disc: |gpu-o64| <= 1e-5|o64| + "
-                      f"{SUN_SLACK[0]:g}|o32-o64|")
+                      f"{SUN_SLACK[0]:g}|o32-o64|; fast: every sun-disc lane within a literal 1e-5 of o64t")
 
 
 def run_c5(args, world, rank, dev, coll_dev, rehearsal):
@@ -714,7 +757,7 @@ def run_c5(args, world, rank, dev, coll_dev, rehearsal):
     if rank == 0:
         del out5
         nbytes = 11 * n5 * 4 * (world - 1)
-        parity = parity_c5(full, n5, world, dev)
+        parity = parity_c5(full, n5, world, dev, em=spec5)
         report = {
             "dirs_per_gpu": n5, "lambdas": 11, "eval_s": te, "eval_kernel_ms": kernel_ms,
             "evals_per_s_whole_job": 11 * n5 * world / te,

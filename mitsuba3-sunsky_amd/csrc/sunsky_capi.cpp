@@ -226,10 +226,17 @@ unsigned grid_for(const DeviceModule* m, KernelId k, size_t work_items) {
     return (unsigned)std::max<size_t>(1, std::min(need, cap));
 }
 
-void launch(hipFunction_t f, unsigned grid, hipStream_t stream, void** args) {
-    hip_check(hipModuleLaunchKernel(f, grid, 1, 1, kBlock, 1, 1, 0, stream, args, nullptr),
+void launch(hipFunction_t f, unsigned grid, hipStream_t stream, void** args, unsigned dyn_lds = 0) {
+    hip_check(hipModuleLaunchKernel(f, grid, 1, 1, kBlock, 1, 1, dyn_lds, stream, args, nullptr),
               "hipModuleLaunchKernel");
 }
+
+// The 11-node spectral kernel with more than one step per lane (configs[4]'s 64M directions
+// per GPU): unused dynamic LDS that holds it to 5 workgroups (5 waves/SIMD) per CU.  Fewer
+// concurrent 11-plane write streams per CU write HBM faster there: 64M x 11 cold, 774 ->
+// 750 us at 5 and 745 us at 4 workgroups per CU, 806 us at 2; at one step per lane (16M)
+// neutral (profiles/r06_v8_nodes_occupancy_cold.log, r06_v7_ab_nodes_lds_cap.log).
+constexpr unsigned kNodesLdsCap = 32000;
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
@@ -946,7 +953,10 @@ int sunsky_eval_spectral_broadcast(const sunsky_emitter* e, sunsky_vec3_in w, co
         if (n4) {
             const float *x = w.x, *y = w.y, *z = w.z;
             void* args[] = {&K, &L, &x, &y, &z, &active, &n4, &out, &ostride, &sign};
-            launch(e->fn(nodes ? K_EVAL_SPEC_NODES_V4 : K_EVAL_SPEC_BCAST_V4, s), grid_for(e->mod, K_EVAL_SPEC_BCAST_V4, n4 / 4), s, args);
+            const unsigned grid = grid_for(e->mod, K_EVAL_SPEC_BCAST_V4, n4 / 4);
+            const bool multi_step = n4 / 4 > (size_t)grid * kBlock;
+            launch(e->fn(nodes ? K_EVAL_SPEC_NODES_V4 : K_EVAL_SPEC_BCAST_V4, s), grid, s, args,
+                   nodes && multi_step ? kNodesLdsCap : 0u);
         }
         if (n4 < n) {
             const float *x = w.x + n4, *y = w.y + n4, *z = w.z + n4;

@@ -371,6 +371,86 @@ __device__ __forceinline__ float fdiv(float a, float b) {
     else return a / b;
 }
 
+// The emitter state as the disc branches read it: through a pointer the compiler cannot prove
+// loop-invariant, so the branch's constant loads (segment thresholds, sun frame, ...) stay in
+// the rare branch instead of being hoisted into SGPRs held across the whole ray loop (the
+// headline kernel then spilled 19-28 SGPRs to VGPR lanes and ran 2-6 % slower).
+__device__ __forceinline__ const SunskyKArgs& opaque_kargs(const SunskyKArgs& K) {
+    int off = 0;   // a zero the compiler cannot see: the pointer stays based on K (no aliasing
+    asm volatile("" : "+s"(off));   // doubts for the main loop's scalar loads) but cannot move
+    return *(&K + off);
+}
+
+// Direction q of a fix-up: its terms from K (the main pass's constants, live in SGPRs
+// already) -- the main pass's bits, disc test included.
+// ------------------------------------------------------------------ sun disc in fp64
+// The FAST eval kernels (eval, eval_direction, the spectral broadcast / node / per-ray kernels,
+// the lat-long bake) evaluate the sun-disc term of their rare disc lanes (~1e-5 of random
+// directions) in fp64 on the fp32 inputs and staged fp32 tables: the exact value of
+// render_sun x compute_sun_ld (sunsky.cpp:572-614, 631-650) up to the tables' own rounding.
+// Near the limb cos psi = sqrt(1 - sin^2 gamma / sin^2(half aperture)) (sunsky.h:385-392)
+// has an unbounded derivative and the limb-darkening sum nearly cancels, so an fp32 Horner
+// there is off by up to 4.9e-5 (the reference's own fp32 by 1.5e-4); this branch holds the
+// literal 1e-5 against the fp64 evaluation of the staged tables
+// (tests/test_gpu_parity.py::test_fast_eval_disc_lanes_literal_bar).  The samplers keep the
+// fp32 form (65 % of their lanes are sun picks, already within 1e-5 of fp64).
+struct SunDisc64 {
+    int pos;     // render_sun's segment: the reference's fp32 decision (sun_segment_index)
+    double x;    // elevation - pi/2 (pos / 45)^3: the fp32 elevation (elevation_fast, 0.7 ulp;
+                 // x enters the polynomial smoothly), the segment start in fp64
+    double cpsi; // compute_cos_psi from the fp32 chord v = wo - n (exact next to the sun)
+};
+
+__device__ __forceinline__ SunDisc64 sun_disc64(const SunskyKArgs& K, float wx, float wy, float cos_theta) {
+    SunDisc64 d;
+    d.pos = sun_segment_index(K, cos_theta);
+    const double frac = (double)d.pos * (1.0 / (double)kNbSunSegments);
+    d.x = (double)elevation_fast(cos_theta) - 1.5707963267948966 * (frac * frac * frac);
+    const double vx = (double)(wx - K.sun_n[0]), vy = (double)(wy - K.sun_n[1]), vz = (double)(cos_theta - K.sun_n[2]);
+    const double v2 = fma(vz, vz, fma(vy, vy, vx * vx));
+    const double inv = (double)K.cpsi_inv_hi + (double)K.cpsi_inv_lo;
+    d.cpsi = sqrt(fmax(fma(-inv, v2 * fma(-0.25, v2, 1.0), 1.0), 0.0));
+    return d;
+}
+
+// RGB: sum_k x^k sum_j cos psi^j S[pos][c][k][j] (sunsky.cpp:597-611), added to the fp32 sky
+// value in fp64 and rounded once
+__device__ __forceinline__ float add_sun_rgb64(const SunskyKArgs& K, const SunDisc64& d, int c, float sky) {
+    const float* s = K.sun_table + d.pos * (3 * kNbSunCtrlPts * kNbSunLdParams) + c * (kNbSunCtrlPts * kNbSunLdParams);
+    double res = 0.0;
+#pragma unroll 1
+    for (int k = kNbSunCtrlPts - 1; k >= 0; --k) {
+        const float* r = s + k * kNbSunLdParams;
+        double inner = (double)r[kNbSunLdParams - 1];
+#pragma unroll
+        for (int j = kNbSunLdParams - 2; j >= 0; --j) inner = fma(inner, d.cpsi, (double)r[j]);
+        res = fma(res, d.x, inner);
+    }
+    return (float)fma((double)K.sun_mul, res, (double)sky);
+}
+
+// Spectral: lerp of sum_k x^k S[pos][c][k] over the channel pair (lo, lo + 1, f) times the
+// lerped limb darkening sum_j cos psi^j ld[c][j] (sunsky.cpp:341-347, 586-594, 631-650);
+// channel 11 (720 nm, weight 0) contributes 0 as in the reference's masked gather
+__device__ __forceinline__ float add_sun_spec64(const SunskyKArgs& K, const SunDisc64& d, int lo, float f, float sky) {
+    const int hi = lo + 1;
+    const double fd = (double)f;
+    auto poly = [&](int c) {
+        const float* q = K.sun_table + (d.pos * kNbWavelengths + c) * kNbSunCtrlPts;
+        return fma(fma(fma((double)q[3], d.x, (double)q[2]), d.x, (double)q[1]), d.x, (double)q[0]);
+    };
+    double sun = poly(lo);
+    if (f != 0.f) sun = fma(fd, (hi < kNbWavelengths ? poly(hi) : 0.0) - sun, sun);
+    double ld = 0.0;
+#pragma unroll 1
+    for (int j = kNbSunLdParams - 1; j >= 0; --j) {
+        double coef = (double)K.sun_ld[lo * kNbSunLdParams + j];
+        if (f != 0.f) coef = fma(fd, (hi < kNbWavelengths ? (double)K.sun_ld[hi * kNbSunLdParams + j] : 0.0) - coef, coef);
+        ld = fma(ld, d.cpsi, coef);
+    }
+    return (float)fma((double)K.sun_mul, sun * ld, (double)sky);
+}
+
 // render_sky (sunsky.cpp:538-555) with the output scale folded in (FastChannel)
 __device__ __forceinline__ float sky_fast(const FastChannel& k, const DirTerms& t) {
     float c1 = fmaf(k.A, fast_exp2(k.Bl2 * t.r), 1.f);
@@ -529,15 +609,29 @@ __device__ __forceinline__ void render_sun_rgb_rows(const SunRowsRgb& R, int row
 // Full RGB eval for one local direction (sunsky.cpp:317-323).
 // chans: the 3 channels (K.fsky / K.sky, or an LDS copy in the sampling kernels,
 // whose other constants already fill the SGPR file).
-template <bool FAST, bool HOIST = false>
+// SUN (FAST only): kSunF32 the fp32 disc term (the samplers and callers), kSunF64 the fp64
+// disc term (the eval kernels: eval, eval_direction, the bake), kSunNone none (*hit reports
+// the disc test).
+enum { kSunF32 = 0, kSunF64 = 1, kSunNone = 2 };
+
+template <bool FAST, bool HOIST = false, int SUN = kSunF32>
 __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
                                                const float* sun_tab, float3_ wo, bool mask, float out[3],
-                                               const SunRowsRgb* rows = nullptr) {
+                                               const SunRowsRgb* rows = nullptr, bool* hit = nullptr) {
     DirTerms t = dir_terms<FAST>(K, wo, mask);
     if constexpr (FAST) {
 #pragma unroll
         for (int c = 0; c < 3; ++c) out[c] = sky_fast(chans[c], t);   // sky_scale and CIE folded
-        if (t.hit_sun) {
+        if (hit) *hit = t.hit_sun;
+        if constexpr (SUN == kSunNone) {
+        } else if constexpr (SUN == kSunF64) {
+            if (t.hit_sun) {
+                const SunskyKArgs& Kf = opaque_kargs(K);   // the disc constants loaded in the branch
+                const SunDisc64 d = sun_disc64(Kf, t.wx, t.wy, t.cos_theta);
+#pragma unroll 1
+                for (int c = 0; c < 3; ++c) out[c] = add_sun_rgb64(Kf, d, c, out[c]);
+            }
+        } else if (t.hit_sun) {
             add_sun_terms<true>(K, t);
             const int row = t.sun_pos - K.sun_row_lo;
             if (rows && row >= 0 && row < kSunRowsLds) {
@@ -571,10 +665,10 @@ __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const typen
     }
 }
 
-template <bool FAST>
+template <bool FAST, int SUN = kSunF32>
 __device__ __forceinline__ void eval_rgb_local(const SunskyKArgs& K, const float* sun_tab, float3_ wo, bool mask,
-                                               float out[3]) {
-    eval_rgb_local<FAST>(K, chan_table<FAST>(K), sun_tab, wo, mask, out);
+                                               float out[3], bool* hit = nullptr) {
+    eval_rgb_local<FAST, false, SUN>(K, chan_table<FAST>(K), sun_tab, wo, mask, out, nullptr, hit);
 }
 
 // Powers of the sun disc's polynomial variables, shared by every wavelength of a lane:
@@ -649,6 +743,19 @@ __device__ __forceinline__ float sun_spec_term(const SunskyKArgs& K, const float
     return FAST ? K.sun_mul * (sun * ld) : K.sun_scale * sun * ld * K.area_ratio;
 }
 
+// The eval kernels' spectral disc term of one direction for channel pair (lo, lo + 1, f),
+// added to its sky value o: FAST in fp64 (SunDisc64, its constants loaded in the branch),
+// the reference kernels in fp32 from add_sun_terms().
+template <bool FAST>
+__device__ __forceinline__ float spec_disc_add(const SunskyKArgs& K, const DirTerms& t, int lo, float f, float o) {
+    if constexpr (FAST) {
+        const SunskyKArgs& Kf = opaque_kargs(K);
+        return add_sun_spec64(Kf, sun_disc64(Kf, t.wx, t.wy, t.cos_theta), lo, f, o);
+    } else {
+        return o + sun_spec_term<false>(K, K.sun_table, K.sun_ld, t, lo, f);
+    }
+}
+
 // Spectral eval of one per-lane wavelength (sunsky.cpp:325-348); `chans` is
 // indexed by a per-lane channel, so it lives in LDS.  `t` carries add_sun_terms().
 template <bool FAST>
@@ -671,7 +778,9 @@ __device__ __forceinline__ float eval_spec_one(const SunskyKArgs& K, const typen
 // with lo <= 9 and f in [0, 1], both sky evaluations always, as eval_spec4 does -- lerpf_
 // returns its operands exactly at f = 0 and f = 1, so a node and 720 nm give eval_spec_one's
 // bits -- and the sun term in the one rare branch with eval_spec_one's own (lo, f).
-template <bool FAST>
+// SUN as eval_rgb_local's: kSunF32 (t carries add_sun_terms), kSunF64 (the eval kernels' fp64
+// disc term, spec_disc_add), kSunNone (no disc term).
+template <bool FAST, int SUN = kSunF32>
 __device__ __forceinline__ float eval_spec_one_flat(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
                                                     const float* sun_tab, const float* ld_tab, const DirTerms& t,
                                                     float lambda) {
@@ -681,7 +790,11 @@ __device__ __forceinline__ float eval_spec_one_flat(const SunskyKArgs& K, const 
     const int lo = c < kNbWavelengths - 2 ? c : kNbWavelengths - 2;
     const float f = ok ? nw - (float)lo : 0.f;
     float res = lerpf_(sky_eval<FAST>(chans[lo], t, K.sky_scale), sky_eval<FAST>(chans[lo + 1], t, K.sky_scale), f);
-    if (t.hit_sun && ok) res += sun_spec_term<FAST>(K, sun_tab, ld_tab, t, c, nw - (float)c);
+    if constexpr (SUN == kSunF64) {
+        if (t.hit_sun && ok) res = spec_disc_add<true>(K, t, c, nw - (float)c, res);
+    } else if constexpr (SUN == kSunF32) {
+        if (t.hit_sun && ok) res += sun_spec_term<FAST>(K, sun_tab, ld_tab, t, c, nw - (float)c);
+    }
     return ok ? res : 0.f;
 }
 
@@ -781,7 +894,8 @@ __device__ __forceinline__ void eval_rgb_body(const SunskyKArgs& K, const float*
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
             float o[3];
-            eval_rgb_local<FAST>(K, K.sun_table, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j], o);
+            // FAST: the disc term in fp64 (SunDisc64)
+            eval_rgb_local<FAST, FAST ? kSunF64 : kSunF32>(K, K.sun_table, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j], o);
             r[j] = o[0]; g[j] = o[1]; b[j] = o[2];
         }
         store_vec<VEC>(out, i, r);
@@ -834,6 +948,42 @@ struct LambdaSet {
     float f[kMaxBroadcastLambda];   // < 0: invalid wavelength (output 0)
 };
 
+// The broadcast / node kernels' FAST disc lanes: in line in their channel loops the fp64 term
+// (four copies, one per direction of a lane) held them to 5-6 waves/SIMD (86 / 80 VGPRs), so a
+// lane that met a disc direction walks its steps again after the main loop instead: each
+// direction re-read (with its mask byte), its terms and disc test recomputed by the same code
+// (the main pass's bits), and for the disc ones each wavelength's sky value as the main pass
+// computes it plus the fp64 term stored over the main pass's value (which had none).  The
+// re-reads are issued after the main stores, so their waits order those before the overwrite.
+// Broadcast list L (lerp factor f < 0: an invalid wavelength, left 0), or the 11 nodes (NODES:
+// channel c, f = 0).  The constants come through opaque_kargs, so nothing of this is hoisted
+// into registers held across the main loop.
+template <int VEC, bool NEG, bool NODES>
+__device__ __forceinline__ void fixup_spec_disc(const SunskyKArgs& K, const FastChannel* chans, const LambdaSet& L,
+                                                const float* __restrict__ wx, const float* __restrict__ wy,
+                                                const float* __restrict__ wz, const uint8_t* __restrict__ active,
+                                                size_t i, float* __restrict__ out, size_t ostride) {
+#pragma unroll 1
+    for (int j = 0; j < VEC; ++j) {
+        const SunskyKArgs& Kf = opaque_kargs(K);
+        const size_t q = i + j;
+        const bool mq = !active || active[q] != 0;
+        const DirTerms tj = dir_terms<true>(Kf, to_local(Kf, flip3<NEG>(wx[q], wy[q], wz[q])), mq);
+        if (!tj.hit_sun) continue;
+        const SunDisc64 d = sun_disc64(Kf, tj.wx, tj.wy, tj.cos_theta);
+        const int m = NODES ? kNbWavelengths : L.m;
+#pragma unroll 1
+        for (int k = 0; k < m; ++k) {
+            const int lo = NODES ? k : L.lo[k];
+            const float f = NODES ? 0.f : L.f[k];
+            if (f < 0.f) continue;
+            float o = sky_eval<true>(chans[lo], tj, Kf.sky_scale);
+            if (f != 0.f) o = lerpf_(o, lo + 1 < kNbWavelengths ? sky_eval<true>(chans[lo + 1], tj, Kf.sky_scale) : 0.f, f);
+            out[(size_t)k * ostride + q] = add_sun_spec64(Kf, d, lo, f, o);
+        }
+    }
+}
+
 template <int VEC, bool FAST, bool NEG>
 __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const LambdaSet& L,
                                                      const float* __restrict__ wx, const float* __restrict__ wy,
@@ -844,6 +994,7 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
     __syncthreads();
     const size_t nvec = n / VEC;
     const size_t stride = (size_t)gridDim.x * blockDim.x;
+    bool had_sun = false;
     for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride) {
         const size_t i = v * VEC;
         float x[VEC], y[VEC], z[VEC];
@@ -856,7 +1007,7 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
             t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);
             any_sun |= t[j].hit_sun;
         }
-        if (any_sun) {
+        if (!FAST && any_sun) {
 #pragma unroll
             for (int j = 0; j < VEC; ++j) add_sun_terms<FAST>(K, t[j]);
         }
@@ -881,15 +1032,23 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
                         for (int j = 0; j < VEC; ++j) o[j] = lerpf_(o[j], 0.f, f);
                     }
                 }
-                if (any_sun) {
+                if (!FAST && any_sun) {
 #pragma unroll
                     for (int j = 0; j < VEC; ++j)
-                        if (t[j].hit_sun) o[j] += sun_spec_term<FAST>(K, K.sun_table, K.sun_ld, t[j], lo, f);
+                        if (t[j].hit_sun) o[j] = spec_disc_add<FAST>(K, t[j], lo, f, o[j]);
                 }
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) o[j] = t[j].active ? o[j] : 0.f;
             }
             store_vec<VEC>(out + (size_t)k * ostride, i, o);
+        }
+        had_sun |= any_sun;
+    }
+    if constexpr (FAST) {   // the disc lanes (fixup_spec_disc)
+        if (had_sun) {
+#pragma unroll 1
+            for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += stride)
+                fixup_spec_disc<VEC, NEG, false>(K, chans, L, wx, wy, wz, active, v * VEC, out, ostride);
         }
     }
 }
@@ -898,7 +1057,10 @@ __device__ __forceinline__ void eval_spec_bcast_body(const SunskyKArgs& K, const
 // sunsky.cpp:332-343): channel c -> plane c with compile-time channel indices.
 // Work split: span_steps (contiguous spans per workgroup); at configs[4]'s 64M directions per
 // GPU (4 steps) each workgroup writes 16 KB contiguous per plane (tools/c5_probe.hip: 3-read /
-// 11-write shapes at 64M, cold).
+// 11-write shapes at 64M, cold).  Loading the next step's directions before this step's 11
+// stores (through LDS with a counted vmcnt, so the wave does not wait for its own stores)
+// measured 1.4 % faster at 64M and 3.6 % slower at 16M (one step per lane): not kept
+// (DESIGN.md §3).
 template <int VEC, bool FAST, bool NEG>
 __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const float* __restrict__ wx,
                                                      const float* __restrict__ wy, const float* __restrict__ wz,
@@ -908,6 +1070,7 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
     const auto* chans = stage_chans<FAST>(K, &S);
     __syncthreads();
     const size_t nvec = n / VEC, G = span_steps(nvec);
+    bool had_sun = false;
     {
 #pragma unroll 1
       for (size_t g = 0; g < G; ++g) {
@@ -924,7 +1087,7 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
             t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);
             any_sun |= t[j].hit_sun;
         }
-        if (any_sun) {
+        if (!FAST && any_sun) {
 #pragma unroll
             for (int j = 0; j < VEC; ++j) add_sun_terms<FAST>(K, t[j]);
         }
@@ -936,16 +1099,28 @@ __device__ __forceinline__ void eval_spec_nodes_body(const SunskyKArgs& K, const
             float o[VEC];
 #pragma unroll
             for (int j = 0; j < VEC; ++j) o[j] = sky_eval<FAST>(ch, t[j], K.sky_scale);
-            if (any_sun) {
+            if (!FAST && any_sun) {
 #pragma unroll
                 for (int j = 0; j < VEC; ++j)
-                    if (t[j].hit_sun) o[j] += sun_spec_term<FAST>(K, K.sun_table, K.sun_ld, t[j], c, 0.f);
+                    if (t[j].hit_sun) o[j] = spec_disc_add<FAST>(K, t[j], c, 0.f, o[j]);
             }
 #pragma unroll
             for (int j = 0; j < VEC; ++j) o[j] = t[j].active ? o[j] : 0.f;
             store_vec<VEC>(out + (size_t)c * ostride, i, o);
         }
+        had_sun |= any_sun;
       }
+    }
+    if constexpr (FAST) {   // the disc lanes (fixup_spec_disc)
+        if (had_sun) {
+            const LambdaSet none = {};
+#pragma unroll 1
+            for (size_t g = 0; g < G; ++g) {
+                const size_t v = ((size_t)blockIdx.x * G + g) * blockDim.x + threadIdx.x;
+                if (v >= nvec) break;
+                fixup_spec_disc<VEC, NEG, true>(K, chans, none, wx, wy, wz, active, v * VEC, out, ostride);
+            }
+        }
     }
 }
 
@@ -984,7 +1159,7 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
             t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);
-            add_sun_terms<FAST>(K, t[j]);
+            if constexpr (!FAST) add_sun_terms<FAST>(K, t[j]);
         }
         for (int k0 = 0; k0 < nlam; k0 += 4) {
             if (k0 > 0) {
@@ -998,7 +1173,7 @@ __device__ __forceinline__ void eval_spec_rays_body(const SunskyKArgs& K, const 
                 float o[VEC];
 #pragma unroll
                 for (int j = 0; j < VEC; ++j)
-                    o[j] = eval_spec_one_flat<FAST>(K, chans, K.sun_table, K.sun_ld, t[j], l4[k][j]);
+                    o[j] = eval_spec_one_flat<FAST, FAST ? kSunF64 : kSunF32>(K, chans, K.sun_table, K.sun_ld, t[j], l4[k][j]);
                 store_vec<VEC>(out + (size_t)(k0 + k) * ostride, i, o);
             }
         }
@@ -2976,7 +3151,7 @@ __device__ __forceinline__ void bake_rgb_body(const SunskyKArgs& K, LatLong G, f
             const unsigned x = x0 + j < (unsigned)G.w ? x0 + j : (unsigned)G.w - 1;
             float3_ d = mk3(G.tab[x] * st, G.tab[G.w + x] * st, ct);
             float o[3];
-            eval_rgb_local<FAST>(K, K.sun_table, to_local(K, d), true, o);
+            eval_rgb_local<FAST, FAST ? kSunF64 : kSunF32>(K, K.sun_table, to_local(K, d), true, o);
             r[j] = o[0]; g[j] = o[1]; b[j] = o[2];
         }
         if (vec_ok) {
@@ -3003,7 +3178,7 @@ __device__ __forceinline__ void bake_spec_body(const SunskyKArgs& K, LatLong G, 
     const size_t stride = (size_t)gridDim.x * blockDim.x;
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         DirTerms t = dir_terms<FAST>(K, to_local(K, latlong_dir(G, i)), true);
-        add_sun_terms<FAST>(K, t);
+        if constexpr (!FAST) add_sun_terms<FAST>(K, t);
         for (int k = 0; k < L.m; ++k) {
             const int lo = L.lo[k];
             const float f = L.f[k];
@@ -3011,7 +3186,7 @@ __device__ __forceinline__ void bake_spec_body(const SunskyKArgs& K, LatLong G, 
             if (f >= 0.f && t.active) {
                 o = sky_eval<FAST>(chans[lo], t, K.sky_scale);
                 if (f != 0.f) o = lerpf_(o, lo + 1 < kNbWavelengths ? sky_eval<FAST>(chans[lo + 1], t, K.sky_scale) : 0.f, f);
-                if (t.hit_sun) o += sun_spec_term<FAST>(K, K.sun_table, K.sun_ld, t, lo, f);
+                if (t.hit_sun) o = spec_disc_add<FAST>(K, t, lo, f, o);
             }
             __builtin_nontemporal_store(o, out + (size_t)k * ostride + i);
         }

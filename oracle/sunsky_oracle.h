@@ -112,11 +112,13 @@ void oracle_sun_coordinates(int year, int month, int day, float hour, float minu
     int oracle_override_spectral_distr_##SFX(oracle_##SFX *o, const double *pdf, int size);    \
     /* test hooks: evaluate with fp32 staged tables (the reference's staging precision,      \
        sunsky.cpp:182-195): round this oracle's own in place, or adopt another                 \
-       implementation's (returns 1 on a size mismatch); both take the fp32 segment decision */\
+       implementation's with its fp32 local sun direction and disc cutoff (returns 1 on a size \
+       mismatch); both take the fp32 segment decision */\
     void oracle_round_staged_tables_##SFX(oracle_##SFX *o);                                      \
     int oracle_adopt_tables_##SFX(oracle_##SFX *o, const float *sky_params, size_t n_sky,        \
                            const float *sky_rad, size_t n_rad, const float *sun_rad,             \
-                           size_t n_sun, const float *sun_ld, size_t n_ld);                      \
+                           size_t n_sun, const float *sun_ld, size_t n_ld,                       \
+                           const float *sun_local /* NULL: keep */, float cos_cutoff);          \
     /* HW solar radiance (restates ArHosekSkyModel.c:686-784 on the packed tables) */          \
     R oracle_hw_sun_radiance_##SFX(const oracle_##SFX *o, R turbidity, R wavelength,            \
                            R elevation, R gamma);                                                \

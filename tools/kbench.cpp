@@ -256,13 +256,15 @@ int main(int argc, char** argv) {
                                             : mode == "sample" ? (full ? args_sample_full : args_sample)
                                             : mode == "pdf" ? args_pdf : mode == "diffuse" ? args_diff
                                             : cond ? args_cond : args_rgb;
-            for (int w = 0; w < 3; ++w) CK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
+            // KB_LDS: dynamic LDS bytes per workgroup in the timed loop (an occupancy cap)
+            const unsigned kb_lds = std::getenv("KB_LDS") ? std::atoi(std::getenv("KB_LDS")) : 0;
+            for (int w = 0; w < 3; ++w) CK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, kb_lds, nullptr, args, nullptr));
             hipEvent_t e0, e1;
             CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
             CK(hipEventRecord(e0, nullptr));
             for (int it = 0; it < iters; ++it) {
                 if (cold > 1) { wx = cx[it % cold]; wy = cy[it % cold]; wz = cz[it % cold]; }
-                CK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
+                CK(hipModuleLaunchKernel(f, grid, 1, 1, 256, 1, 1, kb_lds, nullptr, args, nullptr));
             }
             wx = cx[0]; wy = cy[0]; wz = cz[0];
             CK(hipEventRecord(e1, nullptr));
@@ -294,6 +296,7 @@ int main(int argc, char** argv) {
                     double d = std::fabs((double)h[i] - ref[i]) / std::max(1e-6, std::fabs((double)ref[i]));
                     if (d > maxrel) maxrel = d;
                 }
+            if (kb_lds) std::printf("[lds %u] ", kb_lds);
             std::printf("%-36s bpcu=%-4d grid=%-6u %9.2f us  %7.1f GB/s  %.3e evals/s  maxrel-vs-first=%.2e  "
                         "bitdiff=%zu\n",
                         argv[a], mult, grid, us, bytes / (us * 1e-6) / 1e9, (spec ? 11.0 : 1.0) * n / (us * 1e-6),
@@ -311,10 +314,15 @@ int main(int argc, char** argv) {
                 CK(hipModuleGetFunction(&fb, mod_b, bname));
                 const int rounds = std::getenv("KB_AB_ROUNDS") ? std::atoi(std::getenv("KB_AB_ROUNDS")) : 20;
                 std::vector<double> ta, tb, ratio;
+                // KB_AB_LDS_A / KB_AB_LDS_B: dynamic LDS bytes per workgroup for this / the other
+                // side (an occupancy cap without a code change)
+                const unsigned lds_a = std::getenv("KB_AB_LDS_A") ? std::atoi(std::getenv("KB_AB_LDS_A")) : 0;
+                const unsigned lds_b = std::getenv("KB_AB_LDS_B") ? std::atoi(std::getenv("KB_AB_LDS_B")) : 0;
                 auto burst = [&](hipFunction_t fn) {
+                    const unsigned lds = fn == f ? lds_a : lds_b;
                     CK(hipEventRecord(e0, nullptr));
                     for (int it = 0; it < iters; ++it)
-                        CK(hipModuleLaunchKernel(fn, grid, 1, 1, 256, 1, 1, 0, nullptr, args, nullptr));
+                        CK(hipModuleLaunchKernel(fn, grid, 1, 1, 256, 1, 1, lds, nullptr, args, nullptr));
                     CK(hipEventRecord(e1, nullptr));
                     CK(hipEventSynchronize(e1));
                     float t = 0;

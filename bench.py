@@ -661,9 +661,11 @@ def run_c5(args, world, rank, dev, coll_dev, rehearsal):
     wavelengths, the C3 node kernel), then the gather of every rank's (11, n) radiance
     planes into rank 0's (11, N) planes through the C ABI (sunsky_gather_radiance; at one
     rank the copy of the rank's own shard into the output planes).  Per-GPU eval time (max
-    over ranks), whole-job evals/s, gather time and GB/s; on rank 0 every rank's gathered
-    columns checked bitwise against the root's own evaluation of that rank's inputs and sampled
-    against the oracle (parity_c5).  Returns the report on rank 0, None elsewhere."""
+    over ranks), whole-job evals/s, gather time and GB/s.  Returns rank 0's state for
+    finish_c5 (None elsewhere), which checks every rank's gathered columns bitwise against the
+    root's own evaluation of that rank's inputs and samples them against the oracle -- after
+    the teardown collectives: the other ranks do not wait through rank 0's serial
+    re-evaluations and CPU parity, so no deadline has to cover them."""
     n5 = args.c5_dirs
     wi5 = -hemisphere_dirs(n5, seed=C5_SEED + rank, device=dev)
     spec5 = ss.SunskyEmitter(c5_scene(), "spectral", precision=args.precision, device=dev)
@@ -736,42 +738,57 @@ def run_c5(args, world, rank, dev, coll_dev, rehearsal):
             torch.cuda.synchronize()
             tcat = time.perf_counter() - t0
         del bufs, send
-    shards_ok = 0
-    if rank == 0:
-        # the root's own columns after the gathers, bitwise against its shard evaluated alone
-        ref5 = torch.empty((11, n5), dtype=torch.float32, device=dev)
-        spec5.eval_spectral_broadcast(wi5, lams, out=ref5)
-        own_ok = bool(torch.equal(full[:, :n5].to(dev), ref5))
-        shards_ok = int(own_ok)
-        # the gathered planes are the one-GPU result bit for bit -- every other
-        # rank's columns against the root's own evaluation of that rank's regenerated inputs
-        for r in range(1, world):
-            wr = -hemisphere_dirs(n5, seed=C5_SEED + r, device=dev)
-            spec5.eval_spectral_broadcast(wr, lams, out=ref5)
-            shards_ok += int(torch.equal(full[:, r * n5:(r + 1) * n5].to(dev), ref5))
-            del wr
-        del ref5
-    del wi5
+    del wi5, out5
     tg = sorted(tgs)[1]
-    report = None
-    if rank == 0:
-        del out5
-        nbytes = 11 * n5 * 4 * (world - 1)
-        parity = parity_c5(full, n5, world, dev, em=spec5)
-        report = {
-            "dirs_per_gpu": n5, "lambdas": 11, "eval_s": te, "eval_kernel_ms": kernel_ms,
-            "evals_per_s_whole_job": 11 * n5 * world / te,
-            "eval_achieved_GBps": BYTES_SPEC_PER_DIR * n5 / (kernel_ms * 1e-3) / 1e9,
-            "gather_s": tg, "gather_bytes_to_root": nbytes, "gather_GBps": nbytes / tg / 1e9 if tg and nbytes else None,
-            "gather_bytes_note": ("bytes received by rank 0 from the other ranks" if world > 1 else
-                                  "one rank: the shard is already in place (no bytes move)"),
-            "gather_path": gpath,
-            "gather_timing": "median of 3 gathers into preallocated buffers after one untimed call",
-            "reassemble_planes_s": tcat, "end_to_end_s": te + tg + tcat, "bitwise_own_shard": own_ok,
-            "shards_bitwise_vs_one_gpu": f"{shards_ok}/{world}",
-            "parity": parity,
-            "note": "configs[4]: per-GPU spectral eval (weak scaling) then gather of the radiance to rank 0"}
+    if rank != 0:
+        return None
+    return {"n5": n5, "world": world, "dev": dev, "spec5": spec5, "full": full, "te": te, "kernel_ms": kernel_ms,
+            "tg": tg, "tcat": tcat, "gpath": gpath}
+
+
+def finish_c5(st):
+    """Rank 0 after the teardown collectives: the gathered planes against the root's own
+    evaluation of every rank's inputs (bit for bit) and against the oracle (parity_c5); the
+    configs[4] report."""
+    t_tail = time.perf_counter()
+    n5, world, dev, spec5, full = st["n5"], st["world"], st["dev"], st["spec5"], st["full"]
+    te, kernel_ms, tg, tcat, gpath = st["te"], st["kernel_ms"], st["tg"], st["tcat"], st["gpath"]
+    lams = [float(x) for x in range(320, 721, 40)]
+    # SURVEY.md §8e: the gathered planes are the one-GPU result bit for bit -- every rank's
+    # columns (the root's own included) against the root's evaluation of that rank's
+    # regenerated inputs
+    ref5 = torch.empty((11, n5), dtype=torch.float32, device=dev)
+    shards_ok, own_ok = 0, False
+    for r in range(world):
+        wr = -hemisphere_dirs(n5, seed=C5_SEED + r, device=dev)
+        spec5.eval_spectral_broadcast(wr, lams, out=ref5)
+        ok = bool(torch.equal(full[:, r * n5:(r + 1) * n5].to(dev), ref5))
+        shards_ok += int(ok)
+        own_ok = ok if r == 0 else own_ok
+        del wr
+    del ref5
+    torch.cuda.synchronize()
+    t_bitwise = time.perf_counter() - t_tail
+    nbytes = 11 * n5 * 4 * (world - 1)
+    parity = parity_c5(full, n5, world, dev, em=spec5)
+    report = {
+        "dirs_per_gpu": n5, "lambdas": 11, "eval_s": te, "eval_kernel_ms": kernel_ms,
+        "evals_per_s_whole_job": 11 * n5 * world / te,
+        "eval_achieved_GBps": BYTES_SPEC_PER_DIR * n5 / (kernel_ms * 1e-3) / 1e9,
+        "gather_s": tg, "gather_bytes_to_root": nbytes, "gather_GBps": nbytes / tg / 1e9 if tg and nbytes else None,
+        "gather_bytes_note": ("bytes received by rank 0 from the other ranks" if world > 1 else
+                              "one rank: the shard is already in place (no bytes move)"),
+        "gather_path": gpath,
+        "gather_timing": "median of 3 gathers into preallocated buffers after one untimed call",
+        "reassemble_planes_s": tcat, "end_to_end_s": te + tg + tcat, "bitwise_own_shard": own_ok,
+        "shards_bitwise_vs_one_gpu": f"{shards_ok}/{world}",
+        "parity": parity,
+        "rank0_tail_s": {"bitwise_reeval": t_bitwise, "total": time.perf_counter() - t_tail,
+                         "note": "rank 0's serial re-evaluation of every rank's inputs + CPU parity, after the "
+                                 "teardown collectives (no other rank waits for it)"},
+        "note": "configs[4]: per-GPU spectral eval (weak scaling) then gather of the radiance to rank 0"}
     del full
+    st["full"] = None
     return report
 
 
@@ -840,13 +857,25 @@ def spawn_ranks(n, argv, grace_s=SPAWN_GRACE_S):
     Rank 0 prints the bench line.  When a rank fails, the others get `grace_s` to finish (the
     C5 watchdog ends a rank stuck in a collective) and are then killed.  A SIGTERM / SIGINT to the
     parent is forwarded to the ranks, and a rank gets SIGTERM if the parent dies (PR_SET_PDEATHSIG),
-    so no rank outlives the launch.  Returns the exit code:
-    0 when every rank exited 0, else the first failing rank's code (a signal as 128 + signo)."""
+    so no rank outlives the launch.  The ranks rendezvous through a file store in a private
+    temporary directory (SUNSKY_BENCH_RENDEZVOUS), not a TCP port: a port picked here and
+    released before the ranks bind it could be taken in between.  Returns the exit
+    code: 0 when every rank exited 0, else the first failing rank's code (a signal as 128 + signo)."""
+    import shutil
+    import tempfile
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+        port = s.getsockname()[1]      # informational only (MASTER_PORT of a torchrun-style env)
+    rdv_dir = tempfile.mkdtemp(prefix="sunsky_bench_rdv_")
+    try:
+        return _spawn_and_wait(n, argv, grace_s, port, os.path.join(rdv_dir, "store"))
+    finally:
+        shutil.rmtree(rdv_dir, ignore_errors=True)
+
+
+def _spawn_and_wait(n, argv, grace_s, port, store):
     base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
-                LOCAL_WORLD_SIZE=str(n))
+                LOCAL_WORLD_SIZE=str(n), SUNSKY_BENCH_RENDEZVOUS=store)
     def die_with_parent():   # runs in the child before exec (no GPU touched yet): SIGTERM when the parent dies
         import ctypes as C
         C.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)   # PR_SET_PDEATHSIG
@@ -885,9 +914,10 @@ def spawn_ranks(n, argv, grace_s=SPAWN_GRACE_S):
 
 
 def c5_phase(run, rank, result, limit_s):
-    """configs[4] (`run()`) under a C5Watchdog.  Returns (report, watchdog, failed).  The
+    """configs[4] (`run()`) under a C5Watchdog.  Returns (state, watchdog, failed).  The
     watchdog stays ARMED: teardown() cancels it after the teardown collectives, so a rank
-    left waiting there (a peer whose C5 raised, or hung) still exits non-zero."""
+    left waiting there (a peer whose C5 raised, or hung) still exits non-zero.  Rank 0's
+    serial checks (finish_c5) run after that, outside the deadline."""
     watchdog = C5Watchdog(limit_s, rank, result).start()
     try:
         return run(), watchdog, False
@@ -933,6 +963,9 @@ def main():
     ap.add_argument("--c5-dirs", type=int, default=1 << 26, help="configs[4] directions per GPU (default 64M)")
     ap.add_argument("--launch-check", action="store_true",
                     help="print this rank's launch environment as JSON and exit before any GPU call (tests)")
+    ap.add_argument("--rendezvous-check", action="store_true",
+                    help="meet the other ranks over gloo as the bench does, all-reduce the ranks, print JSON and "
+                         "exit before any GPU call (tests)")
     args = ap.parse_args()
     SUN_SLACK[0] = 4.0 if args.precision == "reference" else 1.25
 
@@ -948,6 +981,17 @@ def main():
         return
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rendezvous_check:
+        store = os.environ.get("SUNSKY_BENCH_RENDEZVOUS")
+        init = {"init_method": f"file://{store}", "rank": rank, "world_size": world} if store else {}
+        dist.init_process_group("gloo", **init)
+        t = torch.tensor([float(rank)])
+        dist.all_reduce(t)
+        print(json.dumps({"rank": rank, "world": world, "rank_sum": float(t.item()),
+                          "rendezvous": "file" if store else "env"}), flush=True)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     # One rank per GPU over RCCL ("nccl").  More ranks than GPUs (a multi-rank rehearsal
     # on a 1-GPU box) share the GPUs and synchronise over gloo with CPU tensors.
     ndev = max(1, torch.cuda.device_count())
@@ -957,10 +1001,13 @@ def main():
     dev = torch.device("cuda", local % ndev)
     coll_dev = dev if backend == "nccl" else torch.device("cpu")
     if world > 1:
+        # spawn_ranks' ranks meet through its file store; a launcher's through env:// (MASTER_*)
+        store = os.environ.get("SUNSKY_BENCH_RENDEZVOUS")
+        init = {"init_method": f"file://{store}", "rank": rank, "world_size": world} if store else {}
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, **init)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, **init)
 
     n = args.n
     # NB input batches of n directions (4 x 201 MB > the 256 MiB Infinity Cache), one per step
@@ -1477,23 +1524,26 @@ def main():
         del full
 
     # ------------------------------------------- configs[4]: spectral shard + gather
-    watchdog, c5_failed = None, False
+    watchdog, c5_failed, c5 = None, False, None
     if not args.no_c5:
         del outs
         c5, watchdog, c5_failed = c5_phase(lambda: run_c5(args, world, rank, dev, coll_dev, rehearsal), rank, result,
                                            float(os.environ.get("SUNSKY_BENCH_C5_TIMEOUT", "150")))
-        if rank == 0:
+        if rank == 0 and c5_failed:
             result["c5_spectral_shard_gather"] = c5
+    # the teardown collectives under the still-armed C5 watchdog (ranks that finished C5 meet
+    # here at once: rank 0's serial checks come after), then every rank but 0 is done
+    teardown(world, rank, watchdog, c5_failed)
 
     if rank == 0:
-        if world == 1 and watchdog is not None:
-            watchdog.cancel()   # no collective follows at one rank: a slow cpu_baseline is not a C5 timeout
+        if c5 is not None and not c5_failed:
+            try:
+                result["c5_spectral_shard_gather"] = finish_c5(c5)
+            except Exception as exc:   # reported beside `value`; never fails the bench line itself
+                result["c5_spectral_shard_gather"] = {"error": f"{type(exc).__name__}: {exc}"}
         if not args.no_cpu and world == 1:   # the CPU baseline: rank 0 at N=1 only
             result["cpu_baseline"] = cpu_baseline(wi.T.cpu().numpy())
         print(json.dumps(result), flush=True)
-        if watchdog is not None:
-            watchdog.printed = True      # a later firing (teardown) exits without a second line
-    teardown(world, rank, watchdog, c5_failed)
 
 
 if __name__ == "__main__":

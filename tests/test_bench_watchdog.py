@@ -109,6 +109,23 @@ def test_gpus_n_without_a_launcher_spawns_n_ranks():
     assert len({d["master"] for d in lines}) == 1 and lines[0]["master"].startswith("127.0.0.1:")
 
 
+def test_spawned_ranks_rendezvous_through_a_file_store():
+    """spawn_ranks' ranks meet through a file store in a private temporary directory
+    (no TCP port to lose to another process between picking and binding it): 3 ranks over gloo
+    all-reduce their ranks and leave no store behind."""
+    import glob
+    import tempfile
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    before = set(glob.glob(os.path.join(tempfile.gettempdir(), "sunsky_bench_rdv_*")))
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--rendezvous-check"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(x) for x in p.stdout.strip().splitlines() if x.startswith("{")]   # (gloo logs too)
+    assert sorted(d["rank"] for d in lines) == [0, 1, 2]
+    assert {d["rank_sum"] for d in lines} == {3.0} and {d["rendezvous"] for d in lines} == {"file"}
+    assert set(glob.glob(os.path.join(tempfile.gettempdir(), "sunsky_bench_rdv_*"))) == before
+
+
 def test_spawned_rank_failure_fails_the_run():
     """A rank that exits non-zero makes the spawning parent exit non-zero (its peers are given
     the grace period, then killed).  Here every rank fails fast: no GPU in the CPU suite."""

@@ -671,7 +671,11 @@ def run_c5(args, world, rank, dev, coll_dev, rehearsal):
     spec5 = ss.SunskyEmitter(c5_scene(), "spectral", precision=args.precision, device=dev)
     lams = [float(x) for x in range(320, 721, 40)]
     full = None
-    if rank == 0 and not rehearsal:
+    # a rehearsal (more ranks than GPUs) gathers over gloo, unless SUNSKY_BENCH_RCCL_DOUBLE names
+    # the multi-process RCCL test double (tests/cpp/fake_rccl_ipc.cpp): then it takes the C ABI
+    # branch below, the one a real multi-GPU run takes, with the double in RCCL's place
+    capi_gather = not rehearsal or bool(os.environ.get("SUNSKY_BENCH_RCCL_DOUBLE"))
+    if rank == 0 and capi_gather:
         # the root evaluates its shard straight into its columns [0, n5) of the final (11, N)
         # planes (plane stride N): sunsky_gather_radiance then finds it in place and copies
         # nothing for it (csrc/sunsky_comm.cpp), so the root's time is the eval plus the receives
@@ -702,13 +706,16 @@ def run_c5(args, world, rank, dev, coll_dev, rehearsal):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         te = float(t.item())
     tgs = []
-    if not rehearsal:
+    if capi_gather:
         # C ABI gather (grouped RCCL send/recv) straight into rank 0's final planes; the root's
         # own columns are already in place (one rank, no torch.distributed: nothing to move)
         from sunsky_amd.sharding import RadianceComm
         gpath = ("sunsky_gather_radiance: RCCL send/recv into rank 0's (11, N) planes, the root's shard "
                  "evaluated in place; no padding / concat" if world > 1 else
                  "sunsky_gather_radiance, one rank: the shard was evaluated in place in the (11, N) planes")
+        if rehearsal:
+            gpath += (f" -- rehearsal: send/recv by the RCCL test double {os.path.basename(os.environ['SUNSKY_AMD_RCCL'])} "
+                      "(hipIpc handles between the rank processes on one GPU), not RCCL; its time is not xGMI's")
         comm = RadianceComm(device=dev)
         comm.gather(out5, n5 * world, out=full)         # untimed: connection setup
         for _ in range(3):
@@ -996,6 +1003,12 @@ def main():
     # on a 1-GPU box) share the GPUs and synchronise over gloo with CPU tensors.
     ndev = max(1, torch.cuda.device_count())
     rehearsal = world > ndev
+    double = os.environ.get("SUNSKY_BENCH_RCCL_DOUBLE")
+    if double:
+        # the C ABI resolves RCCL at its first communicator call (csrc/sunsky_comm.cpp rccl())
+        if not rehearsal:
+            raise SystemExit("SUNSKY_BENCH_RCCL_DOUBLE is for rehearsals (more ranks than GPUs) only")
+        os.environ["SUNSKY_AMD_RCCL"] = os.path.abspath(double)
     backend = "gloo" if rehearsal else os.environ.get("SUNSKY_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local % ndev)
     dev = torch.device("cuda", local % ndev)
@@ -1104,7 +1117,8 @@ def main():
             "config": {"workload": "RGB eval(): 16,777,216 uniform upper-hemisphere dirs per GPU x turbidity {2,6,10}",
                        "dirs_per_gpu": n, "turbidity": list(TURBIDITIES), "sun_elevation_deg": 45,
                        "albedo": 0.1, "precision": args.precision, "parallelism": f"shard{world}",
-                       **({"rehearsal": f"{world} ranks on {ndev} GPU(s), gloo"} if rehearsal else {})},
+                       **({"rehearsal": f"{world} ranks on {ndev} GPU(s), gloo" +
+                           (", C5 gather through the RCCL test double" if double else "")} if rehearsal else {})},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS,
                          "achieved_all_cold": BYTES_RGB * n / (cold_ms * 1e-3) / 1e9,

@@ -80,7 +80,13 @@ std::string code_object_path() {
 // per-direction identity test.  SUNSKY_AMD_CODE_OBJECT_IDENT (a probe build) replaces it.
 std::string ident_code_object_path() {
     if (const char* env = std::getenv("SUNSKY_AMD_CODE_OBJECT_IDENT")) return env;
-    return library_dir() + "/sunsky_kernels_ident.hsaco";
+    const std::string path = library_dir() + "/sunsky_kernels_ident.hsaco";
+    // an A/B run that overrides only the general module would otherwise time the installed
+    // identity module for every identity-to_world emitter without noticing
+    if (std::getenv("SUNSKY_AMD_CODE_OBJECT"))
+        std::fprintf(stderr, "sunsky_amd: SUNSKY_AMD_CODE_OBJECT is set but SUNSKY_AMD_CODE_OBJECT_IDENT is not: "
+                             "emitters with an identity to_world use %s\n", path.c_str());
+    return path;
 }
 
 // An SS_XFORM_IDENTITY build exports sunsky_xform_identity_marker.  Such an object as the

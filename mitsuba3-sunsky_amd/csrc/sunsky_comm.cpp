@@ -11,6 +11,7 @@
 #include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -50,9 +51,18 @@ const Rccl& rccl() {
     static std::once_flag once;
     static std::string err;
     std::call_once(once, [] {
+        // SUNSKY_AMD_RCCL: the RCCL library to use, by path (a specific RCCL build; the tests'
+        // multi-process double on a one-GPU box).  Only that one is tried.
+        if (const char* forced = std::getenv("SUNSKY_AMD_RCCL")) {
+            r.so = dlopen(forced, RTLD_NOW | RTLD_LOCAL);
+            if (!r.so) {
+                err = std::string("RCCL not found (dlopen SUNSKY_AMD_RCCL=") + forced + "): " + dlerror();
+                return;
+            }
+        }
         for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
-            r.so = dlopen(name, RTLD_NOW | RTLD_LOCAL);
             if (r.so) break;
+            r.so = dlopen(name, RTLD_NOW | RTLD_LOCAL);
         }
         if (!r.so) {
             err = std::string("RCCL not found (dlopen librccl.so.1): ") + dlerror();

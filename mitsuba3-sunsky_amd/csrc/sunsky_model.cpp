@@ -521,22 +521,22 @@ int reference_sun_segment(float cos_theta) {
 }
 
 const std::array<float, kNbSunSegments>& sun_segment_thresholds() {
-    // bisection over the fp32 bit patterns of [0, 1] (ordered like the values): the decision
-    // is monotone there (every fp32 checked against the thresholds in tests/test_capi_cpu.py)
-    static const std::array<float, kNbSunSegments> z = [] {
-        std::array<float, kNbSunSegments> t{};
-        auto val = [](uint32_t b) { float f; std::memcpy(&f, &b, 4); return f; };
-        const uint32_t one = 0x3f800000u;
-        for (int j = 1; j < kNbSunSegments; ++j) {
-            uint32_t lo = 0, hi = one;   // reference_sun_segment(val(hi)) >= j always (44 at 1)
-            while (lo < hi) {
-                const uint32_t mid = lo + (hi - lo) / 2;
-                if (reference_sun_segment(val(mid)) >= j) hi = mid; else lo = mid + 1;
-            }
-            t[j] = val(lo);
-        }
-        return t;
-    }();
+    // Committed constants, not derived at run time from whatever libm loads the
+    // library: [j] is the smallest fp32 cos theta in [0, 1] whose reference_sun_segment is >= j,
+    // found by bisection over the fp32 bit patterns of [0, 1] with glibc 2.35's acosf / cbrtf.
+    // tests/test_capi_cpu.py checks EVERY fp32 cos theta in [0, 1] against the oracle's fp32
+    // decision on the libm the tests run on (a libm whose decision moves fails that test).
+    static const std::array<float, kNbSunSegments> z = {{
+    0x0.0p+0f, 0x1.204442p-16f, 0x1.210888p-13f, 0x1.e80444p-12f, 0x1.21310ep-10f,
+    0x1.1a6c7cp-9f, 0x1.e8044p-9f, 0x1.837bbp-8f, 0x1.21322ep-7f, 0x1.9bc35cp-7f,
+    0x1.1a68fep-6f, 0x1.77dfap-6f, 0x1.e7f51ap-6f, 0x1.362b4ep-5f, 0x1.83578cp-5f,
+    0x1.dc527ap-5f, 0x1.20f644p-4f, 0x1.5a7926p-4f, 0x1.9b14ccp-4f, 0x1.e328dep-4f,
+    0x1.1987b2p-3f, 0x1.458df6p-3f, 0x1.75ccb4p-3f, 0x1.aa63e2p-3f, 0x1.e36c74p-3f,
+    0x1.107b84p-2f, 0x1.3184c4p-2f, 0x1.54cea4p-2f, 0x1.7a4e12p-2f, 0x1.a1eed8p-2f,
+    0x1.cb9202p-2f, 0x1.f70bfap-2f, 0x1.12114ap-1f, 0x1.29457ap-1f, 0x1.40f3aap-1f,
+    0x1.58e25cp-1f, 0x1.70cc56p-1f, 0x1.885fa2p-1f, 0x1.9f3c7cp-1f, 0x1.b4f4b8p-1f,
+    0x1.c90b3p-1f, 0x1.daf3dap-1f, 0x1.ea1422p-1f, 0x1.f5c448p-1f, 0x1.fd5146p-1f,
+    }};
     return z;
 }
 

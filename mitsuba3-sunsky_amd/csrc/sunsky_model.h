@@ -36,7 +36,7 @@ struct EvalTangent {
 // min(floor(cbrt(2 (pi/2 - acos z) / pi) 45), 44), libm acosf / cbrtf, no contraction.
 int reference_sun_segment(float cos_theta);
 // SunskyKArgs::sun_seg_z: [j] = the smallest fp32 cos theta in [0, 1] whose
-// reference_sun_segment is >= j ([0] = 0); computed once per process.
+// reference_sun_segment is >= j ([0] = 0); committed constants (sunsky_model.cpp).
 const std::array<float, kNbSunSegments>& sun_segment_thresholds();
 
 class SunskyModel {

@@ -236,7 +236,14 @@ SS_HD inline QuadDir quad_dir(const SunskyKArgs& K, const float* x, const float*
     d.pos = 0;
     d.xs = d.cpsi = 0.f;
     if (d.sun_ok) {
-        d.pos = sun_segment(wl.z, &d.xs);
+        // render_sun's segment (sunsky.cpp:579-587) from the staged cos theta thresholds, as
+        // every eval / sampling / AD kernel takes it (SunskyKArgs::sun_seg_z), not from this
+        // build's acosf / cbrtf: host and device staging and the kernels agree at segment starts
+        int pos = 0;
+        for (int s = 1; s < kNbSunSegments; ++s) pos += wl.z >= K.sun_seg_z[s] ? 1 : 0;
+        const float frac = (float)pos / (float)kNbSunSegments;
+        d.pos = pos;
+        d.xs = (kHalfPi - acosf(wl.z)) - kHalfPi * (frac * frac * frac);
         d.cpsi = cos_psi(g2, K.inv_sin2_half_ap);
     }
     return d;

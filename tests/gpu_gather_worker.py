@@ -1,7 +1,9 @@
-"""Worker of tests/test_gpu_gather.py: one rank of a 2-process run on the GPU box.
+"""Worker of tests/test_gpu_gather.py: one rank of a multi-process run on the GPU box.
 Each rank evaluates its shard of a spectral batch (C3 node kernel, 11 planes) with
-the HIP kernels and the shards are gathered to rank 0 through the C ABI's RCCL gather
-(sunsky_gather_radiance); rank 0 compares with the whole batch evaluated alone.
+the HIP kernels and the shards are gathered to the root (GATHER_ROOT, default 0) through
+the C ABI's RCCL gather (sunsky_gather_radiance); the root compares with the whole batch
+evaluated alone.  With SUNSKY_AMD_RCCL naming tests/cpp/build/libfake_rccl_ipc.so the
+product's send/recv go through that multi-process test double instead of RCCL.
 Exit 0 = bitwise equal, 3 = RCCL refused the configuration (e.g. two ranks on one
 GPU), anything else = failure."""
 import os
@@ -22,6 +24,7 @@ from sunsky_amd.sharding import RadianceComm, shard_range  # noqa: E402
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     n = int(os.environ.get("GATHER_N", str((1 << 20) + 3)))
+    root = int(os.environ.get("GATHER_ROOT", "0"))
     ndev = torch.cuda.device_count()
     torch.cuda.set_device(rank % ndev)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -36,13 +39,13 @@ def main():
         except RuntimeError as e:
             print(f"rank {rank}: RCCL communicator refused: {e}", flush=True)
             return 3
-        full = comm.gather(local, n, root=0)
+        full = comm.gather(local, n, root=root)
         torch.cuda.synchronize()
-        if rank == 0:
+        if rank == root:
             whole = em.eval_spectral_broadcast(wi, lam)
             torch.cuda.synchronize()
             ok = torch.equal(full, whole)
-            print(f"rank 0: gathered {tuple(full.shape)} bitwise equal: {ok}", flush=True)
+            print(f"rank {rank}: gathered {tuple(full.shape)} from {world} ranks, bitwise equal: {ok}", flush=True)
             if not ok:
                 return 1
         comm.close()

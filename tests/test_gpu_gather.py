@@ -10,7 +10,11 @@ final [C][N] planes.
 * the multi-rank send/recv branch itself on one GPU, 2-4 ranks in one process, with the
   RCCL entry points served by the test double tests/cpp/fake_rccl.cpp (linked by the
   test program tests/cpp/gather_double_check): ragged and empty shards, 3 and 11 planes,
-  either root, either call order.
+  either root, either call order;
+* the same branch with the ranks as separate PROCESSES on one GPU (the layout of a real
+  multi-GPU job, and of bench.py's rehearsal with SUNSKY_BENCH_RCCL_DOUBLE): the product
+  dlopens the multi-process double tests/cpp/fake_rccl_ipc.cpp through SUNSKY_AMD_RCCL,
+  torch.distributed (gloo) carries the unique id as in a real job.
 """
 import ctypes as C
 import os
@@ -71,14 +75,14 @@ def test_single_rank_gather_and_in_place():
         L.sunsky_comm_destroy(h)
 
 
-def test_two_ranks_rccl_gather_bitwise():
+def run_workers(world, **extra):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), **extra)
     worker = os.path.join(ROOT, "tests", "gpu_gather_worker.py")
     procs = [subprocess.Popen([sys.executable, worker], env=dict(env, RANK=str(r)), stdout=subprocess.PIPE,
-                              stderr=subprocess.STDOUT, text=True) for r in range(2)]
+                              stderr=subprocess.STDOUT, text=True) for r in range(world)]
     outs = []
     try:
         for p in procs:
@@ -91,10 +95,29 @@ def test_two_ranks_rccl_gather_bitwise():
     codes = [c for c, _ in outs]
     text = "\n".join(o for _, o in outs)
     print(text)
+    return codes, text
+
+
+def test_two_ranks_rccl_gather_bitwise():
+    codes, text = run_workers(2)
     if 3 in codes:
         pytest.skip("RCCL refused this configuration: " + text.strip().splitlines()[-1][:300])
     assert codes == [0, 0], text
     assert "bitwise equal: True" in text
+
+
+@pytest.mark.parametrize("world,root", [(4, 0), (3, 2)])
+def test_rank_processes_gather_through_ipc_double(world, root):
+    """`world` rank processes on one GPU, each evaluating a ragged shard of 2^20 + 3 rays;
+    sunsky_gather_radiance's grouped send / recv served by tests/cpp/fake_rccl_ipc.cpp (device
+    memory exported between the processes with hipIpc handles)."""
+    so = os.path.join(ROOT, "tests", "cpp", "build", "libfake_rccl_ipc.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "cpp"), "build/libfake_rccl_ipc.so"], check=True,
+                       capture_output=True)
+    codes, text = run_workers(world, SUNSKY_AMD_RCCL=so, GATHER_ROOT=str(root), SUNSKY_FAKE_RCCL_TIMEOUT="60")
+    assert codes == [0] * world, text
+    assert f"rank {root}: gathered (11, {(1 << 20) + 3}) from {world} ranks, bitwise equal: True" in text
 
 
 def test_multi_rank_gather_through_rccl_double():

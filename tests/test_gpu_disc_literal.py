@@ -4,7 +4,7 @@ The error of a disc lane splits in two (oracle/oracle_impl.inc `oracle_round_sta
 `oracle_adopt_tables`):
 * table rounding: the reference stages its tables in fp32 (array_from_file<Float64, Float>,
   sunsky.cpp:182-195).  The fp64 evaluation of the fp32-rounded tables ("o64r") against the
-  fp64 tables ("o64") is measured and reported here (<= 3e-7 on every disc lane measured);
+  fp64 tables ("o64") is measured in tests/test_oracle_table_modes.py (<= 1.4e-6 on its disc lanes);
 * the kernel's own arithmetic: the kernel against the fp64 evaluation of the exact fp32
   tables, local sun direction and disc cutoff it was given ("o64t", the oracle adopting the
   product's staged state) -- the exact value of the fp32-staged algorithm on those inputs.

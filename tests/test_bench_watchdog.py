@@ -4,7 +4,6 @@ with the C5 error and every rank exits non-zero (C5Watchdog.EXIT_CODE).  CPU onl
 process, then a gloo world-2 rehearsal in which rank 1 never reaches the barrier."""
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -26,7 +25,7 @@ sys.path.insert(0, {root!r})
 import torch.distributed as dist
 import bench
 rank = int(os.environ["RANK"])
-dist.init_process_group("gloo")
+dist.init_process_group("gloo", init_method="file://" + os.environ["SUNSKY_TEST_STORE"], rank=rank, world_size=2)
 result = {{"metric": "m", "value": 2.0}} if rank == 0 else None
 bench.C5Watchdog(3.0, rank, result).start()
 if rank == 1:
@@ -49,11 +48,9 @@ def test_watchdog_prints_the_line_and_exits_nonzero():
     assert line["value"] == 1.0 and "timed out" in line["c5_spectral_shard_gather"]["error"]
 
 
-def test_watchdog_gloo_world2_rank_stuck_in_collective():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
+def test_watchdog_gloo_world2_rank_stuck_in_collective(tmp_path):
+    # the ranks meet through a file store in the test's own directory (no port race under pytest -n)
+    env = dict(os.environ, SUNSKY_TEST_STORE=str(tmp_path / "rdv"), WORLD_SIZE="2")
     procs = [subprocess.Popen([sys.executable, "-c", _RANK.format(root=ROOT)], env=dict(env, RANK=str(r)),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
     outs = [p.communicate(timeout=120) for p in procs]
@@ -141,7 +138,7 @@ sys.path.insert(0, {root!r})
 import torch.distributed as dist
 import bench
 rank = int(os.environ["RANK"])
-dist.init_process_group("gloo")
+dist.init_process_group("gloo", init_method="file://" + os.environ["SUNSKY_TEST_STORE"], rank=rank, world_size=2)
 result = {{"metric": "m", "value": 3.0}} if rank == 0 else None
 
 def run():
@@ -160,16 +157,13 @@ print("teardown passed", flush=True)
 """
 
 
-def test_c5_failure_on_one_rank_ends_every_rank_nonzero():
+def test_c5_failure_on_one_rank_ends_every_rank_nonzero(tmp_path):
     """a rank whose configs[4] raised skips the teardown collectives and exits
     EXIT_CODE; its peer, left in C5's collective, ends non-zero too: gloo raises when the peer
     is gone (the same path as a C5 error), RCCL would wait and the still-armed watchdog ends it
     (test_watchdog_gloo_world2_rank_stuck_in_collective)."""
     for bad in (1, 0):
-        with socket.socket() as s:
-            s.bind(("127.0.0.1", 0))
-            port = s.getsockname()[1]
-        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
+        env = dict(os.environ, SUNSKY_TEST_STORE=str(tmp_path / f"rdv{bad}"), WORLD_SIZE="2")
         procs = [subprocess.Popen([sys.executable, "-c", _TEARDOWN.format(root=ROOT, bad=bad)],
                                   env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
                  for r in range(2)]

@@ -3,7 +3,6 @@ evaluates its slice of one ray batch and rank 0 gathers; the gathered buffer
 must equal the single-process result bit for bit.  The per-rank compute here
 is the oracle (no GPU in this container) -- what is under test is the
 partitioning and the gather, which the GPU path (bench.py --gather) shares."""
-import os
 
 import numpy as np
 import pytest
@@ -38,9 +37,14 @@ def test_shard_range_errors():
         shard_range(10, 0, 0)
 
 
-def _worker(rank, world, port, n, out_path):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _init(rank, world, store):
+    # a file store in the test's own temporary directory: no port picked in advance that a
+    # parallel test could take in between (pytest -n)
+    dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
+
+
+def _worker(rank, world, store, n, out_path):
+    _init(rank, world, store)
     try:
         import oracle as O
         wi = -hemisphere_wo(n, seed=5)          # every rank can regenerate the batch
@@ -55,12 +59,9 @@ def _worker(rank, world, port, n, out_path):
 
 @pytest.mark.parametrize("n", [4096 + 3, 10000])
 def test_gloo_world2_gather_matches_single_process(tmp_path, n):
-    import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    store = str(tmp_path / "rdv")
     out = str(tmp_path / "full.npy")
-    mp.start_processes(_worker, args=(2, port, n, out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(2, store, n, out), nprocs=2, join=True, start_method="spawn")
     import oracle as O
     ref = O.Oracle(SCENE, "rgb", "jit", "f32").eval(-hemisphere_wo(n, seed=5)).T
     got = np.load(out)
@@ -68,12 +69,11 @@ def test_gloo_world2_gather_matches_single_process(tmp_path, n):
     assert np.array_equal(got, ref)
 
 
-def _key_worker(rank, world, port, out_path):
+def _key_worker(rank, world, store, out_path):
     from sunsky_amd.sharding import _group_key
     dev = torch.device("cuda", 0)               # a device object only: no GPU is touched
     keys = [_group_key(None, dev)]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init(rank, world, store)
     keys.append(_group_key(None, dev))
     dist.destroy_process_group()
     keys.append(_group_key(None, dev))
@@ -85,12 +85,9 @@ def test_comm_cache_key_tracks_the_world(tmp_path):
     """the cached RCCL communicator is keyed by the group's rank and size, so a
     world of another size never reuses one, and a process without torch.distributed gets its
     own world-1 key (a same-size re-initialisation: the test below)."""
-    import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    store = str(tmp_path / "rdv")
     out = str(tmp_path / "keys.npy")
-    mp.start_processes(_key_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_key_worker, args=(2, store, out), nprocs=2, join=True, start_method="spawn")
     keys = [tuple(k) for k in np.load(out, allow_pickle=True)]
     assert keys[0] == (None, 0, 0, 1) and keys[2] == keys[0]
     assert keys[1] == (None, 0, 1, 2)
@@ -108,15 +105,14 @@ class _FakeComm:
         self._h = None
 
 
-def _reinit_worker(rank, world, port, out_path):
+def _reinit_worker(rank, world, store, out_path):
     from sunsky_amd.sharding import clear_radiance_comms, radiance_comm
     dev = torch.device("cuda", 0)               # a device object only: no GPU is touched
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init(rank, world, store)
     a = radiance_comm(device=dev, _factory=_FakeComm)
     a2 = radiance_comm(device=dev, _factory=_FakeComm)
     dist.destroy_process_group()
-    dist.init_process_group("gloo", rank=rank, world_size=world)   # same rank, same size
+    _init(rank, world, store + ".2")   # same rank, same size
     b = radiance_comm(device=dev, _factory=_FakeComm)
     res = [a is a2, b is not a, a._h is None, b._h is not None, len(_FakeComm.made)]
     clear_radiance_comms()
@@ -130,11 +126,8 @@ def test_comm_cache_same_size_reinit_gets_a_new_communicator(tmp_path):
     """a world destroyed and re-initialised with the same rank and size has a new
     process group object; the cached communicator built over the old one is closed and a new
     one created, never reused."""
-    import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    store = str(tmp_path / "rdv")
     out = str(tmp_path / "reinit.npy")
-    mp.start_processes(_reinit_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_reinit_worker, args=(2, store, out), nprocs=2, join=True, start_method="spawn")
     res = list(np.load(out, allow_pickle=True))
     assert res == [True, True, True, True, 2, True], res

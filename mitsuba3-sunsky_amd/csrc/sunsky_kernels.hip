@@ -569,7 +569,8 @@ __device__ __forceinline__ void render_sun_rgb_rows(const SunRowsRgb& R, int row
                                                     float out[3]) {
     static_assert(kNbSunLdParams == 6 && kSunRowFloats == 20, "row slots: 12 pair values, 6 channel-2 values, 2 pad");
     float r0 = 0.f, r1 = 0.f, r2 = 0.f;
-#pragma unroll (HOIST ? 2 : 1)
+    constexpr int kUnroll = HOIST ? 2 : 1;
+#pragma unroll kUnroll
     for (int k = kNbSunCtrlPts - 1; k >= 0; --k) {
         const float4* q = R.r[row][k];
         float v[kSunRowFloats];

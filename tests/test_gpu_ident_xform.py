@@ -94,3 +94,22 @@ def test_code_object_override_of_the_wrong_form_is_refused(var, obj, msg):
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode != 0, "the wrong-form code object was accepted"
     assert msg in r.stderr, r.stderr[-2000:]
+
+
+def test_general_code_object_override_alone_names_the_identity_module():
+    """with only SUNSKY_AMD_CODE_OBJECT set, identity-to_world emitters still run the
+    installed identity module; the C ABI says so once on stderr, so an A/B of a probe build
+    cannot silently time the installed kernels."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, SUNSKY_AMD_CODE_OBJECT=ss.CODE_OBJECT)
+    env.pop("SUNSKY_AMD_CODE_OBJECT_IDENT", None)
+    code = ("import sys, torch; sys.path.insert(0, %r); import sunsky_amd as ss\n"
+            "em = ss.load_dict({'type': 'sunsky', 'sun_direction': [0.3, 0.4, 0.866]})\n"
+            "em.eval(ss.SurfaceInteraction3f(wi=-torch.ones((3, 64), device='cuda') / 3 ** 0.5))\n"
+            "torch.cuda.synchronize()\n" % os.path.dirname(os.path.dirname(ss.__file__)))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "SUNSKY_AMD_CODE_OBJECT is set but SUNSKY_AMD_CODE_OBJECT_IDENT is not" in r.stderr, r.stderr[-2000:]
+    assert "sunsky_kernels_ident.hsaco" in r.stderr

@@ -106,9 +106,10 @@ def test_two_ranks_rccl_gather_bitwise():
     assert "bitwise equal: True" in text
 
 
-@pytest.mark.parametrize("world,root", [(4, 0), (3, 2)])
+@pytest.mark.parametrize("world,root", [(4, 0), (3, 2), (8, 5)])
 def test_rank_processes_gather_through_ipc_double(world, root):
-    """`world` rank processes on one GPU, each evaluating a ragged shard of 2^20 + 3 rays;
+    """`world` rank processes on one GPU (8: the driver's node size), each evaluating a ragged
+    shard of 2^20 + 3 rays;
     sunsky_gather_radiance's grouped send / recv served by tests/cpp/fake_rccl_ipc.cpp (device
     memory exported between the processes with hipIpc handles)."""
     so = os.path.join(ROOT, "tests", "cpp", "build", "libfake_rccl_ipc.so")

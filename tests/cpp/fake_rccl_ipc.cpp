@@ -8,11 +8,13 @@
 //
 // The unique id is a private directory (mkdtemp).  A send and the receive it pairs with (same
 // sender, receiver and position in their order, as NCCL matches point-to-point operations)
-// meet through it: at ncclGroupEnd the sender waits for its stream, exports the buffer's
-// allocation with hipIpcGetMemHandle and publishes (handle, offset, bytes) in a file named by
-// (sender, receiver, sequence); the receiver waits for that file, opens the handle, copies on
-// its stream, waits for the copy, closes the handle and answers with a "done" file; the sender
-// returns when every one of its sends is answered, so its buffer stays valid throughout.  All
+// meet through it: at ncclGroupEnd the sender copies the send into an allocation of its own
+// (exporting the caller's allocation directly hung hipIpcOpenMemHandle for allocations past
+// 2 GiB -- configs[4]'s 2.95 GB shard planes -- while 1.5 GB ones worked), exports it with
+// hipIpcGetMemHandle and publishes (handle, bytes) in a file named by (sender, receiver,
+// sequence); the receiver waits for that file, opens the handle, copies on its stream, waits for
+// the copy, closes the handle and answers with a "done" file; the sender frees its copy when
+// every one of its sends is answered.  All
 // of a group's sends are published before any of its receives waits, so no rank waits on a
 // peer that is itself waiting.  Only float32 (datatype 7).  A missing peer times out (120 s,
 // SUNSKY_FAKE_RCCL_TIMEOUT) with an error instead of hanging.
@@ -48,6 +50,7 @@ struct Op {
     size_t bytes;
     hipStream_t stream;
     unsigned seq;
+    void* stage;   // the sender's exported copy
 };
 
 struct Published {
@@ -60,6 +63,16 @@ thread_local std::vector<Op> t_ops;
 
 std::string path(const Comm* c, const char* kind, int from, int to, unsigned seq) {
     return c->dir + "/" + kind + "_" + std::to_string(from) + "_" + std::to_string(to) + "_" + std::to_string(seq);
+}
+
+// SUNSKY_FAKE_RCCL_DEBUG=1: per-operation timings on stderr
+bool debug() {
+    static const bool on = std::getenv("SUNSKY_FAKE_RCCL_DEBUG") != nullptr;
+    return on;
+}
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 bool wait_for(const std::string& p) {
@@ -86,15 +99,20 @@ bool write_atomic(const std::string& p, const void* data, size_t n) {
     return ok && std::rename(tmp.c_str(), p.c_str()) == 0;
 }
 
-int publish(const Op& s) {
-    if (hipStreamSynchronize(s.stream) != hipSuccess) return kInternal;
-    void* base = nullptr;
-    size_t size = 0;
-    if (hipMemGetAddressRange(&base, &size, s.buf) != hipSuccess) return kInternal;
+int publish(Op& s) {
+    const double t0 = now_s();
+    if (hipMalloc(&s.stage, s.bytes ? s.bytes : 4) != hipSuccess) return kInternal;
+    if (hipMemcpyAsync(s.stage, s.buf, s.bytes, hipMemcpyDeviceToDevice, s.stream) != hipSuccess ||
+        hipStreamSynchronize(s.stream) != hipSuccess)
+        return kInternal;
     Published m{};
-    if (hipIpcGetMemHandle(&m.handle, base) != hipSuccess) return kInternal;
-    m.offset = (size_t)((char*)s.buf - (char*)base);
+    const double t1 = now_s();
+    if (hipIpcGetMemHandle(&m.handle, s.stage) != hipSuccess) return kInternal;
+    m.offset = 0;
     m.bytes = s.bytes;
+    if (debug())
+        std::fprintf(stderr, "fake_rccl_ipc: rank %d send %u to %d: %zu B, stage %.3f s, export %.3f s\n",
+                     s.comm->rank, s.seq, s.peer, s.bytes, t1 - t0, now_s() - t1);
     return write_atomic(path(s.comm, "send", s.comm->rank, s.peer, s.seq), &m, sizeof m) ? kOk : kInternal;
 }
 
@@ -112,20 +130,33 @@ int receive(const Op& r) {
         return kInvalidArgument;
     }
     void* mapped = nullptr;
+    const double t0 = now_s();
     if (hipIpcOpenMemHandle(&mapped, m.handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return kInternal;
+    const double t1 = now_s();
     int rc = kOk;
     if (hipMemcpyAsync(r.buf, (char*)mapped + m.offset, m.bytes, hipMemcpyDeviceToDevice, r.stream) != hipSuccess ||
         hipStreamSynchronize(r.stream) != hipSuccess)
         rc = kInternal;
+    const double t2 = now_s();
     (void)hipIpcCloseMemHandle(mapped);
+    if (debug())
+        std::fprintf(stderr, "fake_rccl_ipc: rank %d recv %u from %d: %zu B, open %.3f s, copy %.3f s, close %.3f s\n",
+                     r.comm->rank, r.seq, r.peer, m.bytes, t1 - t0, t2 - t1, now_s() - t2);
     std::remove(p.c_str());
     const char one = 1;
     if (!write_atomic(path(r.comm, "done", r.peer, r.comm->rank, r.seq), &one, 1)) rc = kInternal;
     return rc;
 }
 
-int run(const std::vector<Op>& ops) {
-    for (const Op& o : ops)
+int run(std::vector<Op>& ops) {
+    struct Free {   // the sender's copies, whatever the outcome
+        std::vector<Op>& ops;
+        ~Free() {
+            for (Op& o : ops)
+                if (o.stage) (void)hipFree(o.stage);
+        }
+    } release{ops};
+    for (Op& o : ops)
         if (o.send)
             if (int rc = publish(o)) return rc;
     for (const Op& o : ops)
@@ -191,12 +222,13 @@ static int enqueue(bool send, const void* buf, size_t count, int datatype, int p
                    hipStream_t stream) {
     if (!comm || datatype != kFloat32 || peer < 0 || peer >= comm->nranks || peer == comm->rank) return kInvalidArgument;
     const unsigned seq = send ? comm->send_seq[peer]++ : comm->recv_seq[peer]++;
-    Op o{send, comm, peer, const_cast<void*>(buf), count * sizeof(float), stream, seq};
+    Op o{send, comm, peer, const_cast<void*>(buf), count * sizeof(float), stream, seq, nullptr};
     if (t_depth > 0) {
         t_ops.push_back(o);
         return kOk;
     }
-    return run({o});
+    std::vector<Op> one{o};
+    return run(one);
 }
 
 int ncclSend(const void* buf, size_t count, int datatype, int peer, ncclComm_t comm, hipStream_t stream) {

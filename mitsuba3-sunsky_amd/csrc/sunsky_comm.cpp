@@ -53,7 +53,8 @@ const Rccl& rccl() {
     std::call_once(once, [] {
         // SUNSKY_AMD_RCCL: the RCCL library to use, by path (a specific RCCL build; the tests'
         // multi-process double on a one-GPU box).  Only that one is tried.
-        if (const char* forced = std::getenv("SUNSKY_AMD_RCCL")) {
+        const char* forced = std::getenv("SUNSKY_AMD_RCCL");
+        if (forced && *forced) {
             r.so = dlopen(forced, RTLD_NOW | RTLD_LOCAL);
             if (!r.so) {
                 err = std::string("RCCL not found (dlopen SUNSKY_AMD_RCCL=") + forced + "): " + dlerror();

@@ -508,22 +508,12 @@ void SunskyModel::stage_geometry() {
     k_.sun_ld = nullptr;
 }
 
-// Index returned by the kernels' discrete_sample_reuse for s = value * sum:
-// JIT, the prefix count of ((cdf < s) || cdf == 0) && cdf != sum over [0, n-1)
-// (distr_1d.h:116-136); scalar, first + #{i in [first, last) : cdf[i] < s}.
-// Both are monotone in s (cdf is non-decreasing).
-int reference_sun_segment(float cos_theta) {
-    const float pi = 3.14159265358979323846f;
-    const float elevation = 0.5f * pi - acosf(cos_theta);
-    const float seg = cbrtf(2.f * elevation * (1.f / pi)) * (float)kNbSunSegments;
-    const int pos = seg > 0.f ? (int)floorf(seg) : 0;
-    return pos < kNbSunSegments - 1 ? pos : kNbSunSegments - 1;
-}
-
 const std::array<float, kNbSunSegments>& sun_segment_thresholds() {
     // Committed constants, not derived at run time from whatever libm loads the
-    // library: [j] is the smallest fp32 cos theta in [0, 1] whose reference_sun_segment is >= j,
-    // found by bisection over the fp32 bit patterns of [0, 1] with glibc 2.35's acosf / cbrtf.
+    // library: [j] is the smallest fp32 cos theta in [0, 1] whose render_sun segment
+    // (sunsky.cpp:579-584: min(floor(cbrt(2 (pi/2 - acosf z) / pi) 45), 44) in fp32, no
+    // contraction) is >= j, found by bisection over the fp32 bit patterns of [0, 1] (the decision
+    // is monotone there) with glibc 2.35's acosf / cbrtf.
     // tests/test_capi_cpu.py checks EVERY fp32 cos theta in [0, 1] against the oracle's fp32
     // decision on the libm the tests run on (a libm whose decision moves fails that test).
     static const std::array<float, kNbSunSegments> z = {{
@@ -540,6 +530,10 @@ const std::array<float, kNbSunSegments>& sun_segment_thresholds() {
     return z;
 }
 
+// Index returned by the kernels' discrete_sample_reuse for s = value * sum:
+// JIT, the prefix count of ((cdf < s) || cdf == 0) && cdf != sum over [0, n-1)
+// (distr_1d.h:116-136); scalar, first + #{i in [first, last) : cdf[i] < s}.
+// Both are monotone in s (cdf is non-decreasing).
 int SunskyModel::gauss_search(float s) const {
     if (semantics_ == kJit) {
         int idx = 0;

@@ -32,11 +32,9 @@ struct EvalTangent {
     float dsun_local[3] = {0, 0, 0};   // d local sun direction (sun_direction)
 };
 
-// render_sun's elevation segment (sunsky.cpp:579-584) in fp32 as the reference forms it:
-// min(floor(cbrt(2 (pi/2 - acos z) / pi) 45), 44), libm acosf / cbrtf, no contraction.
-int reference_sun_segment(float cos_theta);
-// SunskyKArgs::sun_seg_z: [j] = the smallest fp32 cos theta in [0, 1] whose
-// reference_sun_segment is >= j ([0] = 0); committed constants (sunsky_model.cpp).
+// SunskyKArgs::sun_seg_z: [j] = the smallest fp32 cos theta in [0, 1] whose render_sun
+// elevation segment (sunsky.cpp:579-584, fp32: min(floor(cbrt(2 (pi/2 - acos z) / pi) 45), 44))
+// is >= j ([0] = 0); committed constants (sunsky_model.cpp).
 const std::array<float, kNbSunSegments>& sun_segment_thresholds();
 
 class SunskyModel {

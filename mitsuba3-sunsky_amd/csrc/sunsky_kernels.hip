@@ -406,7 +406,10 @@ __device__ __forceinline__ SunDisc64 sun_disc64(const SunskyKArgs& K, float wx, 
     d.pos = sun_segment_index(K, cos_theta);
     const double frac = (double)d.pos * (1.0 / (double)kNbSunSegments);
     d.x = (double)elevation_fast(cos_theta) - 1.5707963267948966 * (frac * frac * frac);
-    const double vx = (double)(wx - K.sun_n[0]), vy = (double)(wy - K.sun_n[1]), vz = (double)(cos_theta - K.sun_n[2]);
+    // v = wo - n in fp64: exact for any aperture (in fp32 only next to the sun, where the
+    // components' differences are exact; a 12 deg disc lost 1e-4 at its limb to the rounding)
+    const double vx = (double)wx - (double)K.sun_n[0], vy = (double)wy - (double)K.sun_n[1],
+                 vz = (double)cos_theta - (double)K.sun_n[2];
     const double v2 = fma(vz, vz, fma(vy, vy, vx * vx));
     const double inv = (double)K.cpsi_inv_hi + (double)K.cpsi_inv_lo;
     d.cpsi = sqrt(fmax(fma(-inv, v2 * fma(-0.25, v2, 1.0), 1.0), 0.0));

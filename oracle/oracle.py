@@ -306,20 +306,20 @@ class Oracle:
 
     def adopt_tables(self, em):
         """Evaluate on the product's own staged fp32 tables (sky coefficients, sky radiance,
-        sun table, limb darkening), its fp32 local sun direction and disc cutoff, with the
-        fp32 segment decision: with precision 'f64', the exact value of what the kernels
-        compute from their inputs, so GPU - this is the kernels' arithmetic error alone.
-        em: a sunsky_amd emitter."""
+        sun table, limb darkening), its fp32 local sun direction, disc cutoff and disc area
+        ratio, with the fp32 segment decision: with precision 'f64', the exact value of what
+        the kernels compute from their inputs, so GPU - this is the kernels' arithmetic error
+        alone.  em: a sunsky_amd emitter."""
         t = [np.ascontiguousarray(em.table(k), dtype=np.float32)
              for k in ("sky_params", "sky_radiance", "sun_radiance", "sun_ld")]
         inf = em.info()
         sun = np.ascontiguousarray(inf["sun_dir_local"], dtype=np.float32)
         f = self._fn("adopt_tables")
-        f.argtypes = [C.c_void_p] + [C.c_void_p, C.c_size_t] * 4 + [C.c_void_p, C.c_float]
+        f.argtypes = [C.c_void_p] + [C.c_void_p, C.c_size_t] * 4 + [C.c_void_p, C.c_float, C.c_float]
         args = []
         for a in t:
             args += [_ptr(a), a.size]
-        if f(self._h, *args, _ptr(sun), C.c_float(inf["cos_cutoff"])) != 0:
+        if f(self._h, *args, _ptr(sun), C.c_float(inf["cos_cutoff"]), C.c_float(inf["area_ratio"])) != 0:
             raise ValueError(lib().oracle_last_error().decode())
 
     def hw_sun_radiance(self, turbidity, wavelength, elevation, gamma):

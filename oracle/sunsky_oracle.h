@@ -118,7 +118,8 @@ void oracle_sun_coordinates(int year, int month, int day, float hour, float minu
     int oracle_adopt_tables_##SFX(oracle_##SFX *o, const float *sky_params, size_t n_sky,        \
                            const float *sky_rad, size_t n_rad, const float *sun_rad,             \
                            size_t n_sun, const float *sun_ld, size_t n_ld,                       \
-                           const float *sun_local /* NULL: keep */, float cos_cutoff);          \
+                           const float *sun_local /* NULL: keep */, float cos_cutoff,           \
+                           float area_ratio /* < 0: keep */);                                   \
     /* HW solar radiance (restates ArHosekSkyModel.c:686-784 on the packed tables) */          \
     R oracle_hw_sun_radiance_##SFX(const oracle_##SFX *o, R turbidity, R wavelength,            \
                            R elevation, R gamma);                                                \

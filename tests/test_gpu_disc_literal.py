@@ -167,3 +167,29 @@ def test_fast_bake_disc_pixels_match_eval():
         assert disc.sum() > 100
         rel = np.abs(img[:, disc] - ref[:, disc]) / np.abs(ref[:, disc])
         assert rel.max() < 1e-4, rel.max()
+
+
+# Beyond the five positions above: the sun at the zenith and just above the horizon (the disc
+# then spans the elevation range where the segment index and the horizon mask change), and
+# wider apertures (more disc lanes, cos psi over a wider chord range).
+EXTRA = [(89.0, 3.0, 0.5358), (0.6, 4.0, 0.5358), (20.0, 2.5, 5.0), (60.0, 7.0, 12.0)]
+
+
+@pytest.mark.parametrize("elev,turb,aperture", EXTRA)
+def test_fast_eval_disc_lanes_literal_bar_extremes(elev, turb, aperture):
+    """RGB eval and the C3 node kernel at the extra sun positions / apertures."""
+    base = angles_dict(turb, 0.3, np.deg2rad(90 - elev), 0.2, 1.0, 1.0, sun_aperture=aperture)
+    for variant in ("rgb", "spectral"):
+        em = ss.SunskyEmitter(base, variant, precision="fast")
+        o32, o64t, o64 = oracles(base, variant, em)
+        inf = o32.info()
+        wo = disc_heavy_wo(inf, 4096, seed=int(elev * 10) + 11)
+        disc = (wo @ inf["sun_dir_local"].astype(np.float32) >= np.float32(inf["cos_cutoff"])) & (wo[:, 2] >= 0)
+        if variant == "rgb":
+            out = host(em.eval(ss.SurfaceInteraction3f(wi=soa(-wo)))).T
+            check(out, o32.eval(-wo), o64t.eval(-wo), o64.eval(-wo), disc, f"rgb {elev} deg ap {aperture}")
+        else:
+            lam = np.repeat(np.asarray(NODES, np.float32)[:, None], wo.shape[0], 1)
+            out = host(em.eval_spectral_broadcast(soa(-wo), NODES))
+            check(out.T, o32.eval(-wo, lam).T, o64t.eval(-wo, lam).T, o64.eval(-wo, lam).T, disc,
+                  f"nodes {elev} deg ap {aperture}")

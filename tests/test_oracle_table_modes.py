@@ -36,6 +36,7 @@ def test_rounded_and_adopted_tables(variant, elev, turb):
     em = ss.SunskyEmitter(d, variant=variant, device="host")
     assert np.array_equal(o64t.info()["sun_dir_local"], em.info()["sun_dir_local"].astype(np.float64))
     assert o64t.info()["cos_cutoff"] == np.float64(np.float32(em.info()["cos_cutoff"]))
+    assert o64t.info()["area_ratio"] == np.float64(np.float32(em.info()["area_ratio"]))
     assert (np.abs(t - r) / np.maximum(np.abs(r), 1e-30)).max() < 2e-5
     # sky lanes: the sky formula on the same tables, at fp32 level in every mode
     ct = np.linspace(0.05, 1, 8)
@@ -50,3 +51,24 @@ def test_adopt_tables_rejects_the_wrong_variant():
     o64 = O.Oracle(d, "rgb", "jit", "f64")
     with pytest.raises(ValueError):
         o64.adopt_tables(ss.SunskyEmitter(d, variant="spectral", device="host"))
+
+
+def test_adopted_area_ratio_away_from_the_default_aperture():
+    """get_area_ratio (sunsky.h:99-101) in fp32 cancels in 1 - cos(half aperture): at a 5 deg
+    aperture the fp32 staged ratio is ~2e-3 from the fp64 one, a scale of the whole disc term.
+    The adopting oracle takes the staged ratio, so its disc lanes follow the fp32 oracle's
+    scale (and the kernels', which are given that ratio)."""
+    d = angles_dict(2.5, 0.3, np.deg2rad(70), 0.2, 1.0, 1.0, sun_aperture=5.0)
+    o32 = O.Oracle(d, "rgb", "jit", "f32")
+    d64 = fp32_sun_input(d, o32)
+    o64 = O.Oracle(d64, "rgb", "jit", "f64")
+    o64t = O.Oracle(d64, "rgb", "jit", "f64")
+    o64t.adopt_tables(ss.SunskyEmitter(d, variant="rgb", device="host"))
+    assert abs(o64.info()["area_ratio"] / o32.info()["area_ratio"] - 1) > 1e-3
+    wo = _disc_dirs(o32, 2048, seed=4)
+    a, b, t = o32.eval(-wo), o64.eval(-wo), o64t.eval(-wo)
+    inside = (b > 0).all(axis=1)
+    assert inside.sum() > 1000
+    rel = lambda x, y: (np.abs(x - y) / np.abs(y))[inside].max()
+    assert rel(b, a) > 1e-3            # fp32 vs fp64: the ratio's cancellation
+    assert rel(t, a) < 2e-5            # the adopted ratio: fp32 arithmetic only

@@ -5,7 +5,8 @@ The shipped `mitsuba3-sunsky_amd/csrc/sunsky_kernels.hip` holds no probe code.  
 (cost ablation, compute-only build, layout experiment) is a list of textual edits applied
 here to a copy of it in tools/build/, which is then compiled to tools/build/probe_<name>.hsaco
 for tools/gpu_ab.sh / kbench.  An edit whose anchor is missing fails loudly, so a probe
-never silently measures the unmodified product.
+never silently measures the unmodified product.  Probes whose anchors a later change removed
+are dropped from the table (their A/B logs stay in profiles/, their edits in git history).
 
 usage: python tools/mk_probe.py <name> [--src FILE]   (tools/Makefile: make build/probe_<name>.hsaco)
 """
@@ -20,48 +21,6 @@ CSRC = os.path.join(ROOT, "mitsuba3-sunsky_amd", "csrc")
 
 # name -> [(anchor, replacement)]: each anchor must occur exactly once in the product source
 PROBES = {
-    # round 6 fp64 disc fix-up variants (A/B against the product build)
-    "rgb_jbarrier": [("""            float o[3];
-            if constexpr (FAST) {
-                bool h;""", """            float o[3];
-            if constexpr (FAST) {
-                __builtin_amdgcn_sched_barrier(0);
-                bool h;""")],
-    "rays_nofix": [("""        // FAST: the disc lanes again with the fp64 disc term (fixup_rgb_disc)
-        if (FAST && any_sun) {""", """        if (false && FAST && any_sun) {""")],
-    "rays_noinline_fix": [("""        // FAST: the disc lanes again with the fp64 disc term (fixup_rgb_disc)
-        if (FAST && any_sun) {
-#pragma unroll 1
-            for (int j = 0; j < VEC; ++j) {""", """        // FAST: the disc lanes again with the fp64 disc term (fixup_rgb_disc)
-        if (FAST && any_sun) fixup_rays_noinline<VEC, FAST, NEG>(K, chans, wx, wy, wz, active, i, lam, lstride, nlam, out, ostride);
-        if (false) {
-#pragma unroll 1
-            for (int j = 0; j < VEC; ++j) {"""),
-        ("""// ======================================================================
-// eval(): spectral with per-ray wavelengths (Mitsuba Spectrum<Float, k>):""", """template <int VEC, bool FAST, bool NEG>
-__device__ __noinline__ void fixup_rays_noinline(const SunskyKArgs& K, const typename ChanSel<FAST>::T* chans,
-    const float* __restrict__ wx, const float* __restrict__ wy, const float* __restrict__ wz, const uint8_t* __restrict__ active,
-    size_t i, const float* __restrict__ lam, size_t lstride, int nlam, float* __restrict__ out, size_t ostride) {
-#pragma unroll 1
-    for (int j = 0; j < VEC; ++j) {
-        const size_t q = i + j;
-        const DirTerms tj = refetch_terms<NEG>(K, wx, wy, wz, active, q);
-        if (!tj.hit_sun) continue;
-        const SunDisc64 d = sun_disc64(K, tj.wx, tj.wy, tj.cos_theta);
-#pragma unroll 1
-        for (int k = 0; k < nlam; ++k)
-            out[(size_t)k * ostride + q] = eval_spec_one_flat<FAST, kSunF64>(K, chans, K.sun_table, K.sun_ld, tj,
-                                                                              lam[(size_t)k * lstride + q], &d, &K);
-    }
-}
-
-// ======================================================================
-// eval(): spectral with per-ray wavelengths (Mitsuba Spectrum<Float, k>):""")],
-    # VERDICT r05 next 1: the node kernel with the next step's directions loaded before this
-    # step's 11 stores (vmcnt counts loads and stores in order: a load issued after the stores
-    # waits for them); rolled channel loop / unrolled with a scheduling barrier per channel
-    "nodes_pf": [('    const size_t nvec = n / VEC, G = span_steps(nvec);\n    {\n#pragma unroll 1\n      for (size_t g = 0; g < G; ++g) {', '    const size_t nvec = n / VEC, G = span_steps(nvec);\n    {\n      float px_[VEC], py_[VEC], pz_[VEC];\n      bool pm_[VEC];\n#pragma unroll 1\n      for (size_t g = 0; g < G; ++g) {'), ("        const size_t v = ((size_t)blockIdx.x * G + g) * blockDim.x + threadIdx.x;\n        if (v >= nvec) break;\n        const size_t i = v * VEC;\n        float x[VEC], y[VEC], z[VEC];\n        bool m[VEC];\n        load_dirs<VEC>(wx, wy, wz, active, i, x, y, z, m);\n        DirTerms t[VEC];\n        bool any_sun = false;\n#pragma unroll\n        for (int j = 0; j < VEC; ++j) {\n            t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);\n            any_sun |= t[j].hit_sun;\n        }\n        if (any_sun) {\n#pragma unroll\n            for (int j = 0; j < VEC; ++j) add_sun_terms<FAST>(K, t[j]);\n        }\n        // Rolled: one channel's constants (LDS broadcast reads) live at a time;\n        // unrolling lets the compiler hoist all 110 out of the ray loop (184 VGPRs).\n#pragma unroll 1\n        for (int c = 0; c < kNbWavelengths; ++c) {", "        const size_t v = ((size_t)blockIdx.x * G + g) * blockDim.x + threadIdx.x;\n        if (v >= nvec) break;\n        const size_t i = v * VEC;\n        if (g == 0) load_dirs<VEC>(wx, wy, wz, active, i, px_, py_, pz_, pm_);\n        DirTerms t[VEC];\n        bool any_sun = false;\n#pragma unroll\n        for (int j = 0; j < VEC; ++j) {\n            t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(px_[j], py_[j], pz_[j])), pm_[j]);\n            any_sun |= t[j].hit_sun;\n        }\n        // the next step's directions, issued before this step's stores\n        if (g + 1 < G && v + blockDim.x < nvec) load_dirs<VEC>(wx, wy, wz, active, i + (size_t)blockDim.x * VEC, px_, py_, pz_, pm_);\n        if (any_sun) {\n#pragma unroll\n            for (int j = 0; j < VEC; ++j) add_sun_terms<FAST>(K, t[j]);\n        }\n#pragma unroll 1\n        for (int c = 0; c < kNbWavelengths; ++c) {\n            ")],
-    "nodes_pf_unroll": [('    const size_t nvec = n / VEC, G = span_steps(nvec);\n    {\n#pragma unroll 1\n      for (size_t g = 0; g < G; ++g) {', '    const size_t nvec = n / VEC, G = span_steps(nvec);\n    {\n      float px_[VEC], py_[VEC], pz_[VEC];\n      bool pm_[VEC];\n#pragma unroll 1\n      for (size_t g = 0; g < G; ++g) {'), ("        const size_t v = ((size_t)blockIdx.x * G + g) * blockDim.x + threadIdx.x;\n        if (v >= nvec) break;\n        const size_t i = v * VEC;\n        float x[VEC], y[VEC], z[VEC];\n        bool m[VEC];\n        load_dirs<VEC>(wx, wy, wz, active, i, x, y, z, m);\n        DirTerms t[VEC];\n        bool any_sun = false;\n#pragma unroll\n        for (int j = 0; j < VEC; ++j) {\n            t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(x[j], y[j], z[j])), m[j]);\n            any_sun |= t[j].hit_sun;\n        }\n        if (any_sun) {\n#pragma unroll\n            for (int j = 0; j < VEC; ++j) add_sun_terms<FAST>(K, t[j]);\n        }\n        // Rolled: one channel's constants (LDS broadcast reads) live at a time;\n        // unrolling lets the compiler hoist all 110 out of the ray loop (184 VGPRs).\n#pragma unroll 1\n        for (int c = 0; c < kNbWavelengths; ++c) {", "        const size_t v = ((size_t)blockIdx.x * G + g) * blockDim.x + threadIdx.x;\n        if (v >= nvec) break;\n        const size_t i = v * VEC;\n        if (g == 0) load_dirs<VEC>(wx, wy, wz, active, i, px_, py_, pz_, pm_);\n        DirTerms t[VEC];\n        bool any_sun = false;\n#pragma unroll\n        for (int j = 0; j < VEC; ++j) {\n            t[j] = dir_terms<FAST>(K, to_local(K, flip3<NEG>(px_[j], py_[j], pz_[j])), pm_[j]);\n            any_sun |= t[j].hit_sun;\n        }\n        // the next step's directions, issued before this step's stores\n        if (g + 1 < G && v + blockDim.x < nvec) load_dirs<VEC>(wx, wy, wz, active, i + (size_t)blockDim.x * VEC, px_, py_, pz_, pm_);\n        if (any_sun) {\n#pragma unroll\n            for (int j = 0; j < VEC; ++j) add_sun_terms<FAST>(K, t[j]);\n        }\n#pragma unroll \n        for (int c = 0; c < kNbWavelengths; ++c) {\n            __builtin_amdgcn_sched_barrier(0);")],
     # compute-only: every global store suppressed (kept live by an impossible compare), for
     # the roofline splits of DESIGN.md §3
     "nostore": [
@@ -97,24 +56,6 @@ __device__ __noinline__ void fixup_rays_noinline(const SunskyKArgs& K, const typ
                 npy[r] = 0.f;
                 npz[r] = 0.f;
 """)],
-    "pos_nostore": [("""                    if (dist) store_nt(dd, dist + i);
-                    if (opx) { store_nt(fmaf(d.x, dd, itp.x), opx + i); store_nt(fmaf(d.y, dd, itp.y), opy + i); store_nt(fmaf(d.z, dd, itp.z), opz + i); }
-""", """                    const float s_ = fmaf(d.x, dd, itp.x) + fmaf(d.y, dd, itp.y) + fmaf(d.z, dd, itp.z);
-                    if (dist && s_ == -1234.5f) store_nt(dd, dist + i);
-""")],
-    # the wave-sorted RGB kernels' un-sort stores as plain stores: ds.dist / ds.p only, or all planes
-    "sorted_plain_pos": [("""                    if (dist) store_nt(dd, dist + i);
-                    if (opx) { store_nt(fmaf(d.x, dd, itp.x), opx + i); store_nt(fmaf(d.y, dd, itp.y), opy + i); store_nt(fmaf(d.z, dd, itp.z), opz + i); }
-                }""", """                    if (dist) dist[i] = dd;
-                    if (opx) { opx[i] = fmaf(d.x, dd, itp.x); opy[i] = fmaf(d.y, dd, itp.y); opz[i] = fmaf(d.z, dd, itp.z); }
-                }""")],
-    "sorted_plain_all": [("""                    if (dist) store_nt(dd, dist + i);
-                    if (opx) { store_nt(fmaf(d.x, dd, itp.x), opx + i); store_nt(fmaf(d.y, dd, itp.y), opy + i); store_nt(fmaf(d.z, dd, itp.z), opz + i); }
-                }""", """                    if (dist) dist[i] = dd;
-                    if (opx) { opx[i] = fmaf(d.x, dd, itp.x); opy[i] = fmaf(d.y, dd, itp.y); opz[i] = fmaf(d.z, dd, itp.z); }
-                }"""),
-        ("""                for (int k = 0; k < 7; ++k) store_nt(Y[k][slot[r]], planes[k] + i);""",
-         """                for (int k = 0; k < 7; ++k) planes[k][i] = Y[k][slot[r]];""")],
     # the spectral general call with it.p prefetched one window ahead (as the RGB kSortPos) instead
     # of read at the store stage: +3 R VGPRs over the passes
     "spec_pos_prefetch": [
@@ -199,27 +140,6 @@ __device__ __noinline__ void fixup_rays_noinline(const SunskyKArgs& K, const typ
         if (v >= nvec) break;
         const size_t i = v * VEC;
         float x[VEC], y[VEC], z[VEC], r[VEC], g[VEC], b[VEC];""")],
-    # the per-ray spectral eval's and the node kernel's grid-stride loops (the split before round 5), for A/B
-    "evals_gridstride": [
-        ("""    if constexpr (NL > 0) nlam = NL;
-    const size_t nvec = n / VEC, G = span_steps(nvec);
-    for (size_t gs = 0; gs < G; ++gs) {
-        const size_t v = ((size_t)blockIdx.x * G + gs) * blockDim.x + threadIdx.x;
-        if (v >= nvec) break;""",
-         """    if constexpr (NL > 0) nlam = NL;
-    const size_t nvec = n / VEC;
-    for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (size_t)gridDim.x * blockDim.x) {"""),
-        ("""    const size_t nvec = n / VEC, G = span_steps(nvec);
-    {
-#pragma unroll 1
-      for (size_t g = 0; g < G; ++g) {
-        const size_t v = ((size_t)blockIdx.x * G + g) * blockDim.x + threadIdx.x;
-        if (v >= nvec) break;""",
-         """    const size_t nvec = n / VEC;
-    {
-#pragma unroll 1
-      for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (size_t)gridDim.x * blockDim.x) {"""),
-    ],
 }
 
 

@@ -72,3 +72,22 @@ def test_adopted_area_ratio_away_from_the_default_aperture():
     rel = lambda x, y: (np.abs(x - y) / np.abs(y))[inside].max()
     assert rel(b, a) > 1e-3            # fp32 vs fp64: the ratio's cancellation
     assert rel(t, a) < 2e-5            # the adopted ratio: fp32 arithmetic only
+
+
+def test_staged_sun_state_is_the_fp32_references_bit_for_bit():
+    """What o64t adopts beyond the tables -- the local sun direction, the disc cutoff and the disc
+    area ratio -- is the fp32 reference restatement's own staged state, bit for bit
+    (dr::normalize of the fp32 sun_direction and the fp32 frame, sunsky.cpp:923, sunsky.h:99-101),
+    over random sun positions, turbidities and apertures: the disc lanes' distance from fp64
+    that the staging owns is the reference's, not the product's."""
+    rng = np.random.default_rng(1)
+    for i in range(24):
+        el, ph, turb = rng.uniform(0.2, 89.8), rng.uniform(0, 2 * np.pi), rng.uniform(1, 10)
+        ap = (0.5358, 1.0, 5.0, 12.0)[i % 4]
+        for variant in ("rgb", "spectral"):
+            d = angles_dict(turb, ph, np.deg2rad(90 - el), 0.3, 1.0, 1.0, sun_aperture=ap)
+            o = O.Oracle(d, variant, "jit", "f32").info()
+            e = ss.SunskyEmitter(d, variant=variant, device="host").info()
+            assert np.array_equal(np.float32(o["sun_dir_local"]), np.float32(e["sun_dir_local"])), (variant, el, ap)
+            assert np.float32(o["cos_cutoff"]) == np.float32(e["cos_cutoff"]), (variant, el, ap)
+            assert np.float32(o["area_ratio"]) == np.float32(e["area_ratio"]), (variant, el, ap)

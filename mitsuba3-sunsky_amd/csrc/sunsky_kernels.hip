@@ -381,8 +381,6 @@ __device__ __forceinline__ const SunskyKArgs& opaque_kargs(const SunskyKArgs& K)
     return *(&K + off);
 }
 
-// Direction q of a fix-up: its terms from K (the main pass's constants, live in SGPRs
-// already) -- the main pass's bits, disc test included.
 // ------------------------------------------------------------------ sun disc in fp64
 // The FAST eval kernels (eval, eval_direction, the spectral broadcast / node / per-ray kernels,
 // the lat-long bake) evaluate the sun-disc term of their rare disc lanes (~1e-5 of random
@@ -391,14 +389,14 @@ __device__ __forceinline__ const SunskyKArgs& opaque_kargs(const SunskyKArgs& K)
 // Near the limb cos psi = sqrt(1 - sin^2 gamma / sin^2(half aperture)) (sunsky.h:385-392)
 // has an unbounded derivative and the limb-darkening sum nearly cancels, so an fp32 Horner
 // there is off by up to 4.9e-5 (the reference's own fp32 by 1.5e-4); this branch holds the
-// literal 1e-5 against the fp64 evaluation of the staged tables
-// (tests/test_gpu_parity.py::test_fast_eval_disc_lanes_literal_bar).  The samplers keep the
+// literal 1e-5 against the fp64 evaluation of the staged fp32 state
+// (tests/test_gpu_disc_literal.py).  The samplers keep the
 // fp32 form (65 % of their lanes are sun picks, already within 1e-5 of fp64).
 struct SunDisc64 {
     int pos;     // render_sun's segment: the reference's fp32 decision (sun_segment_index)
     double x;    // elevation - pi/2 (pos / 45)^3: the fp32 elevation (elevation_fast, 0.7 ulp;
                  // x enters the polynomial smoothly), the segment start in fp64
-    double cpsi; // compute_cos_psi from the fp32 chord v = wo - n (exact next to the sun)
+    double cpsi; // compute_cos_psi from the chord v = wo - n formed in fp64 (exact)
 };
 
 __device__ __forceinline__ SunDisc64 sun_disc64(const SunskyKArgs& K, float wx, float wy, float cos_theta) {
